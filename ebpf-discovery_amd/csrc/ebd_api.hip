@@ -1,0 +1,834 @@
+// ebd_api.hip — the C ABI (include/ebpf_discovery_amd.h): context, device buffers and the
+// per-batch pipeline of ebd_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "ebd_device.h"
+#include "ebd_fresh.h"
+
+namespace ebd {
+hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_carry_insert(const Dev& d, hipStream_t st);
+hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
+hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
+hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
+hipError_t launch_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt, hipStream_t st);
+hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
+		unsigned long long* alen, hipStream_t st);
+hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, EventRec* ev,
+		uint32_t* len, const unsigned long long* off, uint8_t* payload, hipStream_t st);
+void build_gen_tables(GenTables* T);
+} // namespace ebd
+
+using namespace ebd;
+
+#define HIP_TRY(x)                                                                                                   \
+	do {                                                                                                             \
+		hipError_t e_ = (x);                                                                                         \
+		if (e_ != hipSuccess) {                                                                                      \
+			std::fprintf(stderr, "ebd: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+			return -EIO;                                                                                             \
+		}                                                                                                            \
+	} while (0)
+
+static uint32_t next_pow2(uint64_t v) {
+	uint64_t p = 1;
+	while (p < v)
+		p <<= 1;
+	return p > 0x80000000ull ? 0x80000000u : (uint32_t)p;
+}
+
+struct ebd_ctx {
+	std::mutex mu;
+	int device = 0;
+	int cus = 256;
+	hipStream_t stream = nullptr;
+	ebd_config cfg{};
+	// tables
+	DfaTable* dfa_host = nullptr;
+	KeyTrie trie_host{};
+	Interfaces ifs_host{};
+	uint8_t* d_dfa = nullptr;
+	KeyTrie* d_trie = nullptr;
+	Interfaces* d_ifs = nullptr;
+	GenTables* d_gen = nullptr;
+	// services
+	Slot* d_slots = nullptr;
+	uint32_t slot_cap = 0;
+	uint32_t* d_new_slots = nullptr;
+	uint32_t new_cap = 0;
+	uint8_t* d_sarena = nullptr;
+	uint64_t sarena_cap = 0;
+	// per-batch
+	uint32_t max_events = 0;
+	ebd_event_result* d_res = nullptr;
+	Hash128* d_keys = nullptr;
+	SSlot* d_sset = nullptr;
+	uint32_t sset_cap = 0;
+	uint32_t* d_dirty = nullptr;
+	unsigned long long* d_slow[2] = {nullptr, nullptr};
+	void* d_sort_tmp = nullptr;
+	size_t sort_tmp_bytes = 0;
+	Carry* d_carry[2] = {nullptr, nullptr};
+	int carry_cur = 0;
+	uint32_t n_carry = 0;
+	uint32_t carry_cap = 0;
+	SessReq* d_sreq = nullptr;
+	uint8_t* d_sstr = nullptr;
+	uint64_t sstr_cap = 0;
+	unsigned long long* d_ctr = nullptr;
+	unsigned long long* h_ctr = nullptr; // pinned
+	unsigned long long* d_cnt = nullptr;
+	ebd_service* d_collect = nullptr;
+	// host-batch staging
+	EventRec* d_ev = nullptr;
+	uint32_t* d_len = nullptr;
+	uint64_t* d_off = nullptr;
+	uint8_t* d_payload = nullptr;
+	uint64_t payload_cap = 0;
+	// bookkeeping
+	unsigned long long seq_base = 0;
+	uint32_t last_n = 0;
+	uint64_t last_sreq = 0, last_sstr = 0;
+	int last_slow_ran = 0;
+	uint64_t events_total = 0;
+	uint64_t max_live = 0;
+	// EBD_CFG_TIMING: event pairs around each launch, summed lazily
+	struct Timed {
+		int kernel;
+		hipEvent_t a, b;
+	};
+	std::vector<Timed> pending;
+	std::vector<hipEvent_t> free_events;
+	double kt_ms[16] = {0};
+	uint64_t kt_n[16] = {0};
+};
+
+static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
+		"k_agg_fast", "k_reps", "k_sset_clear"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_N };
+
+static hipEvent_t take_event(ebd_ctx* c) {
+	if (!c->free_events.empty()) {
+		hipEvent_t e = c->free_events.back();
+		c->free_events.pop_back();
+		return e;
+	}
+	hipEvent_t e = nullptr;
+	(void)hipEventCreate(&e);
+	return e;
+}
+
+// Runs `launch` on the context stream, bracketed by HIP events when timing is on.
+template <typename F>
+static hipError_t timed(ebd_ctx* c, int kernel, F launch) {
+	if (!(c->cfg.flags & EBD_CFG_TIMING))
+		return launch();
+	hipEvent_t a = take_event(c), b = take_event(c);
+	(void)hipEventRecord(a, c->stream);
+	hipError_t e = launch();
+	(void)hipEventRecord(b, c->stream);
+	c->pending.push_back({kernel, a, b});
+	return e;
+}
+
+static void drain_timing(ebd_ctx* c) {
+	for (auto& t : c->pending) {
+		float ms = 0.f;
+		if (hipEventSynchronize(t.b) == hipSuccess && hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+			c->kt_ms[t.kernel] += ms;
+			c->kt_n[t.kernel]++;
+		}
+		c->free_events.push_back(t.a);
+		c->free_events.push_back(t.b);
+	}
+	c->pending.clear();
+}
+
+static Dev make_dev(ebd_ctx* c) {
+	Dev d{};
+	d.dfa = c->d_dfa;
+	d.di = c->dfa_host->info;
+	d.trie = c->d_trie;
+	d.ifs = c->d_ifs;
+	d.res = c->d_res;
+	d.keys = c->d_keys;
+	d.slots = c->d_slots;
+	d.slot_mask = c->slot_cap - 1;
+	d.new_slots = c->d_new_slots;
+	d.new_cap = c->new_cap;
+	d.sarena = c->d_sarena;
+	d.sarena_cap = c->sarena_cap;
+	d.sset = c->d_sset;
+	d.sset_mask = c->sset_cap - 1;
+	d.dirty = c->d_dirty;
+	d.slow_keys = c->d_slow[0];
+	d.carry_in = c->d_carry[c->carry_cur];
+	d.n_carry_in = c->n_carry;
+	d.carry_out = c->d_carry[c->carry_cur ^ 1];
+	d.carry_cap = c->carry_cap;
+	d.sreq = c->d_sreq;
+	d.sstr = c->d_sstr;
+	d.sstr_cap = c->sstr_cap;
+	d.ctr = c->d_ctr;
+	d.seq_base = c->seq_base;
+	return d;
+}
+
+static void ctx_free(ebd_ctx* c) {
+	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_sarena, c->d_res, c->d_keys,
+			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload};
+	for (void* p : ptrs)
+		if (p)
+			(void)hipFree(p);
+	if (c->h_ctr)
+		(void)hipHostFree(c->h_ctr);
+	for (auto& t : c->pending) {
+		(void)hipEventDestroy(t.a);
+		(void)hipEventDestroy(t.b);
+	}
+	for (auto e : c->free_events)
+		(void)hipEventDestroy(e);
+	if (c->stream)
+		(void)hipStreamDestroy(c->stream);
+	delete c->dfa_host;
+	delete c;
+}
+
+extern "C" {
+
+const char* ebd_strerror(int err) {
+	switch (-err) {
+	case 0: return "success";
+	case EINVAL: return "invalid argument";
+	case ENOMEM: return "out of device memory";
+	case EIO: return "HIP runtime error";
+	case ENOSPC: return "capacity exceeded";
+	case ENODEV: return "no HIP device";
+	default: return "unknown error";
+	}
+}
+
+int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
+	if (!cfg || !out || cfg->max_events == 0)
+		return -EINVAL;
+	*out = nullptr;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+		return -ENODEV;
+	if (cfg->device < 0 || cfg->device >= ndev)
+		return -EINVAL;
+	ebd_ctx* c = new ebd_ctx();
+	c->cfg = *cfg;
+	c->device = cfg->device;
+	c->max_events = cfg->max_events;
+	if (hipSetDevice(c->device) != hipSuccess) {
+		ctx_free(c);
+		return -EIO;
+	}
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+		c->cus = prop.multiProcessorCount;
+	int rc = 0;
+	auto fail = [&](int r) {
+		ctx_free(c);
+		return r;
+	};
+#define CTX_TRY(x)                                                                                                   \
+	do {                                                                                                             \
+		hipError_t e_ = (x);                                                                                         \
+		if (e_ != hipSuccess) {                                                                                      \
+			std::fprintf(stderr, "ebd: %s failed: %s\n", #x, hipGetErrorString(e_));                               \
+			return fail(e_ == hipErrorOutOfMemory ? -ENOMEM : -EIO);                                                 \
+		}                                                                                                            \
+	} while (0)
+	CTX_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	// tables derived from the parser semantics (ebd_spec.h)
+	build_key_trie(&c->trie_host);
+	c->dfa_host = new DfaTable();
+	rc = build_dfa(&c->trie_host, c->dfa_host);
+	if (rc != 0) {
+		std::fprintf(stderr, "ebd: DFA construction failed (%d)\n", rc);
+		return fail(-EIO);
+	}
+	const size_t tbytes = (size_t)c->dfa_host->info.nstates * 256;
+	CTX_TRY(hipMalloc(&c->d_dfa, tbytes));
+	CTX_TRY(hipMemcpy(c->d_dfa, c->dfa_host->next, tbytes, hipMemcpyHostToDevice));
+	CTX_TRY(hipMalloc(&c->d_trie, sizeof(KeyTrie)));
+	CTX_TRY(hipMemcpy(c->d_trie, &c->trie_host, sizeof(KeyTrie), hipMemcpyHostToDevice));
+	std::memset(&c->ifs_host, 0, sizeof(Interfaces));
+	CTX_TRY(hipMalloc(&c->d_ifs, sizeof(Interfaces)));
+	CTX_TRY(hipMemcpy(c->d_ifs, &c->ifs_host, sizeof(Interfaces), hipMemcpyHostToDevice));
+	// service table
+	c->slot_cap = next_pow2(cfg->service_capacity ? cfg->service_capacity : (1u << 22));
+	CTX_TRY(hipMalloc(&c->d_slots, (size_t)c->slot_cap * sizeof(Slot)));
+	CTX_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
+	c->new_cap = c->max_events < c->slot_cap ? c->max_events : c->slot_cap;
+	CTX_TRY(hipMalloc(&c->d_new_slots, (size_t)c->new_cap * sizeof(uint32_t)));
+	c->sarena_cap = cfg->string_arena ? cfg->string_arena : (256ull << 20);
+	CTX_TRY(hipMalloc(&c->d_sarena, c->sarena_cap));
+	// per-batch buffers
+	const uint64_t n = c->max_events;
+	CTX_TRY(hipMalloc(&c->d_res, n * sizeof(ebd_event_result)));
+	CTX_TRY(hipMalloc(&c->d_keys, n * sizeof(Hash128)));
+	const uint32_t lru = cfg->lru_capacity ? cfg->lru_capacity : EBD_MAX_SESSIONS;
+	c->carry_cap = lru;
+	c->sset_cap = next_pow2(2 * (n + lru));
+	CTX_TRY(hipMalloc(&c->d_sset, (size_t)c->sset_cap * sizeof(SSlot)));
+	CTX_TRY(hipMemsetAsync(c->d_sset, 0, (size_t)c->sset_cap * sizeof(SSlot), c->stream));
+	CTX_TRY(hipMalloc(&c->d_dirty, (n + lru) * sizeof(uint32_t)));
+	CTX_TRY(hipMalloc(&c->d_slow[0], n * sizeof(unsigned long long)));
+	CTX_TRY(hipMalloc(&c->d_slow[1], n * sizeof(unsigned long long)));
+	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
+			c->stream));
+	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes ? c->sort_tmp_bytes : 16));
+	CTX_TRY(hipMalloc(&c->d_carry[0], (size_t)lru * sizeof(Carry)));
+	CTX_TRY(hipMalloc(&c->d_carry[1], (size_t)lru * sizeof(Carry)));
+	CTX_TRY(hipMalloc(&c->d_sreq, n * sizeof(SessReq)));
+	c->sstr_cap = n * 160;
+	if (c->sstr_cap < (64ull << 20))
+		c->sstr_cap = 64ull << 20;
+	if (c->sstr_cap > (4ull << 30))
+		c->sstr_cap = 4ull << 30;
+	CTX_TRY(hipMalloc(&c->d_sstr, c->sstr_cap));
+	CTX_TRY(hipMalloc(&c->d_ctr, CTR_COUNT * sizeof(unsigned long long)));
+	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_COUNT * sizeof(unsigned long long), c->stream));
+	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
+	CTX_TRY(hipHostMalloc(&c->h_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long), hipHostMallocDefault));
+	CTX_TRY(hipStreamSynchronize(c->stream));
+#undef CTX_TRY
+	*out = c;
+	return 0;
+}
+
+int ebd_ctx_destroy(ebd_ctx* c) {
+	if (!c)
+		return -EINVAL;
+	(void)hipSetDevice(c->device);
+	(void)hipStreamSynchronize(c->stream);
+	ctx_free(c);
+	return 0;
+}
+
+void* ebd_ctx_stream(ebd_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ebd_set_interfaces(ebd_ctx* c, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6) {
+	if (!c || n4 > 64 || n6 > 32 || (n4 && !v4) || (n6 && !v6))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	std::memset(&c->ifs_host, 0, sizeof(Interfaces));
+	c->ifs_host.n4 = n4;
+	c->ifs_host.n6 = n6;
+	for (uint32_t i = 0; i < n4; i++) {
+		std::memcpy(c->ifs_host.v4[i], v4[i].addr, 4);
+		std::memcpy(c->ifs_host.v4[i] + 4, v4[i].mask, 4);
+	}
+	for (uint32_t i = 0; i < n6; i++) {
+		std::memcpy(c->ifs_host.v6[i], v6[i].addr, 16);
+		std::memcpy(c->ifs_host.v6[i] + 16, v6[i].mask, 16);
+	}
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipMemcpyAsync(c->d_ifs, &c->ifs_host, sizeof(Interfaces), hipMemcpyHostToDevice, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const uint64_t* off, const uint8_t* payload,
+		uint32_t n) {
+	if (n > c->max_events)
+		return -EINVAL;
+	HIP_TRY(hipSetDevice(c->device));
+	Dev d = make_dev(c);
+	d.ev = ev;
+	d.len = len;
+	d.off = off;
+	d.payload = payload;
+	d.n = n;
+	c->last_n = n;
+	c->last_slow_ran = 0;
+	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_BATCH_END * sizeof(unsigned long long), c->stream));
+	if (n == 0) {
+		c->last_sreq = c->last_sstr = 0;
+		return 0;
+	}
+	if (c->n_carry)
+		HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_carry_insert(d, c->stream); }));
+	HIP_TRY(timed(c, KT_FRESH, [&] { return launch_fresh(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	const uint64_t nslow = c->h_ctr[CTR_SLOW];
+	if (nslow > 0) {
+		c->last_slow_ran = 1;
+		int end_bit = 32;
+		while ((1ull << (end_bit - 32)) < c->sset_cap)
+			end_bit++;
+		size_t bytes = c->sort_tmp_bytes;
+		HIP_TRY(timed(c, KT_SORT, [&] {
+			return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[0], c->d_slow[1], (int)nslow, 0,
+					end_bit, c->stream);
+		}));
+		d.slow_keys = c->d_slow[1];
+		HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk(d, (uint32_t)nslow, c->stream, c->cus); }));
+		if (c->n_carry)
+			HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
+	}
+	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_REPS, [&] { return launch_reps(d, c->stream, c->cus); }));
+	if (c->h_ctr[CTR_DIRTY])
+		HIP_TRY(timed(c, KT_SSET_CLEAR, [&] { return launch_sset_clear(d, c->stream, c->cus); }));
+	if (nslow > 0) {
+		HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		uint64_t co = c->h_ctr[CTR_CARRY_OUT];
+		c->n_carry = (uint32_t)(co < c->carry_cap ? co : c->carry_cap);
+		c->carry_cur ^= 1;
+		c->last_sreq = c->h_ctr[CTR_SREQ];
+		c->last_sstr = c->h_ctr[CTR_SSTR];
+		uint64_t bound = c->n_carry + c->h_ctr[CTR_INSERTS];
+		if (bound > c->max_live)
+			c->max_live = bound;
+	} else {
+		c->last_sreq = c->last_sstr = 0;
+	}
+	c->seq_base += n;
+	c->events_total += n;
+	return 0;
+}
+
+int ebd_submit_batch_device(ebd_ctx* c, const ebd_device_batch* b) {
+	if (!c || !b || (b->n && (!b->events || !b->len || !b->off || !b->payload)))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	return run_batch(c, (const EventRec*)b->events, b->len, b->off, b->payload, b->n);
+}
+
+int ebd_set_seq_base(ebd_ctx* c, uint64_t seq) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	c->seq_base = seq;
+	return 0;
+}
+
+int ebd_kernel_times(ebd_ctx* c, ebd_kernel_time* out, uint32_t cap, uint32_t* n) {
+	if (!c || !n)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	(void)hipSetDevice(c->device);
+	drain_timing(c);
+	*n = KT_N;
+	if (!out)
+		return 0;
+	if (cap < (uint32_t)KT_N)
+		return -ENOSPC;
+	for (int k = 0; k < KT_N; k++) {
+		std::memset(out[k].name, 0, sizeof(out[k].name));
+		std::strncpy(out[k].name, kKernelNames[k], sizeof(out[k].name) - 1);
+		out[k].launches = c->kt_n[k];
+		out[k].total_ms = c->kt_ms[k];
+	}
+	return 0;
+}
+
+int ebd_reset_kernel_times(ebd_ctx* c) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	(void)hipSetDevice(c->device);
+	drain_timing(c);
+	for (int k = 0; k < 16; k++) {
+		c->kt_ms[k] = 0;
+		c->kt_n[k] = 0;
+	}
+	return 0;
+}
+
+int ebd_sync(ebd_ctx* c) {
+	if (!c)
+		return -EINVAL;
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n) {
+	if (!c || (n && (!events || !len || !off || (!payload && payload_bytes))))
+		return -EINVAL;
+	if (n > c->max_events)
+		return -EINVAL;
+	for (uint32_t i = 0; i < n; i++) // buffers must lie inside the arena
+		if (len[i] != EBD_NO_BUFFER && (len[i] > EBD_BUFFER_MAX_DATA_SIZE || off[i] > payload_bytes || payload_bytes - off[i] < len[i]))
+			return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_ev) {
+		HIP_TRY(hipMalloc(&c->d_ev, (size_t)c->max_events * sizeof(EventRec)));
+		HIP_TRY(hipMalloc(&c->d_len, (size_t)c->max_events * sizeof(uint32_t)));
+		HIP_TRY(hipMalloc(&c->d_off, (size_t)c->max_events * sizeof(uint64_t)));
+	}
+	const uint64_t need = payload_bytes + 16;
+	if (need > c->payload_cap) {
+		if (c->d_payload)
+			HIP_TRY(hipFree(c->d_payload));
+		c->payload_cap = need < c->cfg.max_payload ? c->cfg.max_payload : need;
+		HIP_TRY(hipMalloc(&c->d_payload, c->payload_cap));
+	}
+	if (n) {
+		HIP_TRY(hipMemcpyAsync(c->d_ev, events, (size_t)n * sizeof(EventRec), hipMemcpyHostToDevice, c->stream));
+		HIP_TRY(hipMemcpyAsync(c->d_len, len, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+		HIP_TRY(hipMemcpyAsync(c->d_off, off, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+		if (payload_bytes)
+			HIP_TRY(hipMemcpyAsync(c->d_payload, payload, payload_bytes, hipMemcpyHostToDevice, c->stream));
+	}
+	int rc = run_batch(c, c->d_ev, c->d_len, c->d_off, c->d_payload, n);
+	if (rc)
+		return rc;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_fetch_results(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t* n) {
+	if (!c || !n || (cap && !out))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	*n = c->last_n;
+	if (cap < c->last_n)
+		return -ENOSPC;
+	HIP_TRY(hipSetDevice(c->device));
+	if (c->last_n)
+		HIP_TRY(hipMemcpyAsync(out, c->d_res, (size_t)c->last_n * sizeof(ebd_event_result), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+const ebd_event_result* ebd_results_device(ebd_ctx* c) { return c ? c->d_res : nullptr; }
+
+int ebd_fetch_session_requests(ebd_ctx* c, ebd_session_request* out, uint32_t cap, uint32_t* n, char* strings,
+		uint64_t strcap, uint64_t* strlen) {
+	if (!c || !n || !strlen)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	*n = (uint32_t)c->last_sreq;
+	*strlen = c->last_sstr < c->sstr_cap ? c->last_sstr : c->sstr_cap;
+	if (!out)
+		return 0;
+	if (cap < *n || strcap < *strlen)
+		return -ENOSPC;
+	HIP_TRY(hipSetDevice(c->device));
+	if (*n)
+		HIP_TRY(hipMemcpyAsync(out, c->d_sreq, (size_t)*n * sizeof(SessReq), hipMemcpyDeviceToHost, c->stream));
+	if (*strlen && strings)
+		HIP_TRY(hipMemcpyAsync(strings, c->d_sstr, *strlen, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n, char* strings, uint64_t strcap,
+		uint64_t* strlen) {
+	if (!c || !n || !strlen)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_collect)
+		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
+	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_collect(c->d_slots, c->slot_cap, c->d_collect, c->d_cnt, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	uint64_t used = c->h_ctr[CTR_SARENA];
+	if (used > c->sarena_cap)
+		used = c->sarena_cap;
+	const uint64_t cnt = c->h_ctr[CTR_COUNT];
+	*strlen = used;
+	*n = (uint32_t)cnt;
+	if (!out)
+		return 0;
+	if (cnt > cap || (used && (!strings || used > strcap)))
+		return -ENOSPC;
+	if (cnt)
+		HIP_TRY(hipMemcpyAsync(out, c->d_collect, cnt * sizeof(ebd_service), hipMemcpyDeviceToHost, c->stream));
+	if (used)
+		HIP_TRY(hipMemcpyAsync(strings, c->d_sarena, used, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_clear(ebd_ctx* c) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
+	if (!c || !s)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	std::memset(s, 0, sizeof(*s));
+	s->events = c->events_total;
+	s->requests = c->h_ctr[CTR_REQUESTS];
+	s->session_events = c->h_ctr[CTR_SESSION_EVENTS];
+	s->kernel_deletes = c->h_ctr[CTR_KDELETES];
+	s->live_sessions = c->n_carry;
+	s->max_live_sessions = c->max_live;
+	s->hash_collisions = c->h_ctr[CTR_COLLISIONS];
+	s->errors = c->h_ctr[CTR_ERRORS];
+	return 0;
+}
+
+// --------------------------------------------------------------------------------------
+// synthetic traces
+// --------------------------------------------------------------------------------------
+static std::mutex g_tables_mu;
+static GenTables* g_tables = nullptr;
+static const GenTables* host_tables() {
+	std::lock_guard<std::mutex> lk(g_tables_mu);
+	if (!g_tables) {
+		g_tables = new GenTables();
+		build_gen_tables(g_tables);
+	}
+	return g_tables;
+}
+
+static bool single_config(uint32_t cfg) { return cfg == 1 || cfg == 11 || cfg == 2 || cfg == 3; }
+
+int ebd_trace_size(const ebd_trace_config* t, uint64_t* payload_bytes) {
+	if (!t || !payload_bytes || !single_config(t->config) || (t->align & (t->align - 1)))
+		return -EINVAL;
+	const GenTables* T = host_tables();
+	const uint32_t a = t->align ? t->align : 1;
+	uint64_t total = 0;
+	for (uint32_t i = 0; i < t->n; i++)
+		total += align_up(gen_single(T, t->config, t->seed, t->first + i, nullptr, nullptr), a);
+	*payload_bytes = total;
+	return 0;
+}
+
+int ebd_trace_generate_host(const ebd_trace_config* t, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
+		uint8_t* payload, uint64_t payload_cap) {
+	if (!t || !single_config(t->config) || (t->align & (t->align - 1)) || (t->n && (!events || !len || !off || !payload)))
+		return -EINVAL;
+	const GenTables* T = host_tables();
+	const uint32_t a = t->align ? t->align : 1;
+	uint64_t at = 0;
+	for (uint32_t i = 0; i < t->n; i++) {
+		const uint32_t L = gen_single(T, t->config, t->seed, t->first + i, nullptr, nullptr);
+		if (at + L > payload_cap)
+			return -ENOSPC;
+		EventRec e;
+		gen_single(T, t->config, t->seed, t->first + i, &e, payload + at);
+		std::memcpy(&events[i], &e, sizeof(e));
+		len[i] = L;
+		off[i] = at;
+		at = align_up(at + L, a);
+	}
+	return 0;
+}
+
+int ebd_trace_size_device(ebd_ctx* c, const ebd_trace_config* t, uint64_t* payload_bytes) {
+	if (!c || !t || !payload_bytes || !single_config(t->config) || (t->align & (t->align - 1)) || t->n == 0)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_gen) {
+		HIP_TRY(hipMalloc(&c->d_gen, sizeof(GenTables)));
+		HIP_TRY(hipMemcpy(c->d_gen, host_tables(), sizeof(GenTables), hipMemcpyHostToDevice));
+	}
+	unsigned long long *alen = nullptr, *sum = nullptr;
+	void* tmp = nullptr;
+	size_t tmp_bytes = 0;
+	HIP_TRY(hipMallocAsync((void**)&alen, (size_t)t->n * 8, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&sum, 8, c->stream));
+	HIP_TRY(launch_gen_len(c->d_gen, t->config, t->seed, t->first, t->n, t->align ? t->align : 1, alen, c->stream));
+	HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, alen, sum, (int)t->n, c->stream));
+	HIP_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 16, c->stream));
+	HIP_TRY(hipcub::DeviceReduce::Sum(tmp, tmp_bytes, alen, sum, (int)t->n, c->stream));
+	unsigned long long v = 0;
+	HIP_TRY(hipMemcpyAsync(&v, sum, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipFreeAsync(sum, c->stream));
+	HIP_TRY(hipFreeAsync(alen, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	*payload_bytes = v;
+	return 0;
+}
+
+int ebd_trace_generate_device(ebd_ctx* c, const ebd_trace_config* t, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
+		uint8_t* payload, uint64_t payload_cap) {
+	if (!c || !t || !single_config(t->config) || (t->align & (t->align - 1)) || t->n == 0)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_gen) {
+		HIP_TRY(hipMalloc(&c->d_gen, sizeof(GenTables)));
+		HIP_TRY(hipMemcpy(c->d_gen, host_tables(), sizeof(GenTables), hipMemcpyHostToDevice));
+	}
+	const uint32_t a = t->align ? t->align : 1;
+	unsigned long long* alen = (unsigned long long*)off;
+	HIP_TRY(launch_gen_len(c->d_gen, t->config, t->seed, t->first, t->n, a, alen, c->stream));
+	size_t tmp_bytes = 0;
+	unsigned long long* tmp_out = nullptr;
+	HIP_TRY(hipMallocAsync((void**)&tmp_out, (size_t)t->n * sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, alen, tmp_out, (int)t->n, c->stream));
+	void* tmp = nullptr;
+	HIP_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 16, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, alen, tmp_out, (int)t->n, c->stream));
+	unsigned long long last_off = 0, last_len = 0;
+	HIP_TRY(hipMemcpyAsync(&last_off, tmp_out + t->n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(&last_len, alen + t->n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	if (last_off + last_len > payload_cap) {
+		HIP_TRY(hipFreeAsync(tmp, c->stream));
+		HIP_TRY(hipFreeAsync(tmp_out, c->stream));
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		return -ENOSPC;
+	}
+	HIP_TRY(hipMemcpyAsync(off, tmp_out, (size_t)t->n * 8, hipMemcpyDeviceToDevice, c->stream));
+	HIP_TRY(launch_gen_write(c->d_gen, t->config, t->seed, t->first, t->n, (EventRec*)events, len,
+			(const unsigned long long*)off, payload, c->stream));
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipFreeAsync(tmp_out, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+// --------------------------------------------------------------------------------------
+// host-side hooks for CPU tests of the shared semantics (no GPU needed)
+// --------------------------------------------------------------------------------------
+int ebd_host_dfa_info(uint32_t* info, uint32_t n) {
+	static KeyTrie trie;
+	static DfaTable* t = nullptr;
+	if (!t) {
+		build_key_trie(&trie);
+		t = new DfaTable();
+		if (build_dfa(&trie, t) != 0)
+			return -EIO;
+	}
+	const uint32_t v[11] = {t->info.nstates, t->info.url_id, t->info.g2, t->info.g3, t->info.g4, t->info.hvc0, t->info.hvh,
+			t->info.fin0, t->info.fin1, t->info.inv, t->info.init};
+	for (uint32_t k = 0; k < n && k < 11; k++)
+		info[k] = v[k];
+	return 0;
+}
+
+static const DfaTable* host_dfa(const KeyTrie** trie_out) {
+	static KeyTrie trie;
+	static DfaTable* t = nullptr;
+	static std::mutex mu;
+	std::lock_guard<std::mutex> lk(mu);
+	if (!t) {
+		build_key_trie(&trie);
+		DfaTable* x = new DfaTable();
+		if (build_dfa(&trie, x) != 0) {
+			delete x;
+			return nullptr;
+		}
+		t = x;
+	}
+	*trie_out = &trie;
+	return t;
+}
+
+static void fill_ifs(Interfaces& ifs, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6) {
+	std::memset(&ifs, 0, sizeof(ifs));
+	ifs.n4 = n4 > 64 ? 64 : n4;
+	ifs.n6 = n6 > 32 ? 32 : n6;
+	for (uint32_t i = 0; i < ifs.n4; i++) {
+		std::memcpy(ifs.v4[i], v4[i].addr, 4);
+		std::memcpy(ifs.v4[i] + 4, v4[i].mask, 4);
+	}
+	for (uint32_t i = 0; i < ifs.n6; i++) {
+		std::memcpy(ifs.v6[i], v6[i].addr, 16);
+		std::memcpy(ifs.v6[i] + 16, v6[i].mask, 16);
+	}
+}
+
+struct HostTab {
+	const uint8_t* t;
+	uint32_t operator[](uint32_t i) const { return t[i]; }
+};
+
+int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags, const uint8_t* src16,
+		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, ebd_event_result* out,
+		uint64_t key[2]) {
+	const KeyTrie* trie;
+	const DfaTable* t = host_dfa(&trie);
+	if (!t || !out || (len && !buf) || len > EBD_BUFFER_MAX_DATA_SIZE)
+		return -EINVAL;
+	static Interfaces ifs;
+	fill_ifs(ifs, v4, n4, v6, n6);
+	FreshScan f;
+	fresh_scan_bytes(HostTab{t->next}, t->info, buf, len, f);
+	FreshResult fr;
+	std::memset(&fr, 0, sizeof(fr));
+	uint8_t zero[16] = {0};
+	fresh_finalize(t->info, f, buf, pid, flags, src16 ? src16 : zero, ifs, fr);
+	*out = fr.r;
+	if (key) {
+		key[0] = fr.key.lo;
+		key[1] = fr.key.hi;
+	}
+	return 0;
+}
+
+int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,
+		uint32_t* consumed, uint32_t* out8) {
+	const KeyTrie* trie;
+	if (!host_dfa(&trie) || !consumed || !out8)
+		return -EINVAL;
+	GenParser g;
+	gp_init(g);
+	uint64_t at = 0;
+	for (uint32_t k = 0; k < nchunks; k++) {
+		const uint8_t* p = data + at;
+		consumed[k] = gp_parse(g, trie, [p](uint32_t i) { return (uint32_t)p[i]; }, chunk_len[k], flags);
+		at += chunk_len[k];
+		if (reset_between && gp_done(g) && k + 1 < nchunks)
+			gp_reset(g);
+	}
+	const uint32_t v[12] = {g.state, g.url_start, g.url_len, (g.f & GPF_HOST) ? g.host_start : 0,
+			(g.f & GPF_HOST) ? g.host_len : 0, g.cip_start, g.cip_len, g.f, g.cipkey, g.mcand, g.mlen,
+			(uint32_t)g.plen | ((uint32_t)g.pminor << 8)};
+	for (int k = 0; k < 12; k++)
+		out8[k] = v[k];
+	return 0;
+}
+
+int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t flags, const ebd_ipv4_network* v4,
+		uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6) {
+	static Interfaces ifs;
+	fill_ifs(ifs, v4, n4, v6, n6);
+	if (is_source)
+		return classify_source(ifs, flags, token);
+	uint32_t tb, te;
+	front_token(token, len, &tb, &te);
+	return classify_token(ifs, token + tb, te - tb);
+}
+
+int ebd_host_pton(int af6, const uint8_t* text, uint32_t len, uint8_t* out) {
+	return af6 ? (inet_pton6(text, len, out) ? 1 : 0) : (inet_pton4(text, len, out) ? 1 : 0);
+}
+
+} // extern "C"

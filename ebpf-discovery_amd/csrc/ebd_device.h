@@ -1,0 +1,121 @@
+// ebd_device.h — device-side data structures shared by the kernels (ebd_kernels.hip).
+#pragma once
+
+#include "../../include/ebpf_discovery_amd.h"
+#include "ebd_dfa.h"
+#include "ebd_gen.h"
+#include "ebd_spec.h"
+
+namespace ebd {
+
+// Service table slot (64 B, one cache line half): the Aggregator's
+// unordered_map<pair<pid, endpoint>, Service> (Aggregator.h:29-37, Service.h:43-66).
+struct Slot {
+	unsigned long long tag;     // Hash128.lo of (pid, endpoint); 0 = empty; claimed by CAS
+	unsigned long long hi;      // Hash128.hi, published by the claimer
+	unsigned long long min_seq; // first-arrival request (global event order), atomicMin
+	unsigned long long ep_off;  // endpoint bytes in the string arena (set by the representative)
+	unsigned int pid;
+	unsigned int internal_clients; // uint32, wraps like Service.h:53-54
+	unsigned int external_clients;
+	unsigned int ep_len;
+	unsigned int dom;  // domain offset | length << 16, within the endpoint
+	unsigned int info; // bit0 https, bit1 representative written
+	unsigned int pad[2];
+};
+static_assert(sizeof(Slot) == 64, "slot is 64 bytes");
+
+// Session-set slot: (pid, fd, sessionID) of every session that needs the sequential
+// path in this batch (Discovery.h:47 LRU key, Types.h:72-86).
+struct SSlot {
+	unsigned long long tag;
+	unsigned long long kv; // fd << 32 | pid
+	unsigned int sid;
+	unsigned int ready;
+	unsigned int carry; // 1 + index into the carried-session array, 0 = none
+	unsigned int visited;
+};
+static_assert(sizeof(SSlot) == 32, "session slot is 32 bytes");
+
+constexpr uint32_t kCarryBytes = 8200; // > DISCOVERY_MAX_HTTP_REQUEST_LENGTH + 1
+
+// A saved session that outlives its batch: the LRU entry (Discovery.cpp:148-150) with
+// its parser state and the bytes of the request in progress.
+struct Carry {
+	uint32_t pid, fd, sid, nbytes;
+	GenParser g;
+	uint8_t bytes[kCarryBytes];
+};
+
+// Session-path request (ebd_session_request in the public header).
+struct SessReq {
+	unsigned long long seq;
+	uint32_t pid;
+	uint32_t str_off;
+	uint16_t host_len, url_len, cip_off, cip_len;
+	uint8_t info, status;
+	uint16_t pad;
+	uint32_t pad2;
+};
+static_assert(sizeof(SessReq) == 32, "session request is 32 bytes");
+
+// 64-bit counters; [0, CTR_BATCH_END) are reset per batch, the rest persist.
+enum Ctr : uint32_t {
+	CTR_UNFINISHED = 0, // fresh-UNFINISHED events (session-set inserts)
+	CTR_SLOW,           // session-path events
+	CTR_SREQ,           // session-path requests
+	CTR_SSTR,           // session string bytes
+	CTR_NEW,            // service slots claimed in this batch
+	CTR_CARRY_OUT,      // sessions saved for the next batch
+	CTR_DIRTY,          // session-set slots claimed in this batch
+	CTR_INSERTS,        // LRU inserts in this batch
+	CTR_BATCH_END = 8,
+	CTR_SARENA = 8,     // service string arena bytes used
+	CTR_ERRORS,         // EBD_ERR_* bitmask
+	CTR_COLLISIONS,
+	CTR_KDELETES,
+	CTR_REQUESTS,
+	CTR_SESSION_EVENTS,
+	CTR_COUNT = 16,
+};
+
+struct Dev {
+	// immutable tables
+	const uint8_t* dfa;
+	DfaInfo di;
+	const KeyTrie* trie;
+	const Interfaces* ifs;
+	// batch
+	const EventRec* ev;
+	const uint32_t* len;
+	const uint64_t* off;
+	const uint8_t* payload;
+	uint32_t n;
+	unsigned long long seq_base;
+	// per-event outputs
+	ebd_event_result* res;
+	Hash128* keys;
+	// service table
+	Slot* slots;
+	uint32_t slot_mask;
+	uint32_t* new_slots;
+	uint32_t new_cap;
+	uint8_t* sarena;
+	unsigned long long sarena_cap;
+	// session path
+	SSlot* sset;
+	uint32_t sset_mask;
+	uint32_t* dirty;
+	unsigned long long* slow_keys;
+	Carry* carry_in;
+	uint32_t n_carry_in;
+	Carry* carry_out;
+	uint32_t carry_cap;
+	SessReq* sreq;
+	uint8_t* sstr;
+	unsigned long long sstr_cap;
+	// counters
+	unsigned long long* ctr;
+};
+
+} // namespace ebd

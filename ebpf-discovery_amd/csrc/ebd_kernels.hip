@@ -1,0 +1,672 @@
+// ebd_kernels.hip — the MI355X kernels of the HTTP per-event parse path.
+//
+// Batch pipeline (one poll cycle of Discovery::fetchAndHandleEvents, Discovery.cpp:48-90):
+//   k_carry_insert  sessions saved by earlier batches join this batch's session set
+//   k_fresh         every NEW_DATA buffer through a fresh parser (DFA in LDS, one lane per
+//                   event); finished requests get their client class and 128-bit key
+//   k_slow_collect  events of sessions that need the sequential path (a fresh parse left
+//                   the request unfinished, or the session was saved by an earlier batch)
+//   k_walk          one lane per such session, events in order: the exact
+//                   handleExistingSession / handleNewSession / handleCloseEvent logic
+//                   (Discovery.cpp:112-198) over the generic parser
+//   k_agg_fast      Aggregator::newRequest for the single-buffer requests
+//   k_reps          first-arrival domain / scheme / endpoint string for new services
+#include <hip/hip_runtime.h>
+
+#include "ebd_device.h"
+#include "ebd_fresh.h"
+
+namespace ebd {
+
+constexpr uint32_t kSpinLimit = 1u << 20;
+
+__device__ __forceinline__ void set_error(const Dev& d, unsigned long long bit) { atomicOr(&d.ctr[CTR_ERRORS], bit); }
+
+__device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
+	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------
+// Service table: open addressing on the 64-bit tag, 128-bit key verified.
+// ---------------------------------------------------------------------------------
+__device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, uint32_t cls) {
+	uint32_t idx = (uint32_t)h.lo & d.slot_mask;
+	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
+		Slot* s = d.slots + idx;
+		unsigned long long t = ld_relaxed(&s->tag);
+		if (t == 0) {
+			t = atomicCAS(&s->tag, 0ull, h.lo);
+			if (t == 0) { // claimed: publish the second key half right away
+				atomicExch(&s->hi, h.hi);
+				const unsigned long long k = atomicAdd(&d.ctr[CTR_NEW], 1ull);
+				if (k < d.new_cap)
+					d.new_slots[k] = idx;
+				else
+					set_error(d, EBD_ERR_TABLE_FULL);
+				t = h.lo;
+			}
+		}
+		if (t == h.lo) {
+			unsigned long long hi = ld_relaxed(&s->hi);
+			for (uint32_t spin = 0; hi == 0; spin++) {
+				if (spin > kSpinLimit) {
+					set_error(d, EBD_ERR_SPIN);
+					return 0xffffffffu;
+				}
+				__builtin_amdgcn_s_sleep(2);
+				hi = atomicOr(&s->hi, 0ull);
+			}
+			if (hi == h.hi) {
+				if (cls == CLS_INTERNAL)
+					atomicAdd(&s->internal_clients, 1u);
+				else if (cls == CLS_EXTERNAL)
+					atomicAdd(&s->external_clients, 1u);
+				if (seq < ld_relaxed(&s->min_seq))
+					atomicMin(&s->min_seq, seq);
+				return idx;
+			}
+			atomicAdd(&d.ctr[CTR_COLLISIONS], 1ull);
+		}
+		idx = (idx + 1) & d.slot_mask;
+	}
+	set_error(d, EBD_ERR_TABLE_FULL);
+	return 0xffffffffu;
+}
+
+// ---------------------------------------------------------------------------------
+// Session set: (pid, fd, sessionID) -> slot.  96-bit key verified after the tag.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long sset_tag(unsigned long long kv, uint32_t sid) {
+	return fmix64(kv ^ ((unsigned long long)sid * 0x9E3779B97F4A7C15ull) ^ 0x5bd1e9955bd1e995ull) | 1ull;
+}
+
+__device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry) {
+	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
+	const unsigned long long tag = sset_tag(kv, sid);
+	uint32_t idx = (uint32_t)tag & d.sset_mask;
+	for (uint32_t probe = 0; probe <= d.sset_mask; probe++) {
+		SSlot* s = d.sset + idx;
+		unsigned long long t = ld_relaxed(&s->tag);
+		bool mine = false;
+		if (t == 0) {
+			t = atomicCAS(&s->tag, 0ull, tag);
+			if (t == 0) {
+				atomicExch(&s->kv, kv);
+				atomicExch(&s->sid, sid);
+				if (carry)
+					atomicExch(&s->carry, carry);
+				__threadfence();
+				atomicExch(&s->ready, 1u);
+				const unsigned long long k = atomicAdd(&d.ctr[CTR_DIRTY], 1ull);
+				d.dirty[k] = idx;
+				mine = true;
+			}
+		}
+		if (mine)
+			return (int)idx;
+		if (t == tag) {
+			for (uint32_t spin = 0; atomicOr(&s->ready, 0u) == 0; spin++) {
+				if (spin > kSpinLimit) {
+					set_error(d, EBD_ERR_SPIN);
+					return -1;
+				}
+				__builtin_amdgcn_s_sleep(2);
+			}
+			__threadfence();
+			if (atomicOr(&s->kv, 0ull) == kv && atomicOr(&s->sid, 0u) == sid) {
+				if (carry)
+					atomicExch(&s->carry, carry);
+				return (int)idx;
+			}
+		}
+		idx = (idx + 1) & d.sset_mask;
+	}
+	set_error(d, EBD_ERR_SESSION_FULL);
+	return -1;
+}
+
+// Lookup after the inserting kernels finished (plain loads are coherent then).
+__device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) {
+	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
+	const unsigned long long tag = sset_tag(kv, sid);
+	uint32_t idx = (uint32_t)tag & d.sset_mask;
+	for (uint32_t probe = 0; probe <= d.sset_mask; probe++) {
+		const SSlot* s = d.sset + idx;
+		const unsigned long long t = s->tag;
+		if (t == 0)
+			return -1;
+		if (t == tag && s->kv == kv && s->sid == sid)
+			return (int)idx;
+		idx = (idx + 1) & d.sset_mask;
+	}
+	return -1;
+}
+
+// ---------------------------------------------------------------------------------
+// k_fresh: one lane per event, DFA table in LDS, 16-byte aligned loads of the buffer.
+// ---------------------------------------------------------------------------------
+struct LdsTable {
+	const uint8_t* t;
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
+};
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_fresh(Dev d) {
+	extern __shared__ __attribute__((aligned(16))) uint8_t T[];
+	const uint32_t tb = d.di.nstates * 256u;
+	for (uint32_t k = threadIdx.x * 16u; k < tb; k += BLOCK * 16u)
+		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
+	__syncthreads();
+	const DfaInfo di = d.di;
+	const LdsTable tab{T};
+	for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < d.n; i += gridDim.x * BLOCK) {
+		const uint8_t* evb = (const uint8_t*)(d.ev + i);
+		const uint8_t flags = evb[32];
+		const uint32_t L = d.len[i];
+		FreshResult fr;
+		fr.r.consumed = 0;
+		fr.r.status = EBD_STATUS_NONE;
+		fr.r.info = 0;
+		fr.r.u.session.index = 0;
+		fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
+		if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER) {
+			if (L > EBD_BUFFER_MAX_DATA_SIZE) {
+				set_error(d, EBD_ERR_BAD_INPUT);
+			} else {
+				const uint8_t* p = d.payload + d.off[i];
+				const uintptr_t pa = (uintptr_t)p;
+				const uint4* q = (const uint4*)(pa & ~(uintptr_t)15);
+				const int skip = (int)(pa & 15);
+				const int end = skip + (int)L;
+				FreshScan f;
+				fresh_init(di, f);
+				for (int base = 0; base < end; base += 16) {
+					const uint4 w = q[base >> 4];
+					const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+					for (int k = 0; k < 16; k++) {
+						const int pos = base + k - skip;
+						const bool v = (uint32_t)pos < L;
+						fresh_byte(tab, di, f, (ws[k >> 2] >> ((k & 3) * 8)) & 0xffu, pos, v);
+					}
+					if (f.s >= di.g4)
+						break;
+				}
+				const uint32_t pid = *(const uint32_t*)evb;
+				fresh_finalize(di, f, p, pid, flags, evb + 16, *d.ifs, fr);
+				if (fr.r.status == EBD_STATUS_FINISHED) {
+					d.keys[i] = fr.key;
+				} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+					// the session may be saved (Discovery.cpp:148-150): sequential path
+					atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+					sset_insert(d, pid, *(const uint32_t*)(evb + 4), *(const uint32_t*)(evb + 8), 0);
+				}
+			}
+		}
+		d.res[i] = fr.r;
+	}
+}
+
+__global__ void k_carry_insert(Dev d) {
+	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d.n_carry_in; c += gridDim.x * blockDim.x) {
+		const Carry& cr = d.carry_in[c];
+		sset_insert(d, cr.pid, cr.fd, cr.sid, c + 1);
+	}
+}
+
+__global__ void k_slow_collect(Dev d) {
+	if (d.ctr[CTR_DIRTY] == 0)
+		return; // no session needs the sequential path in this batch
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
+		const EventRec& e = d.ev[i];
+		if (!(e.flags & (FLAG_NEW | FLAG_END)))
+			continue;
+		const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
+		if (slot >= 0) {
+			const unsigned long long k = atomicAdd(&d.ctr[CTR_SLOW], 1ull);
+			d.slow_keys[k] = ((unsigned long long)(uint32_t)slot << 32) | i;
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// k_walk: the sequential session path.  The bytes of the request in progress are the
+// carried bytes (if the request started in an earlier batch) followed by the buffers
+// of this batch's events from position j0 on.
+// ---------------------------------------------------------------------------------
+struct Walk {
+	const uint8_t* cb; // carried bytes of the request in progress
+	uint32_t clen;
+	uint32_t j0;       // first sorted position whose buffer belongs to the request
+};
+
+__device__ __forceinline__ uint32_t slow_event(const Dev& d, uint32_t j) { return (uint32_t)d.slow_keys[j]; }
+
+__device__ __forceinline__ uint32_t piece_len(const Dev& d, uint32_t j) {
+	const uint32_t i = slow_event(d, j);
+	const uint32_t L = d.len[i];
+	return ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) ? L : 0;
+}
+
+// Visits stream bytes [a, a + n) in order; the stream ends at sorted position jend whose
+// piece is truncated to cend bytes.  fn(byte) returns false to stop.  Returns bytes visited.
+template <typename Fn>
+__device__ uint32_t stream_visit(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, uint32_t a, uint32_t n, Fn fn) {
+	uint32_t pos = 0, done = 0;
+	const uint32_t b = a + n;
+	if (w.clen) {
+		for (uint32_t k = a; k < b && k < w.clen; k++) {
+			if (!fn(w.cb[k]))
+				return done;
+			done++;
+		}
+		pos = w.clen;
+	}
+	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
+		uint32_t pl = piece_len(d, j);
+		if (j == jend)
+			pl = cend;
+		if (pl == 0)
+			continue;
+		const uint32_t lo = a > pos ? a : pos, hi = b < pos + pl ? b : pos + pl;
+		if (lo < hi) {
+			const uint8_t* src = d.payload + d.off[slow_event(d, j)] + (lo - pos);
+			for (uint32_t k = 0; k < hi - lo; k++) {
+				if (!fn(src[k]))
+					return done;
+				done++;
+			}
+		}
+		pos += pl;
+	}
+	return done;
+}
+
+// handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
+// (Discovery.cpp:161-192, 210-212) for a request finished by the session path.
+__device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, const GenParser& g,
+		uint32_t i, ebd_event_result& r) {
+	const EventRec& ev = d.ev[i];
+	const uint32_t hl = (g.f & GPF_HOST) ? g.host_len : 0, ul = g.url_len;
+	uint32_t raw = 0;
+	if (g.f & GPF_CIP_FOUND) // the value up to its first ',' is the front token's source
+		raw = stream_visit(d, w, jend, cend, g.cip_start, g.cip_len, [](uint8_t c) { return c != ','; });
+	const uint32_t total = hl + ul + raw;
+	const unsigned long long at = atomicAdd(&d.ctr[CTR_SSTR], (unsigned long long)total);
+	uint8_t info = (uint8_t)((g.mcand == 'P' ? EBD_INFO_POST : 0) | ((g.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0) | EBD_INFO_SESSION);
+	uint8_t cls;
+	KeyHasher kh;
+	kh.init(ev.pid);
+	uint32_t tb = 0, te = 0;
+	if (at + total > d.sstr_cap) {
+		set_error(d, EBD_ERR_ARENA_FULL);
+		return;
+	}
+	uint8_t* dst = d.sstr + at;
+	uint32_t k = 0;
+	stream_visit(d, w, jend, cend, g.host_start, hl, [&](uint8_t c) {
+		dst[k++] = c;
+		return true;
+	});
+	stream_visit(d, w, jend, cend, g.url_start, ul, [&](uint8_t c) {
+		dst[k++] = c;
+		return true;
+	});
+	if (raw)
+		stream_visit(d, w, jend, cend, g.cip_start, raw, [&](uint8_t c) {
+			dst[k++] = c;
+			return true;
+		});
+	if (g.f & GPF_CIP_FOUND) {
+		front_token(dst + hl + ul, raw, &tb, &te);
+		info |= EBD_INFO_CIP;
+		cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb);
+	} else {
+		cls = classify_source(*d.ifs, ev.flags, ev.sourceIP);
+	}
+	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
+	kh.bytes(dst, hl + ul);
+	agg_insert(d, kh.finish(), d.seq_base + i, cls);
+	atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
+	const unsigned long long q = atomicAdd(&d.ctr[CTR_SREQ], 1ull);
+	SessReq sr;
+	sr.seq = d.seq_base + i;
+	sr.pid = ev.pid;
+	sr.str_off = (uint32_t)at;
+	sr.host_len = (uint16_t)hl;
+	sr.url_len = (uint16_t)ul;
+	sr.cip_off = (uint16_t)(hl + ul + tb);
+	sr.cip_len = (uint16_t)(te - tb);
+	sr.info = info;
+	sr.status = EBD_STATUS_FINISHED;
+	sr.pad = 0;
+	sr.pad2 = 0;
+	d.sreq[q] = sr;
+	r.info = info;
+	r.u.session.index = (uint32_t)q;
+}
+
+__device__ void walk_session(const Dev& d, uint32_t j, uint32_t nslow, uint32_t slot) {
+	SSlot* ss = d.sset + slot;
+	ss->visited = 1;
+	GenParser g;
+	bool live = false;
+	Walk w{nullptr, 0, j};
+	const uint32_t carry = ss->carry;
+	if (carry) { // saved session from an earlier batch (LRU entry)
+		const Carry& c = d.carry_in[carry - 1];
+		g = c.g;
+		live = true;
+		w.cb = c.bytes;
+		w.clen = c.nbytes;
+	} else {
+		gp_init(g);
+	}
+	const KeyTrie* trie = d.trie;
+	uint32_t jj = j;
+	for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
+		const uint32_t i = slow_event(d, jj);
+		const EventRec& ev = d.ev[i];
+		const uint8_t flags = ev.flags;
+		const uint32_t L = d.len[i];
+		ebd_event_result r;
+		r.consumed = 0;
+		r.status = EBD_STATUS_NONE;
+		r.info = EBD_INFO_SESSION;
+		r.u.session.index = 0xffffffffu;
+		r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
+		atomicAdd(&d.ctr[CTR_SESSION_EVENTS], 1ull);
+		if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
+			const uint8_t* buf = d.payload + d.off[i];
+			auto at = [buf](uint32_t k) { return (uint32_t)buf[k]; };
+			if (live) { // handleExistingSession, Discovery.cpp:123-139
+				r.info |= EBD_INFO_EXISTING;
+				const uint32_t c = gp_parse(g, trie, at, L, flags);
+				r.consumed = (uint16_t)c;
+				if (g.state == ST_INVALID) {
+					r.status = EBD_STATUS_INVALID;
+					atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
+					live = false;
+				} else if (g.state == ST_FINISHED) {
+					r.status = EBD_STATUS_FINISHED;
+					emit_session_request(d, w, jj, c, g, i, r);
+					gp_reset(g); // session.reset(); stays saved
+					w = Walk{nullptr, 0, jj + 1};
+				} else {
+					r.status = EBD_STATUS_UNFINISHED;
+				}
+			} else { // handleNewSession, Discovery.cpp:141-159
+				gp_init(g);
+				w = Walk{nullptr, 0, jj};
+				const uint32_t c = gp_parse(g, trie, at, L, flags);
+				r.consumed = (uint16_t)c;
+				if (g.state == ST_INVALID) {
+					r.status = EBD_STATUS_INVALID;
+				} else if (g.state == ST_FINISHED) {
+					r.status = EBD_STATUS_FINISHED;
+					emit_session_request(d, w, jj, c, g, i, r);
+				} else {
+					r.status = EBD_STATUS_UNFINISHED;
+					if (!(flags & FLAG_END)) {
+						live = true; // saveSession
+						atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
+					}
+				}
+			}
+		}
+		if (flags & FLAG_END) // handleCloseEvent, Discovery.cpp:194-198
+			live = false;
+		d.res[i] = r;
+	}
+	if (live) { // saved for the next batch, with the bytes of the request in progress
+		const unsigned long long c = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
+		if (c >= d.carry_cap) {
+			set_error(d, EBD_ERR_LRU_OVERFLOW);
+			return;
+		}
+		Carry& out = d.carry_out[c];
+		const EventRec& ev = d.ev[slow_event(d, j)];
+		out.pid = ev.pid;
+		out.fd = ev.fd;
+		out.sid = ev.sessionID;
+		out.g = g;
+		const uint32_t nb = g.length < kCarryBytes ? g.length : kCarryBytes;
+		out.nbytes = nb;
+		uint32_t k = 0;
+		uint8_t* dst = out.bytes;
+		// the request in progress ends with the last event of this session (fully consumed)
+		stream_visit(d, w, jj - 1, piece_len(d, jj - 1), 0, nb, [&](uint8_t b) {
+			dst[k++] = b;
+			return true;
+		});
+	}
+}
+
+__global__ void k_walk(Dev d, uint32_t nslow) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
+		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
+		if (j > 0 && (uint32_t)(d.slow_keys[j - 1] >> 32) == slot)
+			continue;
+		walk_session(d, j, nslow, slot);
+	}
+}
+
+// Saved sessions with no event in this batch stay saved unchanged.
+__global__ void k_carry_pass(Dev d) {
+	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d.n_carry_in; c += gridDim.x * blockDim.x) {
+		const Carry& cr = d.carry_in[c];
+		const int slot = sset_find(d, cr.pid, cr.fd, cr.sid);
+		if (slot >= 0 && d.sset[slot].visited)
+			continue;
+		const unsigned long long k = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
+		if (k >= d.carry_cap) {
+			set_error(d, EBD_ERR_LRU_OVERFLOW);
+			continue;
+		}
+		Carry& out = d.carry_out[k];
+		out.pid = cr.pid;
+		out.fd = cr.fd;
+		out.sid = cr.sid;
+		out.g = cr.g;
+		out.nbytes = cr.nbytes;
+		for (uint32_t b = 0; b < cr.nbytes; b++)
+			out.bytes[b] = cr.bytes[b];
+	}
+}
+
+__global__ void k_agg_fast(Dev d) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
+		const ebd_event_result r = d.res[i];
+		if (r.status != EBD_STATUS_FINISHED || (r.info & EBD_INFO_SESSION))
+			continue;
+		agg_insert(d, d.keys[i], d.seq_base + i, (r.info >> EBD_INFO_CLASS_SHIFT) & 3u);
+		atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
+	}
+}
+
+// First-arrival representative of every service created in this batch (Aggregator.cpp:
+// 112-130, 160-167): endpoint string, domain, scheme, pid.
+__global__ void k_reps(Dev d) {
+	const unsigned long long nn = d.ctr[CTR_NEW];
+	const uint32_t n_new = (uint32_t)(nn < d.new_cap ? nn : d.new_cap);
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_new; k += gridDim.x * blockDim.x) {
+		Slot* s = d.slots + d.new_slots[k];
+		const unsigned long long seq = s->min_seq;
+		const uint32_t e = (uint32_t)(seq - d.seq_base);
+		const ebd_event_result r = d.res[e];
+		const uint8_t *host, *url;
+		uint32_t hl, ul;
+		if (r.info & EBD_INFO_SESSION) {
+			const SessReq& q = d.sreq[r.u.session.index];
+			host = d.sstr + q.str_off;
+			hl = q.host_len;
+			url = host + hl;
+			ul = q.url_len;
+		} else {
+			const uint8_t* p = d.payload + d.off[e];
+			host = p + r.u.span.host_off;
+			hl = r.u.span.host_len;
+			url = p + r.u.span.url_off;
+			ul = r.u.span.url_len;
+		}
+		const unsigned long long at = atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)(hl + ul));
+		uint32_t doff = 0, dlen = 0;
+		host_domain(host, hl, &doff, &dlen);
+		s->pid = d.ev[e].pid;
+		s->ep_len = hl + ul;
+		s->dom = doff | (dlen << 16);
+		s->info = ((r.info & EBD_INFO_HTTPS) ? 1u : 0u) | 2u;
+		if (at + hl + ul > d.sarena_cap) {
+			set_error(d, EBD_ERR_ARENA_FULL);
+			s->ep_off = ~0ull;
+			continue;
+		}
+		s->ep_off = at;
+		uint8_t* dst = d.sarena + at;
+		for (uint32_t b = 0; b < hl; b++)
+			dst[b] = host[b];
+		for (uint32_t b = 0; b < ul; b++)
+			dst[hl + b] = url[b];
+	}
+}
+
+__global__ void k_sset_clear(Dev d) {
+	const unsigned long long nd = d.ctr[CTR_DIRTY];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
+		SSlot* s = d.sset + d.dirty[k];
+		s->tag = 0;
+		s->kv = 0;
+		s->sid = 0;
+		s->ready = 0;
+		s->carry = 0;
+		s->visited = 0;
+	}
+}
+
+__global__ void k_slots_init(Slot* slots, uint32_t n) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		Slot s;
+		s.tag = 0;
+		s.hi = 0;
+		s.min_seq = ~0ull;
+		s.ep_off = 0;
+		s.pid = 0;
+		s.internal_clients = 0;
+		s.external_clients = 0;
+		s.ep_len = 0;
+		s.dom = 0;
+		s.info = 0;
+		s.pad[0] = s.pad[1] = 0;
+		slots[k] = s;
+	}
+}
+
+__global__ void k_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const Slot& s = slots[k];
+		if (s.tag == 0)
+			continue;
+		const unsigned long long at = atomicAdd(cnt, 1ull);
+		ebd_service v;
+		v.pid = s.pid;
+		v.internal_clients = s.internal_clients;
+		v.external_clients = s.external_clients;
+		v.https = (uint8_t)(s.info & 1u);
+		v.pad_[0] = v.pad_[1] = v.pad_[2] = 0;
+		v.endpoint_off = s.ep_off;
+		v.endpoint_len = s.ep_len;
+		v.domain_off = s.dom & 0xffffu;
+		v.domain_len = s.dom >> 16;
+		v.pad2_ = 0;
+		v.first_seq = s.min_seq;
+		out[at] = v;
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// Synthetic trace generation in HBM (ebd_gen.h).
+// ---------------------------------------------------------------------------------
+__global__ void k_gen_len(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
+		uint32_t align, unsigned long long* alen) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+		alen[i] = align_up(gen_single(T, config, seed, first + i, nullptr, nullptr), align);
+}
+
+__global__ void k_gen_write(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
+		EventRec* ev, uint32_t* len, const unsigned long long* off, uint8_t* payload) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		EventRec e;
+		const uint32_t L = gen_single(T, config, seed, first + i, &e, payload + off[i]);
+		ev[i] = e;
+		len[i] = L;
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// launch wrappers (called from ebd_api.cpp)
+// ---------------------------------------------------------------------------------
+static int grid_for(uint64_t items, int block, int cap) {
+	uint64_t g = (items + block - 1) / block;
+	if (g < 1)
+		g = 1;
+	return (int)(g > (uint64_t)cap ? cap : g);
+}
+
+constexpr int kFreshBlock = 256;
+
+hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
+	const size_t lds = (size_t)d.di.nstates * 256;
+	const int grid = grid_for(d.n, kFreshBlock, cus * 8);
+	hipLaunchKernelGGL(k_fresh<kFreshBlock>, dim3(grid), dim3(kFreshBlock), lds, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_carry_insert(const Dev& d, hipStream_t st) {
+	hipLaunchKernelGGL(k_carry_insert, dim3(grid_for(d.n_carry_in, 256, 256)), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_slow_collect, dim3(grid_for(d.n, 256, cus * 8)), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, 64, cus * 16)), dim3(64), 0, st, d, nslow);
+	return hipGetLastError();
+}
+hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
+	hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_agg_fast, dim3(grid_for(d.n, 256, cus * 8)), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_reps(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_reps, dim3(cus * 4), dim3(64), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_sset_clear, dim3(cus * 4), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st) {
+	hipLaunchKernelGGL(k_slots_init, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n);
+	return hipGetLastError();
+}
+hipError_t launch_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt, hipStream_t st) {
+	hipLaunchKernelGGL(k_collect, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n, out, cnt);
+	return hipGetLastError();
+}
+hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
+		unsigned long long* alen, hipStream_t st) {
+	hipLaunchKernelGGL(k_gen_len, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, T, config, (unsigned long long)seed,
+			(unsigned long long)first, n, align, alen);
+	return hipGetLastError();
+}
+hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, EventRec* ev,
+		uint32_t* len, const unsigned long long* off, uint8_t* payload, hipStream_t st) {
+	hipLaunchKernelGGL(k_gen_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, T, config, (unsigned long long)seed,
+			(unsigned long long)first, n, ev, len, off, payload);
+	return hipGetLastError();
+}
+
+} // namespace ebd

@@ -1,0 +1,364 @@
+"""ebd — Python binding of libebd_amd.so (include/ebpf_discovery_amd.h) over ctypes.
+
+Mirrors the reference's consumer-side surface for the HTTP per-event parse path:
+Context.submit ~ Discovery::fetchAndHandleEvents (one poll cycle, Discovery.cpp:48-90),
+Context.services ~ Aggregator::collectServices (Aggregator.cpp:170-181),
+Context.clear ~ Aggregator::clear (Aggregator.cpp:136-153).
+
+There is no CPU fallback: if libebd_amd.so is missing, importing this module fails.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_DIR, "libebd_amd.so")
+
+FLAG_IPV4, FLAG_IPV6, FLAG_UNENCRYPTED, FLAG_SSL, FLAG_NEW_DATA, FLAG_DATA_END = 2, 4, 8, 16, 32, 64
+NO_BUFFER = 0xFFFFFFFF
+STATUS_NONE, STATUS_UNFINISHED, STATUS_FINISHED, STATUS_INVALID = 0, 1, 2, 3
+INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING = 0x01, 0x02, 0x04, 0x08, 0x40
+CLASS_NONE, CLASS_INTERNAL, CLASS_EXTERNAL = 0, 1, 2
+ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "SPIN", 32: "BAD_INPUT"}
+
+EVENT_DTYPE = np.dtype([("pid", "<u4"), ("fd", "<u4"), ("sessionID", "<u4"), ("bufferSeq", "<u4"),
+                        ("sourceIP", "u1", (16,)), ("flags", "u1"), ("pad", "u1", (3,))])
+RESULT_DTYPE = np.dtype([("consumed", "<u2"), ("status", "u1"), ("info", "u1"), ("url_off", "<u2"),
+                         ("url_len", "<u2"), ("host_off", "<u2"), ("host_len", "<u2"), ("cip_off", "<u2"),
+                         ("cip_len", "<u2")])
+SESSION_REQ_DTYPE = np.dtype([("seq", "<u8"), ("pid", "<u4"), ("str_off", "<u4"), ("host_len", "<u2"),
+                              ("url_len", "<u2"), ("cip_off", "<u2"), ("cip_len", "<u2"), ("info", "u1"),
+                              ("status", "u1"), ("pad", "<u2"), ("pad2", "<u4")])
+SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4"), ("https", "u1"),
+                          ("pad", "u1", (3,)), ("endpoint_off", "<u8"), ("endpoint_len", "<u4"),
+                          ("domain_off", "<u4"), ("domain_len", "<u4"), ("pad2", "<u4"), ("first_seq", "<u8")])
+assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
+assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 48
+CFG_TIMING = 2
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("max_events", C.c_uint32), ("max_payload", C.c_uint64),
+                ("service_capacity", C.c_uint32), ("string_arena", C.c_uint64), ("lru_capacity", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+class DeviceBatch(C.Structure):
+    _fields_ = [("events", C.c_void_p), ("len", C.c_void_p), ("off", C.c_void_p), ("payload", C.c_void_p),
+                ("n", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("events", C.c_uint64), ("requests", C.c_uint64), ("session_events", C.c_uint64),
+                ("kernel_deletes", C.c_uint64), ("live_sessions", C.c_uint64), ("max_live_sessions", C.c_uint64),
+                ("services", C.c_uint64), ("hash_collisions", C.c_uint64), ("errors", C.c_uint64)]
+
+
+class KernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 24), ("launches", C.c_uint64), ("total_ms", C.c_double)]
+
+
+class TraceConfig(C.Structure):
+    _fields_ = [("config", C.c_uint32), ("seed", C.c_uint64), ("first", C.c_uint64), ("n", C.c_uint32),
+                ("align", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Ipv4Network(C.Structure):
+    _fields_ = [("addr", C.c_uint8 * 4), ("mask", C.c_uint8 * 4)]
+
+
+class Ipv6Network(C.Structure):
+    _fields_ = [("addr", C.c_uint8 * 16), ("mask", C.c_uint8 * 16)]
+
+
+# Every function the public headers declare (checked by tests/test_abi.py).
+_SIGS = {
+    "ebd_ctx_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
+    "ebd_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "ebd_ctx_stream": (C.c_void_p, [C.c_void_p]),
+    "ebd_set_interfaces": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    "ebd_submit_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                   C.c_uint32]),
+    "ebd_submit_batch_device": (C.c_int, [C.c_void_p, C.POINTER(DeviceBatch)]),
+    "ebd_sync": (C.c_int, [C.c_void_p]),
+    "ebd_set_seq_base": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "ebd_kernel_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "ebd_reset_kernel_times": (C.c_int, [C.c_void_p]),
+    "ebd_fetch_results": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "ebd_results_device": (C.c_void_p, [C.c_void_p]),
+    "ebd_fetch_session_requests": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
+                                             C.c_uint64, C.POINTER(C.c_uint64)]),
+    "ebd_collect_services": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
+                                       C.c_uint64, C.POINTER(C.c_uint64)]),
+    "ebd_clear": (C.c_int, [C.c_void_p]),
+    "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "ebd_strerror": (C.c_char_p, [C.c_int]),
+    "ebd_trace_size": (C.c_int, [C.POINTER(TraceConfig), C.POINTER(C.c_uint64)]),
+    "ebd_trace_generate_host": (C.c_int, [C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_uint64]),
+    "ebd_trace_size_device": (C.c_int, [C.c_void_p, C.POINTER(TraceConfig), C.POINTER(C.c_uint64)]),
+    "ebd_trace_generate_device": (C.c_int, [C.c_void_p, C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_uint64]),
+    # testing header
+    "ebd_host_dfa_info": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
+                                 C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "ebd_host_gp_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
+    "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
+                                    C.c_uint32]),
+    "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Loads libebd_amd.so; raises if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libebd_amd.so not built ({LIB_PATH}); run `make -C ebpf-discovery_amd`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class EbdError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise EbdError(f"{what}: {lib().ebd_strerror(rc).decode()} ({rc})")
+
+
+def _p(a):
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):  # torch tensor
+        return C.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(C.c_void_p) if a.size else None
+
+
+def _nets4(v4):
+    arr = (Ipv4Network * max(len(v4), 1))()
+    for k, (a, m) in enumerate(v4):
+        arr[k].addr[:] = list(a)
+        arr[k].mask[:] = list(m)
+    return arr
+
+
+def _nets6(v6):
+    arr = (Ipv6Network * max(len(v6), 1))()
+    for k, (a, m) in enumerate(v6):
+        arr[k].addr[:] = list(a)
+        arr[k].mask[:] = list(m)
+    return arr
+
+
+class Context:
+    """One GPU context: the Discovery consumer state (session LRU) + the Aggregator."""
+
+    def __init__(self, max_events, device=0, max_payload=0, service_capacity=0, string_arena=0, lru_capacity=0,
+                 timing=False):
+        cfg = Config(device=device, max_events=max_events, max_payload=max_payload,
+                     service_capacity=service_capacity, string_arena=string_arena, lru_capacity=lru_capacity,
+                     flags=CFG_TIMING if timing else 0)
+        h = C.c_void_p()
+        _check(lib().ebd_ctx_create(C.byref(cfg), C.byref(h)), "ebd_ctx_create")
+        self.h = h
+        self.max_events = max_events
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ebd_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    @property
+    def stream(self):
+        return lib().ebd_ctx_stream(self.h)
+
+    def set_interfaces(self, v4=(), v6=()):
+        v4, v6 = list(v4), list(v6)
+        _check(lib().ebd_set_interfaces(self.h, _nets4(v4), len(v4), _nets6(v6), len(v6)), "ebd_set_interfaces")
+
+    def submit(self, events, lens, offs, payload):
+        events = np.ascontiguousarray(events, dtype=EVENT_DTYPE)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        _check(lib().ebd_submit_batch(self.h, _p(events), _p(lens), _p(offs), _p(payload), payload.size,
+                                      len(events)), "ebd_submit_batch")
+
+    def submit_device(self, events, lens, offs, payload, n):
+        """Device-resident batch (torch tensors on the context's device or raw pointers)."""
+        b = DeviceBatch(events=_ptrval(events), len=_ptrval(lens), off=_ptrval(offs), payload=_ptrval(payload), n=n)
+        _check(lib().ebd_submit_batch_device(self.h, C.byref(b)), "ebd_submit_batch_device")
+
+    def sync(self):
+        _check(lib().ebd_sync(self.h), "ebd_sync")
+
+    def set_seq_base(self, seq):
+        _check(lib().ebd_set_seq_base(self.h, seq), "ebd_set_seq_base")
+
+    def kernel_times(self):
+        """{kernel: (launches, total_ms)} of the HIP-event timed launches (timing=True)."""
+        n = C.c_uint32()
+        _check(lib().ebd_kernel_times(self.h, None, 0, C.byref(n)), "ebd_kernel_times")
+        arr = (KernelTime * n.value)()
+        _check(lib().ebd_kernel_times(self.h, arr, n.value, C.byref(n)), "ebd_kernel_times")
+        return {a.name.decode(): (a.launches, a.total_ms) for a in arr}
+
+    def reset_kernel_times(self):
+        _check(lib().ebd_reset_kernel_times(self.h), "ebd_reset_kernel_times")
+
+    def results(self):
+        n = C.c_uint32()
+        lib().ebd_fetch_results(self.h, None, 0, C.byref(n))
+        out = np.zeros(n.value, RESULT_DTYPE)
+        _check(lib().ebd_fetch_results(self.h, _p(out), n.value, C.byref(n)), "ebd_fetch_results")
+        return out
+
+    def session_requests(self):
+        n, sl = C.c_uint32(), C.c_uint64()
+        _check(lib().ebd_fetch_session_requests(self.h, None, 0, C.byref(n), None, 0, C.byref(sl)), "sreq")
+        out = np.zeros(n.value, SESSION_REQ_DTYPE)
+        buf = np.zeros(max(sl.value, 1), np.uint8)
+        _check(lib().ebd_fetch_session_requests(self.h, _p(out), n.value, C.byref(n), _p(buf), buf.size,
+                                                C.byref(sl)), "ebd_fetch_session_requests")
+        return out, buf[:sl.value].tobytes()
+
+    def services(self, with_seq=False):
+        """[(pid, endpoint, domain, scheme, internal, external)] sorted by (pid, endpoint);
+        with_seq appends the first-arrival sequence number (for cross-shard merges)."""
+        n, sl = C.c_uint32(), C.c_uint64()
+        _check(lib().ebd_collect_services(self.h, None, 0, C.byref(n), None, 0, C.byref(sl)), "collect")
+        out = np.zeros(max(n.value, 1), SERVICE_DTYPE)
+        buf = np.zeros(max(sl.value, 1), np.uint8)
+        _check(lib().ebd_collect_services(self.h, _p(out), out.size, C.byref(n), _p(buf), buf.size, C.byref(sl)),
+               "ebd_collect_services")
+        s = buf.tobytes()
+        res = []
+        for r in out[:n.value]:
+            o, L = int(r["endpoint_off"]), int(r["endpoint_len"])
+            ep = s[o:o + L]
+            dom = ep[int(r["domain_off"]):int(r["domain_off"]) + int(r["domain_len"])]
+            t = (int(r["pid"]), ep, dom, b"https" if r["https"] else b"http", int(r["internal"]), int(r["external"]))
+            res.append(t + (int(r["first_seq"]),) if with_seq else t)
+        res.sort(key=lambda t: (t[0], t[1]))
+        return res
+
+    def clear(self):
+        _check(lib().ebd_clear(self.h), "ebd_clear")
+
+    def stats(self):
+        s = Stats()
+        _check(lib().ebd_get_stats(self.h, C.byref(s)), "ebd_get_stats")
+        d = {k: getattr(s, k) for k, _ in Stats._fields_}
+        d["error_names"] = [v for b, v in ERR_BITS.items() if d["errors"] & b]
+        return d
+
+
+def _ptrval(x):
+    if x is None:
+        return None
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return int(x)
+
+
+def trace_config(config, seed, first, n, align=1):
+    return TraceConfig(config=config, seed=seed, first=first, n=n, align=align)
+
+
+def trace_size(config, seed, first, n, align=1):
+    t = trace_config(config, seed, first, n, align)
+    v = C.c_uint64()
+    _check(lib().ebd_trace_size(C.byref(t), C.byref(v)), "ebd_trace_size")
+    return v.value
+
+
+def generate_host(config, seed, first, n, align=1):
+    """Synthetic trace on the host: (events, lens, offs, payload)."""
+    size = trace_size(config, seed, first, n, align)
+    ev = np.zeros(n, EVENT_DTYPE)
+    lens = np.zeros(n, np.uint32)
+    offs = np.zeros(n, np.uint64)
+    payload = np.zeros(size + 16, np.uint8)
+    t = trace_config(config, seed, first, n, align)
+    _check(lib().ebd_trace_generate_host(C.byref(t), _p(ev), _p(lens), _p(offs), _p(payload), payload.size),
+           "ebd_trace_generate_host")
+    return ev, lens, offs, payload
+
+
+def trace_size_device(ctx, config, seed, first, n, align=1):
+    t = trace_config(config, seed, first, n, align)
+    v = C.c_uint64()
+    _check(lib().ebd_trace_size_device(ctx.h, C.byref(t), C.byref(v)), "ebd_trace_size_device")
+    return v.value
+
+
+def generate_device(ctx, config, seed, first, n, events, lens, offs, payload, payload_cap, align=1):
+    t = trace_config(config, seed, first, n, align)
+    _check(lib().ebd_trace_generate_device(ctx.h, C.byref(t), _ptrval(events), _ptrval(lens), _ptrval(offs),
+                                           _ptrval(payload), payload_cap), "ebd_trace_generate_device")
+
+
+# ---- host hooks (product semantics on the CPU, for tests) -------------------------------
+def dfa_info():
+    a = np.zeros(11, np.uint32)
+    _check(lib().ebd_host_dfa_info(_p(a), 11), "dfa_info")
+    keys = ["nstates", "url_id", "g2", "g3", "g4", "hvc0", "hvh", "fin0", "fin1", "inv", "init"]
+    return dict(zip(keys, (int(x) for x in a)))
+
+
+def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_DATA, src16=bytes(16), v4=(), v6=()):
+    out = np.zeros(1, RESULT_DTYPE)
+    key = np.zeros(2, np.uint64)
+    b = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+    s = np.frombuffer(src16, np.uint8)
+    v4, v6 = list(v4), list(v6)
+    _check(lib().ebd_host_fresh(_p(b), len(buf), pid, flags, _p(s), _nets4(v4), len(v4), _nets6(v6), len(v6),
+                                _p(out), _p(key)), "ebd_host_fresh")
+    return out[0], (int(key[0]), int(key[1]))
+
+
+def host_gp_parse(chunks, flags=FLAG_UNENCRYPTED, reset_between=False):
+    data = b"".join(chunks)
+    d = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
+    cl = np.array([len(c) for c in chunks], np.uint32) if chunks else np.zeros(1, np.uint32)
+    cons = np.zeros(max(len(chunks), 1), np.uint32)
+    o = np.zeros(12, np.uint32)
+    _check(lib().ebd_host_gp_parse(_p(d), _p(cl), len(chunks), flags, int(reset_between), _p(cons), _p(o)),
+           "ebd_host_gp_parse")
+    keys = ["state", "url_start", "url_len", "host_start", "host_len", "cip_start", "cip_len", "f", "cipkey", "mcand",
+            "mlen", "proto"]
+    return [int(x) for x in cons[:len(chunks)]], dict(zip(keys, (int(x) for x in o))), data
+
+
+def host_classify_token(token: bytes, v4=(), v6=()):
+    b = np.frombuffer(token, np.uint8) if token else np.zeros(1, np.uint8)
+    v4, v6 = list(v4), list(v6)
+    return lib().ebd_host_classify(_p(b), len(token), 0, 0, _nets4(v4), len(v4), _nets6(v6), len(v6))
+
+
+def host_classify_source(src16: bytes, flags, v4=(), v6=()):
+    b = np.frombuffer(src16, np.uint8)
+    v4, v6 = list(v4), list(v6)
+    return lib().ebd_host_classify(_p(b), 16, 1, flags, _nets4(v4), len(v4), _nets6(v6), len(v6))
+
+
+def host_pton(text: bytes, af6: bool):
+    b = np.frombuffer(text, np.uint8) if text else np.zeros(1, np.uint8)
+    out = np.zeros(16, np.uint8)
+    ok = lib().ebd_host_pton(1 if af6 else 0, _p(b), len(text), _p(out))
+    return bytes(out[:16 if af6 else 4]) if ok else None

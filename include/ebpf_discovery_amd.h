@@ -1,0 +1,265 @@
+/*
+ * ebpf_discovery_amd.h — C ABI of the MI355X-native HTTP per-event parse path.
+ *
+ * Drop-in boundary for dynatrace-oss/eBPF-Discovery's event-consumer hot path:
+ *   libebpfdiscovery/src/Discovery.cpp:73-198   (drain, per-event dispatch, session LRU)
+ *   libhttpparser/src/HttpRequestParser.cpp:85-409 (per-byte request-line / header scanner)
+ *   libservice/src/Aggregator.cpp:44-181         (per-(pid, endpoint) client counters)
+ *   libservice/src/IpAddressCheckerImpl.cpp:39-180 (internal / external classification)
+ * The reference calls HttpRequestParser::parse once per captured buffer and
+ * Aggregator::newRequest once per finished request; this ABI takes a whole batch of
+ * captured buffers (the packed form of the BPF queue + savedBuffersMap) and runs the
+ * same semantics as hand-written HIP kernels on one GPU.  Plain C types only.
+ *
+ * Errors: 0 on success, a negative errno otherwise (the reference's int convention,
+ * Discovery.cpp:48-58).  An HTTP parse failure is data (EBD_STATUS_INVALID), not an
+ * error.  Nothing throws across this boundary.
+ *
+ * Threading: one submitting thread per context (the reference has one poll thread,
+ * ServiceDetectionTask.cpp:43-49); ebd_collect_services / ebd_clear may be called from
+ * another thread (the reporting thread) and are serialised by the context, like
+ * Aggregator.h:66.  Every call on a context is ordered on the context's private HIP
+ * stream.
+ */
+#ifndef EBPF_DISCOVERY_AMD_H
+#define EBPF_DISCOVERY_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EBD_ABI_VERSION 1
+
+/* --- wire format (libebpfdiscoveryshared/headers/ebpfdiscoveryshared/Types.h) ----- */
+
+/* DiscoveryEvent, Types.h:201-205 — 36 bytes, byte-identical to the BPF record. */
+typedef struct ebd_discovery_event {
+	uint32_t pid;       /* DiscoverySavedBufferKey.pid        @0  */
+	uint32_t fd;        /* .fd                                @4  */
+	uint32_t sessionID; /* .sessionID                         @8  */
+	uint32_t bufferSeq; /* .bufferSeq                         @12 */
+	uint8_t sourceIP[16]; /* DiscoverySockSourceIP            @16 */
+	uint8_t flags;      /* DiscoveryFlags                     @32 */
+	uint8_t pad_[3];
+} ebd_discovery_event;
+
+/* DiscoveryFlags, Types.h:122-129 */
+#define EBD_FLAG_SESSION_IPV4 2
+#define EBD_FLAG_SESSION_IPV6 4
+#define EBD_FLAG_SESSION_UNENCRYPTED_HTTP 8
+#define EBD_FLAG_SESSION_SSL_HTTP 16
+#define EBD_FLAG_EVENT_NEW_DATA 32
+#define EBD_FLAG_EVENT_DATA_END 64
+
+/* Constants.h:19-24 */
+#define EBD_BUFFER_MAX_DATA_SIZE 8192
+#define EBD_MAX_SESSIONS 8192
+#define EBD_MAX_HTTP_REQUEST_LENGTH 8192
+
+/* len[i] == EBD_NO_BUFFER: the NEW_DATA event's saved buffer is missing
+ * (bpf_map_lookup_and_delete_elem failed, Discovery.cpp:103-107). */
+#define EBD_NO_BUFFER 0xffffffffu
+
+/* InterfacesReader.h:15-24, addresses and masks in network byte order (in_addr bytes). */
+typedef struct ebd_ipv4_network {
+	uint8_t addr[4];
+	uint8_t mask[4];
+} ebd_ipv4_network;
+typedef struct ebd_ipv6_network {
+	uint8_t addr[16];
+	uint8_t mask[16];
+} ebd_ipv6_network;
+
+/* --- per-event result (replaces the per-call HttpRequestParser::parse outcome) ------ */
+
+enum {
+	EBD_STATUS_NONE = 0,       /* no parse: DATA_END-only event or missing buffer */
+	EBD_STATUS_UNFINISHED = 1, /* parser waits for more buffers (Discovery.cpp:131-134) */
+	EBD_STATUS_FINISHED = 2,   /* a request was handed to the aggregator */
+	EBD_STATUS_INVALID = 3,    /* HttpRequestParser::isInvalidState() */
+};
+#define EBD_INFO_POST 0x01     /* method POST (else GET) */
+#define EBD_INFO_HTTPS 0x02    /* HttpRequest::isHttps (flags & SSL of the finishing event) */
+#define EBD_INFO_SESSION 0x04  /* produced by the session path: see ebd_event_result.session */
+#define EBD_INFO_CIP 0x08      /* request.clientIp non-empty (cip_* spans the front token) */
+#define EBD_INFO_CLASS_SHIFT 4 /* bits 4-5: 0 not counted, 1 internal, 2 external */
+#define EBD_INFO_EXISTING 0x40 /* parsed by a saved session (Discovery.cpp:123-139) */
+
+/* 16 bytes.  consumed = HttpRequestParser::parse() return value for this buffer.
+ * Fast-path (single-buffer) requests: spans are byte offsets inside this event's
+ * buffer.  EBD_INFO_SESSION requests (spanning several buffers): `session` indexes the
+ * array returned by ebd_fetch_session_requests. */
+typedef struct ebd_event_result {
+	uint16_t consumed;
+	uint8_t status;
+	uint8_t info;
+	union {
+		struct {
+			uint16_t url_off, url_len;
+			uint16_t host_off, host_len;
+			uint16_t cip_off, cip_len;
+		} span;
+		struct {
+			uint32_t index;
+			uint32_t pad_[2];
+		} session;
+	} u;
+} ebd_event_result;
+
+/* A request finished by the session path: strings live in the batch's session string
+ * buffer (ebd_fetch_session_requests): host at str_off, url right after it, then the
+ * client-IP front token. */
+typedef struct ebd_session_request {
+	uint64_t seq; /* global event order of the finishing event */
+	uint32_t pid;
+	uint32_t str_off;  /* host bytes, then url bytes */
+	uint16_t host_len, url_len;
+	uint16_t cip_off;  /* client-IP front token, relative to str_off */
+	uint16_t cip_len;
+	uint8_t info;      /* EBD_INFO_* */
+	uint8_t status;
+	uint16_t pad_;
+	uint32_t pad2_;
+} ebd_session_request; /* 32 bytes */
+
+/* --- services (Service.h:43-66) ------------------------------------------------------ */
+typedef struct ebd_service {
+	uint32_t pid;
+	uint32_t internal_clients; /* uint32, wraps like Service.h:53-54 */
+	uint32_t external_clients;
+	uint8_t https; /* scheme "https" / "http" of the first request that created the key */
+	uint8_t pad_[3];
+	uint64_t endpoint_off; /* into the caller's string buffer */
+	uint32_t endpoint_len;
+	uint32_t domain_off; /* relative to endpoint_off */
+	uint32_t domain_len;
+	uint32_t pad2_;
+	uint64_t first_seq; /* global order of the request that created it (first arrival) */
+} ebd_service; /* 48 bytes */
+
+typedef struct ebd_stats {
+	uint64_t events;            /* events submitted */
+	uint64_t requests;          /* Aggregator::newRequest equivalents */
+	uint64_t session_events;    /* events handled by the session (multi-buffer) path */
+	uint64_t kernel_deletes;    /* bpfDiscoveryDeleteSession equivalents, Discovery.cpp:125-129 */
+	uint64_t live_sessions;     /* saved (LRU) sessions after the last batch */
+	uint64_t max_live_sessions; /* peak saved sessions seen inside any batch */
+	uint64_t services;          /* distinct (pid, endpoint) keys */
+	uint64_t hash_collisions;   /* 64-bit slot tag matched but the 128-bit key did not */
+	uint64_t errors;            /* bitmask of EBD_ERR_* conditions seen */
+} ebd_stats;
+
+#define EBD_ERR_TABLE_FULL 1u      /* service table probe limit reached */
+#define EBD_ERR_ARENA_FULL 2u      /* string arena exhausted */
+#define EBD_ERR_LRU_OVERFLOW 4u    /* > EBD_MAX_SESSIONS live sessions: reference would evict */
+#define EBD_ERR_SESSION_FULL 8u    /* session scratch exhausted */
+#define EBD_ERR_SPIN 16u           /* bounded wait on a slot publication expired */
+#define EBD_ERR_BAD_INPUT 32u      /* len > EBD_BUFFER_MAX_DATA_SIZE, bad offsets */
+
+typedef struct ebd_config {
+	int device;                /* HIP device ordinal */
+	uint32_t max_events;       /* largest batch; device work buffers are sized for it */
+	uint64_t max_payload;      /* largest payload arena (bytes) of a host batch */
+	uint32_t service_capacity; /* service hash slots (power of two, 0 = default 1<<22) */
+	uint64_t string_arena;     /* bytes for service endpoint strings (0 = default 256 MiB) */
+	uint32_t lru_capacity;     /* 0 = EBD_MAX_SESSIONS (Discovery.cpp:39) */
+	uint32_t flags;            /* EBD_CFG_* */
+} ebd_config;
+
+#define EBD_CFG_TIMING 2u /* time every kernel launch with HIP events (ebd_kernel_times) */
+
+typedef struct ebd_ctx ebd_ctx;
+
+/* Device-resident batch: every pointer is a device (HBM) pointer that stays valid
+ * until the next ebd_sync.  payload reads are done in aligned 16-byte blocks, so the
+ * allocation must be readable up to the next 16-byte boundary after each buffer. */
+typedef struct ebd_device_batch {
+	const ebd_discovery_event* events;
+	const uint32_t* len;
+	const uint64_t* off;
+	const uint8_t* payload;
+	uint32_t n;
+} ebd_device_batch;
+
+int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out);
+int ebd_ctx_destroy(ebd_ctx* ctx);
+/* The context's HIP stream (hipStream_t), for callers that time or order work. */
+void* ebd_ctx_stream(ebd_ctx* ctx);
+
+/* IpAddressCheckerImpl's interface list (InterfacesReader::collectAllIpInterfaces,
+ * InterfacesReader.cpp:50-78) — injected, because it is host dependent. */
+int ebd_set_interfaces(ebd_ctx* ctx, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6);
+
+/* One poll cycle (Discovery::fetchAndHandleEvents): events[i] with its saved buffer at
+ * payload + off[i], len[i] bytes (len <= 8192, or EBD_NO_BUFFER).  Host memory: the
+ * batch is staged through pinned memory.  Blocks until the batch is processed. */
+int ebd_submit_batch(ebd_ctx* ctx, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n);
+/* The same with the batch already in HBM.  Asynchronous: enqueued on the context stream. */
+int ebd_submit_batch_device(ebd_ctx* ctx, const ebd_device_batch* batch);
+int ebd_sync(ebd_ctx* ctx);
+/* Global order of the next submitted event (default: events submitted so far).  Shards of
+ * one trace set it to their first global event index so first-arrival ties resolve in
+ * trace order after the cross-GPU merge. */
+int ebd_set_seq_base(ebd_ctx* ctx, uint64_t seq);
+
+/* Per-kernel device time over all launches since the last reset (EBD_CFG_TIMING):
+ * HIP events recorded on the context stream around each launch. */
+typedef struct ebd_kernel_time {
+	char name[24];
+	uint64_t launches;
+	double total_ms;
+} ebd_kernel_time;
+int ebd_kernel_times(ebd_ctx* ctx, ebd_kernel_time* out, uint32_t cap, uint32_t* n);
+int ebd_reset_kernel_times(ebd_ctx* ctx);
+
+/* Per-event results of the last batch (host copy), n <= cap. */
+int ebd_fetch_results(ebd_ctx* ctx, ebd_event_result* out, uint32_t cap, uint32_t* n);
+/* Device pointer to the last batch's per-event results (valid until the next submit). */
+const ebd_event_result* ebd_results_device(ebd_ctx* ctx);
+/* Session-path requests of the last batch and their strings. */
+int ebd_fetch_session_requests(ebd_ctx* ctx, ebd_session_request* out, uint32_t cap, uint32_t* n, char* strings,
+		uint64_t strcap, uint64_t* strlen);
+
+/* Aggregator::collectServices (Aggregator.cpp:170-181): services and their strings.
+ * Call with out == NULL to get the sizes.  Order is unspecified (unordered_map). */
+int ebd_collect_services(ebd_ctx* ctx, ebd_service* out, uint32_t cap, uint32_t* n, char* strings, uint64_t strcap,
+		uint64_t* strlen);
+/* Aggregator::clear (Aggregator.cpp:136-153, network counters off). */
+int ebd_clear(ebd_ctx* ctx);
+int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
+const char* ebd_strerror(int err);
+
+/* --- multi-GPU: compact service table export / merge (RCCL carries the bytes) --------- */
+/* Export this context's services as packed device records for an owner-partitioned
+ * exchange; see ebd_export_* in INTEGRATION.md.  (Round 1: host-side merge helper.) */
+
+/* --- synthetic traces, identical on host and device ---------- */
+typedef struct ebd_trace_config {
+	uint32_t config; /* 1, 2, 3 (single-buffer); 4 (fragmented, keep-alive) */
+	uint64_t seed;
+	uint64_t first;  /* first event index (shards / samples regenerate identically) */
+	uint32_t n;      /* events */
+	uint32_t align;  /* payload offset alignment (power of two, >= 1) */
+	uint32_t pad_;
+} ebd_trace_config;
+
+/* Payload bytes needed for events [first, first + n) of a single-buffer config. */
+int ebd_trace_size(const ebd_trace_config* cfg, uint64_t* payload_bytes);
+/* Host generation into caller arrays (events[n], len[n], off[n], payload). */
+int ebd_trace_generate_host(const ebd_trace_config* cfg, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
+		uint8_t* payload, uint64_t payload_cap);
+/* Payload bytes for a single-buffer config, computed on the context's GPU. */
+int ebd_trace_size_device(ebd_ctx* ctx, const ebd_trace_config* cfg, uint64_t* payload_bytes);
+/* Device generation straight into HBM (pointers are device pointers). */
+int ebd_trace_generate_device(ebd_ctx* ctx, const ebd_trace_config* cfg, ebd_discovery_event* events, uint32_t* len,
+		uint64_t* off, uint8_t* payload, uint64_t payload_cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,53 @@
+"""The C-ABI library loads and exports every function include/*.h declares (CPU only:
+no compute call needs a GPU here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import ebd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in ("ebpf_discovery_amd.h", "ebpf_discovery_amd_testing.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[\w\s\*]+?\b(ebd_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = ebd.lib()
+    names = declared_functions()
+    assert len(names) >= 20
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, missing
+    # and the Python binding types every one of them
+    assert names <= set(ebd._SIGS), sorted(names - set(ebd._SIGS))
+
+
+def test_struct_layouts_match_header():
+    assert ebd.EVENT_DTYPE.itemsize == 36          # DiscoveryEvent, Types.h:201-205
+    assert ebd.RESULT_DTYPE.itemsize == 16
+    assert ebd.SESSION_REQ_DTYPE.itemsize == 32
+    assert ebd.SERVICE_DTYPE.itemsize == 48
+    assert C.sizeof(ebd.Config) == 40
+    assert C.sizeof(ebd.Stats) == 72
+
+
+def test_strerror():
+    assert ebd.lib().ebd_strerror(0) == b"success"
+    assert ebd.lib().ebd_strerror(-22) == b"invalid argument"
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(ebd.EbdError):
+        ebd.Context(max_events=16)

@@ -1,0 +1,181 @@
+"""GPU parity: the HIP path through the C ABI against the oracle on the same inputs.
+
+Bit-exact comparison of per-event parse outcomes (status, consumed bytes, host, url,
+client-IP front token, client class, scheme) and of the service table
+(pid, endpoint, domain, scheme, internal, external)."""
+import socket
+
+import numpy as np
+import pytest
+
+import ebd
+import oracle_py as O
+import traces as T
+
+pytestmark = pytest.mark.gpu
+
+
+def b(s):
+    return s.encode("latin-1")
+
+
+def run_gpu(ev, lens, offs, payload, batches=1, lru=0, v4=(), v6=(), max_events=None):
+    n = len(ev)
+    ctx = ebd.Context(max_events=max_events or max(n, 1), max_payload=payload.size, lru_capacity=lru)
+    if v4 or v6:
+        ctx.set_interfaces(v4, v6)
+    views = []
+    bounds = np.linspace(0, n, batches + 1).astype(int)
+    for a, z in zip(bounds[:-1], bounds[1:]):
+        ctx.submit(ev[a:z], lens[a:z], offs[a:z], payload)
+        res = ctx.results()
+        sreq, sstr = ctx.session_requests()
+        views += T.gpu_view(res, offs[a:z], payload, sreq, sstr)
+    st = ctx.stats()
+    svcs = ctx.services()
+    return views, svcs, st, ctx
+
+
+def run_oracle(ev, lens, offs, payload, lru=8192, v4=(), v6=()):
+    o = O.Oracle(lru_capacity=lru, v4_ifaces=list(v4), v6_ifaces=list(v6))
+    out, blob = o.process(ev, lens, offs, payload)
+    return T.oracle_view(out, blob), o.services(), o.stats()
+
+
+def assert_parity(ev, lens, offs, payload, batches=1, v4=(), v6=()):
+    gv, gs, gst, _ = run_gpu(ev, lens, offs, payload, batches=batches, v4=v4, v6=v6)
+    ov, os_, ost = run_oracle(ev, lens, offs, payload, v4=v4, v6=v6)
+    assert gst["errors"] == 0, gst
+    bad = [i for i in range(len(ov)) if gv[i] != ov[i]]
+    assert not bad, [(i, gv[i], ov[i]) for i in bad[:5]]
+    assert gs == os_
+    assert gst["kernel_deletes"] == ost["kernel_deletes"]
+    assert gst["live_sessions"] == ost["lru_size"]
+    return gv, gs
+
+
+def test_config1_probe(vectors):
+    for case in vectors["config1"]:
+        n = case["n"]
+        lens, offs, payload = T.pack([b(case["payload"])] * n)
+        ev = T.events([dict(sid=i + 1, flags=2 | 8 | 32) for i in range(n)])
+        gv, gs, st, _ = run_gpu(ev, lens, offs, payload)
+        exp = [(s["pid"], b(s["endpoint"]), b(s["domain"]), b(s["scheme"]), s["internal"], s["external"])
+               for s in case["services"]]
+        assert gs == exp
+        assert st["live_sessions"] == case["saved_sessions"]
+
+
+def test_reference_parser_vectors_as_sessions(vectors):
+    cases = vectors["parser_valid"] + vectors["parser_invalid"]
+    chunk_lists = [[b(c) for c in case["chunks"]] for case in cases]
+    ev, lens, offs, payload = T.session_trace(chunk_lists)
+    gv, gs = assert_parity(ev, lens, offs, payload)
+    # per case: total consumed bytes as the reference test expects
+    k = 0
+    for case, chunks in zip(cases, chunk_lists):
+        assert sum(gv[k + j][1] for j in range(len(chunks))) == case["total"], case
+        k += len(chunks)
+
+
+def test_reference_parser_vectors_interleaved_and_closed(vectors):
+    cases = vectors["parser_valid"] + vectors["parser_invalid"] + vectors["probe_parser"][:9]
+    chunk_lists = [[b(c) for c in case["chunks"]] for case in cases]
+    ev, lens, offs, payload = T.session_trace(chunk_lists, interleave=True, close=True)
+    assert_parity(ev, lens, offs, payload)
+
+
+def test_aggregator_vectors_real_checker(vectors):
+    rows, bufs = [], []
+    for k, r in enumerate(vectors["aggregator"]["requests"]):
+        src = b""
+        if r["real_src"]:
+            src = socket.inet_pton(socket.AF_INET6, r["real_src"]) if ":" in r["real_src"] else socket.inet_pton(
+                socket.AF_INET, r["real_src"])
+        rows.append(dict(pid=r["pid"], sid=k + 1, flags=(r["flags"] or 0) | ebd.FLAG_NEW_DATA, src=src))
+        bufs.append(b("GET %s HTTP/1.1\r\nHost: %s\r\n\r\n" % (r["url"], r["host"])))
+    lens, offs, payload = T.pack(bufs)
+    ev = T.events(rows)
+    _, gs, _, _ = run_gpu(ev, lens, offs, payload)
+    exp = sorted((e["pid"], b(e["endpoint"]), b(e["domain"]), b(e["scheme"]), e["internal"], e["external"])
+                 for e in vectors["aggregator"]["expected"])
+    assert gs == exp
+    assert_parity(ev, lens, offs, payload)
+
+
+def test_checker_vectors_through_the_path(vectors):
+    # every IpAddressCheckerTest address as an X-Forwarded-For client (internal expected)
+    addrs = vectors["v4_reserved_internal"] + [t for t, _ in vectors["v6_cases"]] + ["8.8.8.8", "2001:4860::1"]
+    bufs = [b("GET /c HTTP/1.1\r\nHost: h\r\nX-Forwarded-For: %s\r\n\r\n" % a) for a in addrs]
+    lens, offs, payload = T.pack(bufs)
+    ev = T.events([dict(sid=k + 1, flags=2 | 8 | 32) for k in range(len(bufs))])
+    v6i = [(socket.inet_pton(socket.AF_INET6, a), socket.inet_pton(socket.AF_INET6, m))
+           for a, m in vectors["v6_iface"]["v6_ifaces"]]
+    assert_parity(ev, lens, offs, payload, v6=v6i)
+
+
+@pytest.mark.parametrize("align", [1, 16])
+def test_config3_sample_single_and_multi_batch(align):
+    ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 60000, align=align)
+    assert_parity(ev, lens, offs, payload)
+    assert_parity(ev, lens, offs, payload, batches=7)
+
+
+def test_config2_sample():
+    ev, lens, offs, payload = ebd.generate_host(2, 2, 0, 50000)
+    gv, gs = assert_parity(ev, lens, offs, payload)
+    assert len(gs) == 1 and gs[0][1] == b"10.0.0.1:8080/index.html"
+
+
+def test_fragmented_keepalive_sessions():
+    ev, lens, offs, payload = T.fragmented_trace(3000, seed=4, window=256)
+    assert_parity(ev, lens, offs, payload)
+    # the same trace across several batches: sessions carried between polls
+    assert_parity(ev, lens, offs, payload, batches=9)
+
+
+def test_missing_buffers_and_data_end_only():
+    req = b"GET /a HTTP/1.1\r\nHost: h\r\n\r\n"
+    bufs = [req[:10], None, req[10:], None, req, req[:5]]
+    rows = [dict(sid=1, seq=1, flags=42), dict(sid=1, seq=2, flags=42), dict(sid=1, seq=3, flags=42),
+            dict(sid=1, seq=3, flags=64), dict(sid=2, flags=42 | 64), dict(sid=3, flags=42 | 64)]
+    lens, offs, payload = T.pack(bufs)
+    assert_parity(T.events(rows), lens, offs, payload)
+
+
+def test_device_generator_matches_host():
+    import torch
+    n = 20000
+    hev, hl, ho, hp = ebd.generate_host(3, 3, 123, n, align=16)
+    ctx = ebd.Context(max_events=n)
+    dev = torch.device("cuda:0")
+    size = ebd.trace_size(3, 3, 123, n, align=16)
+    e = torch.empty(n * 36, dtype=torch.uint8, device=dev)
+    l_ = torch.empty(n, dtype=torch.int32, device=dev)
+    o_ = torch.empty(n, dtype=torch.int64, device=dev)
+    p_ = torch.zeros(size + 64, dtype=torch.uint8, device=dev)
+    ebd.generate_device(ctx, 3, 3, 123, n, e, l_, o_, p_, p_.numel(), align=16)
+    torch.cuda.synchronize()
+    assert np.array_equal(e.cpu().numpy().view(ebd.EVENT_DTYPE), hev)
+    assert np.array_equal(l_.cpu().numpy().view(np.uint32), hl)
+    assert np.array_equal(o_.cpu().numpy().view(np.uint64), ho)
+    pd = p_.cpu().numpy()
+    for i in range(0, n, 97):
+        a = int(ho[i])
+        assert pd[a:a + int(hl[i])].tobytes() == hp[a:a + int(hl[i])].tobytes()
+    # the device batch path over the HBM-resident trace equals the host path
+    ctx.submit_device(e, l_, o_, p_, n)
+    ctx.sync()
+    g1 = ctx.services()
+    ctx2 = ebd.Context(max_events=n, max_payload=hp.size)
+    ctx2.submit(hev, hl, ho, hp)
+    assert g1 == ctx2.services()
+
+
+def test_large_config3_against_oracle():
+    ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 1_000_000, align=16)
+    gv, gs, st, _ = run_gpu(ev, lens, offs, payload, batches=2)
+    ov, os_, _ = run_oracle(ev, lens, offs, payload)
+    assert st["errors"] == 0 and st["hash_collisions"] == 0
+    assert gs == os_
+    assert gv == ov

@@ -1,0 +1,255 @@
+"""The product's parse semantics (ebd_spec.h / ebd_fresh.h — the code the GPU kernels
+run) executed on the CPU through libebd_amd.so's host hooks, against the oracle and the
+reference vectors.  CPU only."""
+import random
+import socket
+
+import numpy as np
+import pytest
+
+import ebd
+import oracle_py as O
+
+UNENC, SSL = ebd.FLAG_UNENCRYPTED, ebd.FLAG_SSL
+NEW4 = ebd.FLAG_IPV4 | UNENC | ebd.FLAG_NEW_DATA
+ST = {"FINISHED": ebd.STATUS_FINISHED, "INVALID": ebd.STATUS_INVALID}
+GP_STATE = {10: "FINISHED", 11: "INVALID"}
+
+
+def b(s):
+    return s.encode("latin-1")
+
+
+def test_dfa_layout():
+    i = ebd.dfa_info()
+    assert i["nstates"] <= 256
+    assert i["url_id"] < i["g2"] < i["g3"] < i["g4"]
+    assert i["hvc0"] == i["g3"] - 1
+    assert (i["fin0"], i["fin1"], i["inv"]) == (i["g4"], i["g4"] + 1, i["g4"] + 2)
+    assert i["nstates"] == i["g4"] + 3
+
+
+def oracle_single(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=(), v6=()):
+    o = O.Oracle(v4_ifaces=list(v4), v6_ifaces=list(v6))
+    ev = np.zeros(1, O.EVENT_DTYPE)
+    ev["pid"], ev["fd"], ev["sessionID"], ev["bufferSeq"], ev["flags"] = pid, 3, 1, 1, flags
+    ev["sourceIP"][0] = np.frombuffer(src.ljust(16, b"\0"), np.uint8)
+    out, blob = o.process(ev, np.array([len(buf)], np.uint32), np.zeros(1, np.uint64),
+                          np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8))
+    return out[0], blob, o.services()
+
+
+def check_fresh_against_oracle(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=(), v6=()):
+    r, key = ebd.host_fresh(buf, pid, flags, src.ljust(16, b"\0"), v4, v6)
+    o, blob, svcs = oracle_single(buf, flags, src, pid, v4, v6)
+    if o["status"] == O_STATUS_UNF:
+        assert r["status"] == ebd.STATUS_UNFINISHED, buf
+        assert r["consumed"] == len(buf)
+        return
+    assert r["status"] == {2: ebd.STATUS_FINISHED, 3: ebd.STATUS_INVALID}[int(o["status"])], buf
+    assert r["consumed"] == o["consumed"], buf
+    if r["status"] != ebd.STATUS_FINISHED:
+        return
+    host = blob[o["host_off"]:o["host_off"] + o["host_len"]]
+    url = blob[o["url_off"]:o["url_off"] + o["url_len"]]
+    assert buf[r["host_off"]:r["host_off"] + r["host_len"]] == host, buf
+    assert buf[r["url_off"]:r["url_off"] + r["url_len"]] == url, buf
+    assert bool(r["info"] & ebd.INFO_CIP) == bool(o["has_cip"]), buf
+    if o["has_cip"]:
+        cip = blob[o["cip_off"]:o["cip_off"] + o["cip_len"]]
+        assert buf[r["cip_off"]:r["cip_off"] + r["cip_len"]] == cip, buf
+    assert (r["info"] >> 4) & 3 == o["cls"], buf
+    assert bool(r["info"] & ebd.INFO_HTTPS) == bool(o["is_https"])
+
+
+O_STATUS_UNF = 1
+
+
+def test_fresh_reference_vectors(vectors):
+    for case in vectors["parser_valid"] + vectors["parser_invalid"]:
+        if len(case["chunks"]) == 1:
+            check_fresh_against_oracle(b(case["chunks"][0]), flags=NEW4 | (SSL if case.get("is_https") else 0))
+    for case in vectors["probe_parser"]:
+        if "chunks" in case and len(case["chunks"]) == 1:
+            check_fresh_against_oracle(b(case["chunks"][0]))
+
+
+QUIRKS = [
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: , 1.2.3.4\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: 1.2.3.4 , 5.6.7.8\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: [::1]:80\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: [ ::1 ]\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: [::1\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: ::ffff:1.2.3.4\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: 01.2.3.4\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: 1.2.3.4:5:6\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: ,,,\r\n\r\n",
+    b"GET / HTTP/1.1\r\nX-Forwarded-For: \"1.2.3.4\r\n\r\n",
+    b"GET / HTTP/1.1\r\nTrue-Client-IP: 8.8.8.8\r\nX-Forwarded-For: 10.0.0.1\r\n\r\n",
+    b"GET / HTTP/1.1\r\nx-http-client-ip: 2001:db8::1\r\nHost: [fe80::1]:80\r\n\r\n",
+    b"GET / HTTP/1.1\r\nrproxy_remote_address: 9.9.9.9\r\n\r\n",
+    b"GET / HTTP/1.1\r\nRPROXY_REMOTE_ADDRESS_EXTRA: 9.9.9.9\r\n\r\n",
+    b"GET / HTTP/1.1\r\nx-forwarded-forx: 9.9.9.9\r\n\r\n",
+    b"GET / HTTP/1.1\r\nHost: [::1\r\n\r\n",
+    b"GET / HTTP/1.1\r\nHost: a:b:c\r\n\r\n",
+    b"GET / HTTP/1.1\r\nHost : a\r\n\r\n",
+    b"GET / HTTP/1.1\r\n Host: a\r\n\r\n",
+    b"GET / HTTP/1.1\r\nHost:a\r\n\r\n",
+    b"GET /a?b=c&d=%20#x HTTP/1.0\r\n\r\n",
+    b"POST /x HTTP/1.1\r\nContent-Length: 3\r\n\r\nabc",
+    b"GET / HTTP/1.1\r\nFoo\r\n",
+    b"GET / HTTP/1.1\r\nFoo\r\nHost: x\r\n\r\n",
+    b"GET / HTTP/1.1\r\n\r\nGET /b HTTP/1.1\r\n\r\n",
+    b"GET / HTTP/1.1\r\nA: b\r\r\n",
+    b"GET / HTTP/1.1\r\nA: \x80\r\n\r\n",
+    b"GET / HTTP/1.1\r\nA:\t b\r\n\r\n",
+    b"GET / HTTP/1.12\r\n\r\n",
+    b"GET / HTTP/1.\r\n\r\n",
+    b"GE",
+    b"POS",
+    b"",
+    b"GET",
+    b"GET /",
+    b"GET / HTTP/1.1\r\nHost: h\r\nX-Client-IP: 1.1.1.1",
+]
+
+
+def test_fresh_quirks():
+    for buf in QUIRKS:
+        check_fresh_against_oracle(buf)
+        check_fresh_against_oracle(buf, flags=ebd.FLAG_IPV6 | SSL | ebd.FLAG_NEW_DATA, src=bytes(15) + b"\x01")
+
+
+def test_fresh_generated_config3_sample():
+    ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 4000)
+    o = O.Oracle()
+    out, blob = o.process(ev, lens, offs, payload)
+    pay = payload.tobytes()
+    for i in range(len(ev)):
+        buf = pay[int(offs[i]):int(offs[i]) + int(lens[i])]
+        r, _ = ebd.host_fresh(buf, int(ev["pid"][i]), int(ev["flags"][i]), ev["sourceIP"][i].tobytes())
+        assert r["consumed"] == out["consumed"][i], i
+        assert r["status"] == {1: 1, 2: 2, 3: 3}[int(out["status"][i])], i
+        if r["status"] == ebd.STATUS_FINISHED:
+            oh = blob[out["host_off"][i]:out["host_off"][i] + out["host_len"][i]]
+            ou = blob[out["url_off"][i]:out["url_off"][i] + out["url_len"][i]]
+            assert buf[r["host_off"]:r["host_off"] + r["host_len"]] == oh
+            assert buf[r["url_off"]:r["url_off"] + r["url_len"]] == ou
+            assert (r["info"] >> 4) & 3 == out["cls"][i], (i, buf)
+
+
+def test_fresh_random_mutations():
+    rng = random.Random(11)
+    base = [b"GET /p/q?x=1 HTTP/1.1\r\nHost: svc.example.com:80\r\nX-Forwarded-For: 8.8.8.8:9, 10.0.0.1\r\n"
+            b"User-Agent: a b/c\r\nAccept: */*\r\n\r\n",
+            b"POST /up HTTP/1.0\r\nhost: [2001:db8::1]:443\r\ntrue-client-ip: [fd00::5]\r\n\r\nBODY"]
+    alphabet = b"GETPOSH/ :\r\n,.[]-_xX0123456789\x01\x80\t"
+    for _ in range(3000):
+        s = bytearray(rng.choice(base))
+        for _ in range(rng.randint(1, 3)):
+            op = rng.random()
+            k = rng.randrange(len(s))
+            if op < 0.4:
+                s[k] = rng.choice(alphabet)
+            elif op < 0.7:
+                del s[k]
+            else:
+                s.insert(k, rng.choice(alphabet))
+        check_fresh_against_oracle(bytes(s))
+
+
+def test_generic_parser_chunked_vectors(vectors):
+    for case in vectors["parser_valid"] + vectors["parser_invalid"]:
+        chunks = [b(c) for c in case["chunks"]]
+        cons, st, data = ebd.host_gp_parse(chunks, SSL if case.get("is_https") else UNENC)
+        p = O.Parser()
+        ocons = [p.parse(c, SSL if case.get("is_https") else UNENC) for c in chunks]
+        assert cons == ocons, case
+        assert sum(cons) == case["total"]
+        r = p.result()
+        name = {10: "FINISHED", 11: "INVALID"}.get(st["state"])
+        assert (name or "other") == (p.state if p.state in ("FINISHED", "INVALID") else "other")
+        if p.state == "INVALID":
+            continue
+        assert data[st["url_start"]:st["url_start"] + st["url_len"]] == r["url"], case
+        assert data[st["host_start"]:st["host_start"] + st["host_len"]] == r["host"], case
+        if r["client_ip"]:
+            raw = data[st["cip_start"]:st["cip_start"] + st["cip_len"]]
+            assert O.parse_client_ip(raw)[0] == r["client_ip"][0], case
+        method = b"GET"[:st["mlen"]] if st["mcand"] == ord("G") else (b"POST"[:st["mlen"]] if st["mlen"] else b"")
+        assert method == r["method"], case
+
+
+def test_generic_parser_length_cap():
+    for total, state in ((8193, 10), (8194, 11)):
+        req = b"GET /" + b"a" * (total - 18) + b" HTTP/1.1\r\n\r\n"
+        cons, st, _ = ebd.host_gp_parse([req[:8192], req[8192:]])
+        assert st["state"] == state and sum(cons) == 8193
+
+
+def test_generic_parser_sticky_key():
+    first = b"GET / HTTP/1.1\r\nX-Forwarded-For: 1.2.3.4\r\n\r\n"
+    second = b"GET / HTTP/1.1\r\nTrue-Client-IP: 5.6.7.8\r\nx-forwarded-for: 9.9.9.9\r\n\r\n"
+    cons, st, data = ebd.host_gp_parse([first, second], reset_between=True)
+    assert st["state"] == 10
+    base = len(first)  # after reset() stream positions restart at the second request
+    raw = data[base + st["cip_start"]:base + st["cip_start"] + st["cip_len"]]
+    assert raw == b"9.9.9.9"
+
+
+def test_pton_matches_oracle_and_glibc():
+    rng = random.Random(5)
+    alphabet = "0123456789abcdefABCDEF:.[] "
+    cases = ["1.2.3.4", "01.2.3.4", "::", "::1", "::ffff:1.2.3.4", "1:2:3:4:5:6:7:8", "1::2::3", ":1", "1:", "",
+             "2001:db8::1", "::ffff:01.2.3.4", "1.2.3.4.5", "255.255.255.255", "256.1.1.1"]
+    cases += ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 18))) for _ in range(20000)]
+    for t in cases:
+        tb = t.encode()
+        assert ebd.host_pton(tb, False) == O.pton4(tb), t
+        assert ebd.host_pton(tb, True) == O.pton6(tb), t
+
+
+def test_classification_matches_oracle(vectors):
+    o = O.Oracle()
+    for t in vectors["v4_reserved_internal"] + ["8.8.8.8", "200.1.2.3"]:
+        a = socket.inet_pton(socket.AF_INET, t)
+        assert ebd.host_classify_source(a + bytes(12), ebd.FLAG_IPV4) == (2 if o.is_v4_external(a) else 1)
+    for t, exp in vectors["v6_cases"]:
+        a = socket.inet_pton(socket.AF_INET6, t)
+        assert ebd.host_classify_source(a, ebd.FLAG_IPV6) == (2 if exp else 1), t
+    v6i = [(socket.inet_pton(socket.AF_INET6, a), socket.inet_pton(socket.AF_INET6, m))
+           for a, m in vectors["v6_iface"]["v6_ifaces"]]
+    for t, exp in vectors["v6_iface"]["cases"]:
+        a = socket.inet_pton(socket.AF_INET6, t)
+        assert ebd.host_classify_source(a, ebd.FLAG_IPV6, v6=v6i) == (2 if exp else 1), t
+    v4i = [(socket.inet_pton(socket.AF_INET, a), socket.inet_pton(socket.AF_INET, m))
+           for a, m in vectors["v4_iface"]["v4_ifaces"]]
+    for t, exp in vectors["v4_iface"]["cases"]:
+        a = socket.inet_pton(socket.AF_INET, t)
+        assert ebd.host_classify_source(a + bytes(12), ebd.FLAG_IPV4, v4=v4i) == (2 if exp else 1)
+    assert ebd.host_classify_source(bytes(16), 0) == 0
+    assert ebd.host_classify_token(b"1.2.3.4:80") == 2
+    assert ebd.host_classify_token(b"[fd00::1]:80") == 1
+    assert ebd.host_classify_token(b"01.2.3.4") == 0
+
+
+def test_generator_is_deterministic_and_shaped():
+    a = ebd.generate_host(3, 3, 1000, 2000)
+    b_ = ebd.generate_host(3, 3, 1000, 2000)
+    for x, y in zip(a, b_):
+        assert np.array_equal(x, y)
+    # a shard regenerates identically inside a bigger range
+    c = ebd.generate_host(3, 3, 0, 3000)
+    assert np.array_equal(c[0][1000:], a[0])
+    assert np.array_equal(c[1][1000:], a[1])
+    ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 20000)
+    assert 32 <= lens.min() and lens.max() <= 1100
+    assert 230 <= lens.mean() <= 285, lens.mean()
+    assert 0.05 < (ev["flags"] & ebd.FLAG_SSL).astype(bool).mean() < 0.25
+    ev2, l2, o2, p2 = ebd.generate_host(2, 2, 0, 100)
+    assert (l2 == 64).all()
+    assert p2[:64].tobytes() == b"GET /index.html HTTP/1.1\r\nHost: 10.0.0.1:8080\r\nAccept: */*xx\r\n\r\n"
+    ev1, l1, o1, p1 = ebd.generate_host(1, 0, 0, 10)
+    assert (l1 == 35).all() and (ev1["pid"] == 1000).all()
+    _, l16, o16, _ = ebd.generate_host(3, 3, 0, 100, align=16)
+    assert (o16 % 16 == 0).all()
