@@ -22,6 +22,7 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
 hipError_t launch_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt, hipStream_t st);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
@@ -68,6 +69,8 @@ struct ebd_ctx {
 	uint32_t slot_cap = 0;
 	uint32_t* d_new_slots = nullptr;
 	uint32_t new_cap = 0;
+	VerifyRec* d_verify = nullptr;
+	uint32_t verify_cap = 0;
 	uint8_t* d_sarena = nullptr;
 	uint64_t sarena_cap = 0;
 	// per-batch
@@ -116,8 +119,8 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_reps", "k_sset_clear"};
-enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_N };
+		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_N };
 
 static hipEvent_t take_event(ebd_ctx* c) {
 	if (!c->free_events.empty()) {
@@ -168,6 +171,8 @@ static Dev make_dev(ebd_ctx* c) {
 	d.slot_mask = c->slot_cap - 1;
 	d.new_slots = c->d_new_slots;
 	d.new_cap = c->new_cap;
+	d.verify = c->d_verify;
+	d.verify_cap = c->verify_cap;
 	d.sarena = c->d_sarena;
 	d.sarena_cap = c->sarena_cap;
 	d.sset = c->d_sset;
@@ -187,7 +192,7 @@ static Dev make_dev(ebd_ctx* c) {
 }
 
 static void ctx_free(ebd_ctx* c) {
-	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_sarena, c->d_res, c->d_keys,
+	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload};
 	for (void* p : ptrs)
@@ -277,6 +282,8 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
 	c->new_cap = c->max_events < c->slot_cap ? c->max_events : c->slot_cap;
 	CTX_TRY(hipMalloc(&c->d_new_slots, (size_t)c->new_cap * sizeof(uint32_t)));
+	c->verify_cap = c->max_events;
+	CTX_TRY(hipMalloc(&c->d_verify, (size_t)c->verify_cap * sizeof(VerifyRec)));
 	c->sarena_cap = cfg->string_arena ? cfg->string_arena : (256ull << 20);
 	CTX_TRY(hipMalloc(&c->d_sarena, c->sarena_cap));
 	// per-batch buffers
@@ -387,6 +394,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	}
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_REPS, [&] { return launch_reps(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
 	if (c->h_ctr[CTR_DIRTY])
 		HIP_TRY(timed(c, KT_SSET_CLEAR, [&] { return launch_sset_clear(d, c->stream, c->cus); }));
 	if (nslow > 0) {

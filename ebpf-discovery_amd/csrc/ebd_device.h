@@ -31,7 +31,7 @@ struct SSlot {
 	unsigned long long tag;
 	unsigned long long kv; // fd << 32 | pid
 	unsigned int sid;
-	unsigned int ready;
+	unsigned int pad;
 	unsigned int carry; // 1 + index into the carried-session array, 0 = none
 	unsigned int visited;
 };
@@ -69,14 +69,20 @@ enum Ctr : uint32_t {
 	CTR_CARRY_OUT,      // sessions saved for the next batch
 	CTR_DIRTY,          // session-set slots claimed in this batch
 	CTR_INSERTS,        // LRU inserts in this batch
-	CTR_BATCH_END = 8,
-	CTR_SARENA = 8,     // service string arena bytes used
+	CTR_VERIFY,         // deferred service-key verifications
+	CTR_BATCH_END = 9,
+	CTR_SARENA = 9,     // service string arena bytes used
 	CTR_ERRORS,         // EBD_ERR_* bitmask
 	CTR_COLLISIONS,
 	CTR_KDELETES,
 	CTR_REQUESTS,
 	CTR_SESSION_EVENTS,
 	CTR_COUNT = 16,
+};
+
+struct VerifyRec {
+	unsigned long long hi;
+	uint32_t slot, pad;
 };
 
 struct Dev {
@@ -100,6 +106,8 @@ struct Dev {
 	uint32_t slot_mask;
 	uint32_t* new_slots;
 	uint32_t new_cap;
+	VerifyRec* verify;
+	uint32_t verify_cap;
 	uint8_t* sarena;
 	unsigned long long sarena_cap;
 	// session path

@@ -18,63 +18,92 @@
 
 namespace ebd {
 
-constexpr uint32_t kSpinLimit = 1u << 20;
-
 __device__ __forceinline__ void set_error(const Dev& d, unsigned long long bit) { atomicOr(&d.ctr[CTR_ERRORS], bit); }
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Coherent reads of words another workgroup publishes during this launch.  A load (even an
+// agent-scope one) can be served by a stale line of this XCD's L2; an idempotent RMW such
+// as atomicOr(p, 0) may be folded into such a load by the compiler.  A compare-and-swap
+// with an impossible comparand is a real memory-side RMW that never changes the word.
+__device__ __forceinline__ unsigned long long rmw_read(unsigned long long* p) { return atomicCAS(p, ~0ull, ~0ull); }
+__device__ __forceinline__ unsigned int rmw_read(unsigned int* p) { return atomicCAS(p, 0xffffffffu, 0xffffffffu); }
+
 // ---------------------------------------------------------------------------------
 // Service table: open addressing on the 64-bit tag, 128-bit key verified.
+//
+// No lane ever waits for another lane's publication: a same-wave claimer whose publish
+// sits on a divergent loop exit would be scheduled after the waiter (SIMT deadlock).
+// A claimer CASes the tag and stores the second half; a finder compares the second half
+// when it is already visible and otherwise queues (slot, hi) for k_verify, which runs
+// after the inserting kernel.  A mismatch there is reported as EBD_ERR_COLLISION.
 // ---------------------------------------------------------------------------------
 __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, uint32_t cls) {
 	uint32_t idx = (uint32_t)h.lo & d.slot_mask;
+	bool found = false;
 	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
 		Slot* s = d.slots + idx;
 		unsigned long long t = ld_relaxed(&s->tag);
+		bool claimed = false;
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, h.lo);
-			if (t == 0) { // claimed: publish the second key half right away
+			if (t == 0) {
 				atomicExch(&s->hi, h.hi);
 				const unsigned long long k = atomicAdd(&d.ctr[CTR_NEW], 1ull);
 				if (k < d.new_cap)
 					d.new_slots[k] = idx;
 				else
 					set_error(d, EBD_ERR_TABLE_FULL);
-				t = h.lo;
+				claimed = true;
 			}
+		}
+		if (claimed) {
+			found = true;
+			break;
 		}
 		if (t == h.lo) {
 			unsigned long long hi = ld_relaxed(&s->hi);
-			for (uint32_t spin = 0; hi == 0; spin++) {
-				if (spin > kSpinLimit) {
-					set_error(d, EBD_ERR_SPIN);
-					return 0xffffffffu;
+			if (hi == 0)
+				hi = rmw_read(&s->hi);
+			if (hi == 0) { // claimer's store not visible yet: verify after this kernel
+				const unsigned long long k = atomicAdd(&d.ctr[CTR_VERIFY], 1ull);
+				if (k < d.verify_cap) {
+					d.verify[k].slot = idx;
+					d.verify[k].hi = h.hi;
+				} else {
+					set_error(d, EBD_ERR_VERIFY_FULL);
 				}
-				__builtin_amdgcn_s_sleep(2);
-				hi = atomicOr(&s->hi, 0ull);
+				found = true;
+				break;
 			}
 			if (hi == h.hi) {
-				if (cls == CLS_INTERNAL)
-					atomicAdd(&s->internal_clients, 1u);
-				else if (cls == CLS_EXTERNAL)
-					atomicAdd(&s->external_clients, 1u);
-				if (seq < ld_relaxed(&s->min_seq))
-					atomicMin(&s->min_seq, seq);
-				return idx;
+				found = true;
+				break;
 			}
-			atomicAdd(&d.ctr[CTR_COLLISIONS], 1ull);
+			atomicAdd(&d.ctr[CTR_COLLISIONS], 1ull); // same tag, other key: keep probing
 		}
 		idx = (idx + 1) & d.slot_mask;
 	}
-	set_error(d, EBD_ERR_TABLE_FULL);
-	return 0xffffffffu;
+	if (!found) {
+		set_error(d, EBD_ERR_TABLE_FULL);
+		return 0xffffffffu;
+	}
+	Slot* s = d.slots + idx;
+	if (cls == CLS_INTERNAL)
+		atomicAdd(&s->internal_clients, 1u);
+	else if (cls == CLS_EXTERNAL)
+		atomicAdd(&s->external_clients, 1u);
+	if (seq < ld_relaxed(&s->min_seq))
+		atomicMin(&s->min_seq, seq);
+	return idx;
 }
 
 // ---------------------------------------------------------------------------------
-// Session set: (pid, fd, sessionID) -> slot.  96-bit key verified after the tag.
+// Session set: (pid, fd, sessionID) -> slot.  Claimed by a CAS on the 64-bit tag; the
+// full key is stored by the claimer and compared by sset_find in later kernels (a tag
+// shared by two keys is reported as EBD_ERR_COLLISION there).
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ unsigned long long sset_tag(unsigned long long kv, uint32_t sid) {
 	return fmix64(kv ^ ((unsigned long long)sid * 0x9E3779B97F4A7C15ull) ^ 0x5bd1e9955bd1e995ull) | 1ull;
@@ -84,45 +113,33 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
 	const unsigned long long tag = sset_tag(kv, sid);
 	uint32_t idx = (uint32_t)tag & d.sset_mask;
+	int res = -1;
 	for (uint32_t probe = 0; probe <= d.sset_mask; probe++) {
 		SSlot* s = d.sset + idx;
 		unsigned long long t = ld_relaxed(&s->tag);
-		bool mine = false;
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, tag);
 			if (t == 0) {
-				atomicExch(&s->kv, kv);
-				atomicExch(&s->sid, sid);
-				if (carry)
-					atomicExch(&s->carry, carry);
-				__threadfence();
-				atomicExch(&s->ready, 1u);
+				s->kv = kv;
+				s->sid = sid;
 				const unsigned long long k = atomicAdd(&d.ctr[CTR_DIRTY], 1ull);
 				d.dirty[k] = idx;
-				mine = true;
+				t = tag;
 			}
 		}
-		if (mine)
-			return (int)idx;
 		if (t == tag) {
-			for (uint32_t spin = 0; atomicOr(&s->ready, 0u) == 0; spin++) {
-				if (spin > kSpinLimit) {
-					set_error(d, EBD_ERR_SPIN);
-					return -1;
-				}
-				__builtin_amdgcn_s_sleep(2);
-			}
-			__threadfence();
-			if (atomicOr(&s->kv, 0ull) == kv && atomicOr(&s->sid, 0u) == sid) {
-				if (carry)
-					atomicExch(&s->carry, carry);
-				return (int)idx;
-			}
+			res = (int)idx;
+			break;
 		}
 		idx = (idx + 1) & d.sset_mask;
 	}
-	set_error(d, EBD_ERR_SESSION_FULL);
-	return -1;
+	if (res < 0) {
+		set_error(d, EBD_ERR_SESSION_FULL);
+		return -1;
+	}
+	if (carry)
+		d.sset[res].carry = carry;
+	return res;
 }
 
 // Lookup after the inserting kernels finished (plain loads are coherent then).
@@ -135,8 +152,11 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 		const unsigned long long t = s->tag;
 		if (t == 0)
 			return -1;
-		if (t == tag && s->kv == kv && s->sid == sid)
-			return (int)idx;
+		if (t == tag) {
+			if (s->kv == kv && s->sid == sid)
+				return (int)idx;
+			set_error(d, EBD_ERR_COLLISION); // two sessions share a 64-bit tag
+		}
 		idx = (idx + 1) & d.sset_mask;
 	}
 	return -1;
@@ -530,6 +550,14 @@ __global__ void k_reps(Dev d) {
 	}
 }
 
+__global__ void k_verify(Dev d) {
+	const unsigned long long nv = d.ctr[CTR_VERIFY];
+	const uint32_t n = (uint32_t)(nv < d.verify_cap ? nv : d.verify_cap);
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+		if (d.slots[d.verify[k].slot].hi != d.verify[k].hi)
+			set_error(d, EBD_ERR_COLLISION);
+}
+
 __global__ void k_sset_clear(Dev d) {
 	const unsigned long long nd = d.ctr[CTR_DIRTY];
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
@@ -537,7 +565,7 @@ __global__ void k_sset_clear(Dev d) {
 		s->tag = 0;
 		s->kv = 0;
 		s->sid = 0;
-		s->ready = 0;
+		s->pad = 0;
 		s->carry = 0;
 		s->visited = 0;
 	}
@@ -642,6 +670,10 @@ hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
 }
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_reps, dim3(cus * 4), dim3(64), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_verify(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_verify, dim3(cus), dim3(256), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus) {

@@ -21,7 +21,8 @@ NO_BUFFER = 0xFFFFFFFF
 STATUS_NONE, STATUS_UNFINISHED, STATUS_FINISHED, STATUS_INVALID = 0, 1, 2, 3
 INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING = 0x01, 0x02, 0x04, 0x08, 0x40
 CLASS_NONE, CLASS_INTERNAL, CLASS_EXTERNAL = 0, 1, 2
-ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "SPIN", 32: "BAD_INPUT"}
+ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "VERIFY_FULL", 32: "BAD_INPUT",
+            64: "COLLISION"}
 
 EVENT_DTYPE = np.dtype([("pid", "<u4"), ("fd", "<u4"), ("sessionID", "<u4"), ("bufferSeq", "<u4"),
                         ("sourceIP", "u1", (16,)), ("flags", "u1"), ("pad", "u1", (3,))])
@@ -120,6 +121,10 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"libebd_amd.so not built ({LIB_PATH}); run `make -C ebpf-discovery_amd`")
+        try:  # torch ships its own HIP runtime under another file name: load it first so that
+            import torch  # noqa: F401  libebd_amd.so binds to that one (one runtime per process)
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

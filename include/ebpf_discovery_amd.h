@@ -156,8 +156,9 @@ typedef struct ebd_stats {
 #define EBD_ERR_ARENA_FULL 2u      /* string arena exhausted */
 #define EBD_ERR_LRU_OVERFLOW 4u    /* > EBD_MAX_SESSIONS live sessions: reference would evict */
 #define EBD_ERR_SESSION_FULL 8u    /* session scratch exhausted */
-#define EBD_ERR_SPIN 16u           /* bounded wait on a slot publication expired */
+#define EBD_ERR_VERIFY_FULL 16u    /* deferred key-verification list exhausted */
 #define EBD_ERR_BAD_INPUT 32u      /* len > EBD_BUFFER_MAX_DATA_SIZE, bad offsets */
+#define EBD_ERR_COLLISION 64u      /* two keys share a 64-bit tag (results not trusted) */
 
 typedef struct ebd_config {
 	int device;                /* HIP device ordinal */
