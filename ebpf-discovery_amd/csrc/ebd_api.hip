@@ -268,7 +268,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		std::fprintf(stderr, "ebd: DFA construction failed (%d)\n", rc);
 		return fail(-EIO);
 	}
-	const size_t tbytes = (size_t)c->dfa_host->info.nstates * 256;
+	const size_t tbytes = sizeof(c->dfa_host->next);
 	CTX_TRY(hipMalloc(&c->d_dfa, tbytes));
 	CTX_TRY(hipMemcpy(c->d_dfa, c->dfa_host->next, tbytes, hipMemcpyHostToDevice));
 	CTX_TRY(hipMalloc(&c->d_trie, sizeof(KeyTrie)));
@@ -736,6 +736,7 @@ int ebd_host_dfa_info(uint32_t* info, uint32_t n) {
 	}
 	const uint32_t v[11] = {t->info.nstates, t->info.url_id, t->info.g2, t->info.g3, t->info.g4, t->info.hvc0, t->info.hvh,
 			t->info.fin0, t->info.fin1, t->info.inv, t->info.init};
+	(void)t->info.hvc1;
 	for (uint32_t k = 0; k < n && k < 11; k++)
 		info[k] = v[k];
 	return 0;
@@ -787,12 +788,13 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 		return -EINVAL;
 	static Interfaces ifs;
 	fill_ifs(ifs, v4, n4, v6, n6);
-	FreshScan f;
-	fresh_scan_bytes(HostTab{t->next}, t->info, buf, len, f);
+	ScanRec sr;
+	const uint32_t skip = (uint32_t)((uintptr_t)buf & 15u);
+	const uint32_t s = fresh_scan_host(HostTab{t->next}, t->info, buf, skip, len, sr);
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
-	fresh_finalize(t->info, f, buf, pid, flags, src16 ? src16 : zero, ifs, fr);
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, buf, skip, len, pid, flags, src16 ? src16 : zero, ifs, fr);
 	*out = fr.r;
 	if (key) {
 		key[0] = fr.key.lo;

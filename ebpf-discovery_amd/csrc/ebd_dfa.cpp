@@ -207,51 +207,71 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 			return gx < gy;
 		return rank(states[x]) < rank(states[y]);
 	});
-	std::vector<int> newid(n);
-	for (int i = 0; i < n; i++)
-		newid[order[i]] = i;
+	// HV(client) states leave their groups for ids 254 / 255
+	std::vector<int> newid(n, -1);
+	int next_id = 0, hvc_seen = 0;
+	for (int i = 0; i < n; i++) {
+		const AState& a = states[order[i]];
+		if (a.state == ST_HDR_VAL && a.kt == KT_CLIENT0) {
+			newid[order[i]] = a.host ? 255 : 254;
+			hvc_seen++;
+		} else {
+			newid[order[i]] = next_id++;
+		}
+	}
+	if (hvc_seen != 2 || next_id > 254)
+		return -2;
 
 	std::memset(out, 0, sizeof(*out));
 	DfaInfo& in = out->info;
-	in.nstates = (uint32_t)n;
+	in.nstates = 256;
 	in.init = (uint32_t)newid[0];
-	int first_in_group[5] = {-1, -1, -1, -1, -1};
+	in.url_id = in.g2 = in.g3 = in.g4 = in.hvh = in.fin0 = in.fin1 = in.inv = 0xffffffffu;
+	in.hvc0 = 254;
+	in.hvc1 = 255;
 	for (int i = 0; i < n; i++) {
-		int g = group(states[order[i]]);
-		if (first_in_group[g] < 0)
-			first_in_group[g] = i;
-	}
-	in.g2 = (uint32_t)first_in_group[2];
-	in.g3 = (uint32_t)first_in_group[3];
-	in.g4 = (uint32_t)first_in_group[4];
-	in.url_id = in.hvc0 = in.hvh = in.fin0 = in.fin1 = in.inv = 0xffffffffu;
-	for (int i = 0; i < n; i++) {
-		const AState& a = states[order[i]];
+		const AState& a = states[i];
+		const uint32_t id = (uint32_t)newid[i];
+		if (id >= 254)
+			continue;
 		if (a.state == ST_URL)
-			in.url_id = (uint32_t)i;
-		if (a.state == ST_HDR_VAL && a.kt == KT_CLIENT0 && !a.host)
-			in.hvc0 = (uint32_t)i;
+			in.url_id = id;
 		if (a.state == ST_HDR_VAL && a.kt == KT_HOST && a.host)
-			in.hvh = (uint32_t)i;
+			in.hvh = id;
 		if (a.state == ST_FINISHED)
-			(a.host ? in.fin1 : in.fin0) = (uint32_t)i;
+			(a.host ? in.fin1 : in.fin0) = id;
 		if (a.state == ST_INVALID)
-			in.inv = (uint32_t)i;
+			in.inv = id;
 	}
-	// Layout checks the kernel relies on.
-	if (in.url_id + 1 != (uint32_t)first_in_group[1] || in.hvc0 + 1 != in.g3 || in.fin0 != in.g4 || in.fin1 != in.g4 + 1 ||
-			in.inv != in.g4 + 2 || (uint32_t)n != in.g4 + 3 || in.hvh == 0xffffffffu)
-		return -3;
-	const AState& hv1 = states[order[in.g3]];
-	if (!(hv1.state == ST_HDR_VAL && hv1.kt == KT_CLIENT0 && hv1.host))
-		return -4;
+	uint32_t first[5] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 	for (int i = 0; i < n; i++) {
-		const int gi = group(states[order[i]]);
+		const uint32_t id = (uint32_t)newid[i];
+		if (id >= 254)
+			continue;
+		const int g = group(states[i]);
+		if (id < first[g])
+			first[g] = id;
+	}
+	in.g2 = first[2];
+	in.g3 = first[3];
+	in.g4 = first[4];
+	if (in.url_id + 1 != first[1] || in.fin0 != in.g4 || in.fin1 != in.g4 + 1 || in.inv != in.g4 + 2 ||
+			(uint32_t)next_id != in.g4 + 3 || in.hvh == 0xffffffffu)
+		return -3;
+	auto group_of_id = [&](int i) {
+		const AState& a = states[i];
+		return group(a);
+	};
+	for (int row = 0; row < 256; row++)
+		for (int b = 0; b < 256; b++)
+			out->next[row * 256 + b] = (uint8_t)in.inv; // unreachable rows
+	for (int i = 0; i < n; i++) {
+		const int gi = group_of_id(i);
 		for (int b = 0; b < 256; b++) {
-			const int j = newid[trans[order[i]][b]];
-			if (group(states[order[j]]) < gi)
+			const int j = trans[i][b];
+			if (group_of_id(j) < gi)
 				return -5;
-			out->next[i * 256 + b] = (uint8_t)j;
+			out->next[newid[i] * 256 + b] = (uint8_t)newid[j];
 		}
 	}
 	return 0;

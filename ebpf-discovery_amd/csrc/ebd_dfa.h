@@ -4,14 +4,18 @@
 // search, every state the generic parser (ebd_spec.h gp_step, the restatement of
 // HttpRequestParser.cpp:124-364) can reach from reset, projected onto what decides
 // future transitions of a fresh parser, and records the projected transition for
-// every byte value.  State ids are then laid out in "phase groups" so the kernel can
-// recover spans with counters:
+// every byte value.  State ids are then laid out in "phase groups" (see DESIGN.md):
 //   G0 [0, url_id]        METHOD progress, SPACE_BEFORE_URL, URL (url_id last)
 //   G1 (url_id, g2)       SPACE_BEFORE_PROTOCOL, PROTOCOL progress
-//   G2 [g2, g3)           header section, Host not seen yet; HV(client) last (= hvc0)
-//   G3 [g3, g4)           header section, Host seen; HV(client) first (= g3), HV(host) = hvh
-//   G4 [g4, nstates)      FINISHED (no host), FINISHED (host), INVALID
-// Transitions never go to a lower group.
+//   G2 [g2, g3)           header section, Host not seen yet
+//   G3 [g3, g4)           header section, Host seen; HV(host) = hvh
+//   G4 = [g4, g4 + 3)     FINISHED (no host), FINISHED (host), INVALID
+//   254, 255              HV(client) without / with Host seen (hvc0, hvc1): one compare
+//                         (s >= 254) tells "inside a client-IP header value"
+// Rows between the used ids and 254 are unreachable (filled with INVALID).
+// Phases are monotone: the group of the state never decreases (HV(client) counts as the
+// header group of its world), which lets the kernel find every span from per-chunk
+// crossings and a 16-byte rescan.
 #pragma once
 
 #include "ebd_spec.h"
@@ -21,7 +25,8 @@ namespace ebd {
 struct DfaInfo {
 	uint32_t nstates;
 	uint32_t url_id, g2, g3, g4;
-	uint32_t hvc0, hvh;            // HV(client, no host) = g3 - 1, HV(host) in G3
+	uint32_t hvc0, hvh;            // HV(client, no host) = 254, HV(host) in G3
+	uint32_t hvc1;                 // HV(client, host seen) = 255
 	uint32_t fin0, fin1, inv;
 	uint32_t init;                 // reset state (METHOD, empty)
 };

@@ -163,67 +163,165 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 }
 
 // ---------------------------------------------------------------------------------
-// k_fresh: one lane per event, DFA table in LDS, 16-byte aligned loads of the buffer.
+// k_fresh: one lane per event, DFA table in LDS.
+//
+// A workgroup takes tiles of kTile events and counting-sorts each tile by its number of
+// 16-byte chunks (LDS histogram), so a wave scans 64 buffers of nearly equal length and
+// its lanes finish together.  Buffers are read with 16-byte global loads, one chunk ahead.
+// Per byte: extract, table step, one wave ballot (client-IP value state); per chunk: the
+// crossing trackers of ebd_fresh.h.
 // ---------------------------------------------------------------------------------
 struct LdsTable {
 	const uint8_t* t;
 	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
 };
 
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void k_fresh(Dev d) {
-	extern __shared__ __attribute__((aligned(16))) uint8_t T[];
-	const uint32_t tb = d.di.nstates * 256u;
-	for (uint32_t k = threadIdx.x * 16u; k < tb; k += BLOCK * 16u)
-		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
-	__syncthreads();
-	const DfaInfo di = d.di;
-	const LdsTable tab{T};
-	for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < d.n; i += gridDim.x * BLOCK) {
-		const uint8_t* evb = (const uint8_t*)(d.ev + i);
-		const uint8_t flags = evb[32];
-		const uint32_t L = d.len[i];
-		FreshResult fr;
-		fr.r.consumed = 0;
-		fr.r.status = EBD_STATUS_NONE;
-		fr.r.info = 0;
-		fr.r.u.session.index = 0;
-		fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
-		if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER) {
-			if (L > EBD_BUFFER_MAX_DATA_SIZE) {
-				set_error(d, EBD_ERR_BAD_INPUT);
-			} else {
-				const uint8_t* p = d.payload + d.off[i];
-				const uintptr_t pa = (uintptr_t)p;
-				const uint4* q = (const uint4*)(pa & ~(uintptr_t)15);
-				const int skip = (int)(pa & 15);
-				const int end = skip + (int)L;
-				FreshScan f;
-				fresh_init(di, f);
-				for (int base = 0; base < end; base += 16) {
-					const uint4 w = q[base >> 4];
-					const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+// 16-byte load through a global (not flat) pointer: global_load_dwordx4
+__device__ __forceinline__ uint4 gload16(uintptr_t a) {
+	const v4u v = *(const __attribute__((address_space(1))) v4u*)a;
+	return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+constexpr int kFreshThreads = 1024;
+constexpr int kTile = 4096;
+constexpr int kBins = 128;
+constexpr size_t kFreshLds = 65536 + kTile * 2 + kBins * 4;
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& w, int k) {
+	const uint32_t x = k < 4 ? w.x : k < 8 ? w.y : k < 12 ? w.z : w.w;
+	return __builtin_amdgcn_ubfe(x, (k & 3) * 8, 8);
+}
+
+__device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
+	const uint8_t flags = ((const uint8_t*)(d.ev + i))[32];
+	const uint32_t L = d.len[i];
+	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || L > EBD_BUFFER_MAX_DATA_SIZE)
+		return 0;
+	const uint32_t skip = (uint32_t)(d.off[i] + (uintptr_t)d.payload) & 15u;
+	const uint32_t ch = (skip + L + 15) >> 4;
+	return ch < kBins ? ch : kBins - 1;
+}
+
+__device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint32_t i) {
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint8_t flags = evb[32];
+	const uint32_t L = d.len[i];
+	FreshResult fr;
+	fr.r.consumed = 0;
+	fr.r.status = EBD_STATUS_NONE;
+	fr.r.info = 0;
+	fr.r.u.session.index = 0;
+	fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
+	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER) {
+		if (L > EBD_BUFFER_MAX_DATA_SIZE) {
+			set_error(d, EBD_ERR_BAD_INPUT);
+		} else {
+			const DfaInfo& di = d.di;
+			const uint8_t* p = d.payload + d.off[i];
+			const uintptr_t pa = (uintptr_t)p;
+			const uintptr_t q = pa & ~(uintptr_t)15;
+			const uint32_t skip = (uint32_t)(pa & 15);
+			const uint32_t end = skip + L;
+			const uint32_t nch = (end + 15) >> 4;
+			ScanRec sr;
+			rec_init(sr);
+			uint32_t s = di.init;
+			uint4 cur = make_uint4(0, 0, 0, 0);
+			if (nch)
+				cur = gload16(q);
+			const uint32_t lane = __lane_id();
+			for (uint32_t c = 0; c < nch; c++) {
+				uint4 nxt = cur;
+				if (c + 1 < nch)
+					nxt = gload16(q + 16 * (uintptr_t)(c + 1));
+				const uint32_t s0 = s;
+				unsigned long long hits = 0;
+				const bool full = (c > 0 || skip == 0) && c * 16 + 16 <= end;
+				if (__all(full)) {
 #pragma unroll
 					for (int k = 0; k < 16; k++) {
-						const int pos = base + k - skip;
-						const bool v = (uint32_t)pos < L;
-						fresh_byte(tab, di, f, (ws[k >> 2] >> ((k & 3) * 8)) & 0xffu, pos, v);
+						s = T[(s << 8) | byte_of(cur, k)];
+						hits |= __ballot(s >= 254);
 					}
-					if (f.s >= di.g4)
-						break;
+				} else {
+#pragma unroll
+					for (int k = 0; k < 16; k++) {
+						const uint32_t pos = c * 16 + k;
+						const bool v = pos >= skip && pos < end;
+						const uint32_t sn = T[(s << 8) | byte_of(cur, k)];
+						hits |= __ballot(v && sn >= 254);
+						s = v ? sn : s;
+					}
 				}
-				const uint32_t pid = *(const uint32_t*)evb;
-				fresh_finalize(di, f, p, pid, flags, evb + 16, *d.ifs, fr);
-				if (fr.r.status == EBD_STATUS_FINISHED) {
-					d.keys[i] = fr.key;
-				} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
-					// the session may be saved (Discovery.cpp:148-150): sequential path
-					atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-					sset_insert(d, pid, *(const uint32_t*)(evb + 4), *(const uint32_t*)(evb + 8), 0);
-				}
+				if (chunk_track(di, sr, c, s0, s, (hits >> lane) & 1ull))
+					break;
+				cur = nxt;
+			}
+			fresh_finalize(LdsTable{T}, di, sr, s, p, skip, L, *(const uint32_t*)evb, flags, evb + 16, *d.ifs, fr);
+			if (fr.r.status == EBD_STATUS_FINISHED) {
+				d.keys[i] = fr.key;
+			} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+				// the session may be saved (Discovery.cpp:148-150): sequential path
+				atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+				sset_insert(d, *(const uint32_t*)evb, *(const uint32_t*)(evb + 4), *(const uint32_t*)(evb + 8), 0);
 			}
 		}
-		d.res[i] = fr.r;
+	}
+	d.res[i] = fr.r;
+}
+
+__global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
+	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+	uint8_t* T = lds;
+	uint16_t* perm = (uint16_t*)(lds + 65536);
+	uint32_t* hist = (uint32_t*)(lds + 65536 + kTile * 2);
+	for (uint32_t k = threadIdx.x * 16u; k < 65536u; k += kFreshThreads * 16u)
+		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	constexpr int kPer = kTile / kFreshThreads;
+	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
+	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+		const uint32_t base = tile * kTile;
+		const uint32_t cnt = d.n - base < (uint32_t)kTile ? d.n - base : (uint32_t)kTile;
+		__syncthreads(); // previous tile's perm fully consumed; table loaded
+		if (threadIdx.x < kBins)
+			hist[threadIdx.x] = 0;
+		__syncthreads();
+		uint32_t bin[kPer], rank[kPer];
+#pragma unroll
+		for (int k = 0; k < kPer; k++) {
+			const uint32_t t = threadIdx.x + k * kFreshThreads;
+			bin[k] = t < cnt ? event_bin(d, base + t) : 0;
+			rank[k] = t < cnt ? atomicAdd(&hist[bin[k]], 1u) : 0;
+		}
+		__syncthreads();
+		if (wave == 0) { // exclusive scan of the 128 bins, two per lane
+			const uint32_t a = hist[2 * lane], b = hist[2 * lane + 1];
+			uint32_t x = a + b;
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint32_t y = __shfl_up(x, o);
+				if ((int)lane >= o)
+					x += y;
+			}
+			const uint32_t excl = x - a - b;
+			hist[2 * lane] = excl;
+			hist[2 * lane + 1] = excl + a;
+		}
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < kPer; k++) {
+			const uint32_t t = threadIdx.x + k * kFreshThreads;
+			if (t < cnt)
+				perm[hist[bin[k]] + rank[k]] = (uint16_t)t;
+		}
+		__syncthreads();
+		for (uint32_t g = wave; g * 64 < cnt; g += kFreshThreads / 64) {
+			const uint32_t t = g * 64 + lane;
+			if (t < cnt)
+				fresh_event(d, T, base + perm[t]);
+		}
 	}
 }
 
@@ -640,12 +738,10 @@ static int grid_for(uint64_t items, int block, int cap) {
 	return (int)(g > (uint64_t)cap ? cap : g);
 }
 
-constexpr int kFreshBlock = 256;
-
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
-	const size_t lds = (size_t)d.di.nstates * 256;
-	const int grid = grid_for(d.n, kFreshBlock, cus * 8);
-	hipLaunchKernelGGL(k_fresh<kFreshBlock>, dim3(grid), dim3(kFreshBlock), lds, st, d);
+	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
+	const int grid = (int)(ntiles < (uint32_t)cus * 2 ? ntiles : (uint32_t)cus * 2);
+	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), kFreshLds, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_carry_insert(const Dev& d, hipStream_t st) {
