@@ -20,6 +20,7 @@ hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_cip(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
@@ -77,6 +78,7 @@ struct ebd_ctx {
 	uint32_t max_events = 0;
 	ebd_event_result* d_res = nullptr;
 	Hash128* d_keys = nullptr;
+	uint32_t* d_cipq = nullptr;
 	SSlot* d_sset = nullptr;
 	uint32_t sset_cap = 0;
 	uint32_t* d_dirty = nullptr;
@@ -119,8 +121,8 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify"};
-enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_N };
+		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify", "k_cip"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_CIP, KT_N };
 
 static hipEvent_t take_event(ebd_ctx* c) {
 	if (!c->free_events.empty()) {
@@ -167,6 +169,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.ifs = c->d_ifs;
 	d.res = c->d_res;
 	d.keys = c->d_keys;
+	d.cipq = c->d_cipq;
 	d.slots = c->d_slots;
 	d.slot_mask = c->slot_cap - 1;
 	d.new_slots = c->d_new_slots;
@@ -192,7 +195,7 @@ static Dev make_dev(ebd_ctx* c) {
 }
 
 static void ctx_free(ebd_ctx* c) {
-	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
+	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys, c->d_cipq,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload};
 	for (void* p : ptrs)
@@ -290,6 +293,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	const uint64_t n = c->max_events;
 	CTX_TRY(hipMalloc(&c->d_res, n * sizeof(ebd_event_result)));
 	CTX_TRY(hipMalloc(&c->d_keys, n * sizeof(Hash128)));
+	CTX_TRY(hipMalloc(&c->d_cipq, n * sizeof(uint32_t)));
 	const uint32_t lru = cfg->lru_capacity ? cfg->lru_capacity : EBD_MAX_SESSIONS;
 	c->carry_cap = lru;
 	c->sset_cap = next_pow2(2 * (n + lru));
@@ -392,6 +396,8 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		if (c->n_carry)
 			HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
 	}
+	if (c->h_ctr[CTR_CIPQ])
+		HIP_TRY(timed(c, KT_CIP, [&] { return launch_cip(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_REPS, [&] { return launch_reps(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
@@ -488,7 +494,7 @@ int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32
 		HIP_TRY(hipMalloc(&c->d_len, (size_t)c->max_events * sizeof(uint32_t)));
 		HIP_TRY(hipMalloc(&c->d_off, (size_t)c->max_events * sizeof(uint64_t)));
 	}
-	const uint64_t need = payload_bytes + 16;
+	const uint64_t need = payload_bytes + EBD_PAYLOAD_PAD;
 	if (need > c->payload_cap) {
 		if (c->d_payload)
 			HIP_TRY(hipFree(c->d_payload));
@@ -779,6 +785,29 @@ struct HostTab {
 	uint32_t operator[](uint32_t i) const { return t[i]; }
 };
 
+// fresh_finalize's buffer access on the host: bytes outside the buffer read as 0 (the
+// device reads whatever follows; those bytes are masked off either way).
+struct HostMem {
+	const uint8_t* p;
+	uint32_t skip, L;
+	Chunk chunk(uint32_t c) const {
+		Chunk ch{};
+		for (uint32_t k = 0; k < 16; k++) {
+			const int pos = (int)(c * 16 + k) - (int)skip;
+			if (pos >= 0 && (uint32_t)pos < L)
+				ch.w[k >> 2] |= (uint32_t)p[pos] << (8 * (k & 3));
+		}
+		return ch;
+	}
+	unsigned long long ld8(uint32_t o) const {
+		unsigned long long v = 0;
+		for (uint32_t b = 0; b < 8; b++)
+			if (o + b < L)
+				v |= (unsigned long long)p[o + b] << (8 * b);
+		return v;
+	}
+};
+
 int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags, const uint8_t* src16,
 		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, ebd_event_result* out,
 		uint64_t key[2]) {
@@ -794,7 +823,16 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
-	fresh_finalize(HostTab{t->next}, t->info, sr, s, buf, skip, len, pid, flags, src16 ? src16 : zero, ifs, fr);
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, HostMem{buf, skip, len}, skip, len, pid, flags, src16 ? src16 : zero,
+			ifs, fr);
+	if (fr.cip) { // what k_cip does for this event
+		uint32_t tb, te;
+		uint8_t cls;
+		cip_token(ifs, [buf](uint32_t b) { return (uint32_t)buf[b]; }, fr.r.u.span.cip_off, fr.r.consumed, &tb, &te, &cls);
+		fr.r.u.span.cip_off = (uint16_t)tb;
+		fr.r.u.span.cip_len = (uint16_t)(te - tb);
+		fr.r.info = (uint8_t)(fr.r.info | (cls << EBD_INFO_CLASS_SHIFT));
+	}
 	*out = fr.r;
 	if (key) {
 		key[0] = fr.key.lo;
@@ -835,6 +873,18 @@ int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t
 	uint32_t tb, te;
 	front_token(token, len, &tb, &te);
 	return classify_token(ifs, token + tb, te - tb);
+}
+
+int ebd_host_endpoint_key(uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]) {
+	if (!key || (len && !endpoint))
+		return -EINVAL;
+	KeyHasher kh;
+	kh.init(pid);
+	kh.bytes(endpoint, len);
+	const Hash128 h = kh.finish();
+	key[0] = h.lo;
+	key[1] = h.hi;
+	return 0;
 }
 
 int ebd_host_pton(int af6, const uint8_t* text, uint32_t len, uint8_t* out) {

@@ -177,20 +177,40 @@ struct LdsTable {
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64a1 __attribute__((aligned(1)));
 // 16-byte load through a global (not flat) pointer: global_load_dwordx4
-__device__ __forceinline__ uint4 gload16(uintptr_t a) {
+__device__ __forceinline__ Chunk gload16(uintptr_t a) {
 	const v4u v = *(const __attribute__((address_space(1))) v4u*)a;
-	return make_uint4(v.x, v.y, v.z, v.w);
+	Chunk c;
+	c.w[0] = v.x;
+	c.w[1] = v.y;
+	c.w[2] = v.z;
+	c.w[3] = v.w;
+	return c;
 }
+// 8 bytes at any alignment: global_load_dwordx2 (gfx950 runs in unaligned-access mode)
+__device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
+	return *(const __attribute__((address_space(1))) u64a1*)a;
+}
+
+// Buffer access for fresh_finalize on the device.  The payload must stay readable up to
+// the next 16-byte boundary after each buffer plus 8 bytes (ebd_api.hip pads it).
+struct DevMem {
+	const uint8_t* p;
+	uintptr_t q; // p rounded down to 16
+	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16(q + 16 * (uintptr_t)c); }
+	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
+};
 
 constexpr int kFreshThreads = 1024;
 constexpr int kTile = 4096;
 constexpr int kBins = 128;
 constexpr size_t kFreshLds = 65536 + kTile * 2 + kBins * 4;
 
-__device__ __forceinline__ uint32_t byte_of(const uint4& w, int k) {
-	const uint32_t x = k < 4 ? w.x : k < 8 ? w.y : k < 12 ? w.z : w.w;
-	return __builtin_amdgcn_ubfe(x, (k & 3) * 8, 8);
+// (s << 8) | byte k of w in one v_perm_b32: result byte 0 = byte (k & 3) of w,
+// byte 1 = byte 0 of s, bytes 2-3 = 0.
+__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t w, int k) {
+	return __builtin_amdgcn_perm(s, w, 0x0c0c0400u | (uint32_t)(k & 3));
 }
 
 __device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
@@ -203,6 +223,27 @@ __device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
 	return ch < kBins ? ch : kBins - 1;
 }
 
+// 16 DFA steps over one chunk; m collects the maximum next state.
+template <bool kFull>
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t pos0,
+		uint32_t skip, uint32_t end) {
+#pragma unroll
+	for (int k = 0; k < 16; k++) {
+		const uint32_t sn = T[tab_index(s, w.w[k >> 2], k)];
+		if (kFull) {
+			s = sn;
+			if (k & 1)
+				m = max(m, s);
+			else
+				m = max(m, sn); // pairs fold into v_max3
+		} else {
+			const bool v = pos0 + k >= skip && pos0 + k < end;
+			s = v ? sn : s;
+			m = max(m, v ? sn : 0u);
+		}
+	}
+}
+
 __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint32_t i) {
 	const uint8_t* evb = (const uint8_t*)(d.ev + i);
 	const uint8_t flags = evb[32];
@@ -213,6 +254,7 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 	fr.r.info = 0;
 	fr.r.u.session.index = 0;
 	fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
+	fr.cip = false;
 	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER) {
 		if (L > EBD_BUFFER_MAX_DATA_SIZE) {
 			set_error(d, EBD_ERR_BAD_INPUT);
@@ -225,40 +267,39 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 			const uint32_t end = skip + L;
 			const uint32_t nch = (end + 15) >> 4;
 			ScanRec sr;
-			rec_init(sr);
+			rec_init(di, sr);
 			uint32_t s = di.init;
-			uint4 cur = make_uint4(0, 0, 0, 0);
-			if (nch)
-				cur = gload16(q);
-			const uint32_t lane = __lane_id();
+			// three chunks in flight ahead of the one being scanned
+			Chunk w0 = gload16(q), w1 = w0, w2 = w0;
+			if (nch > 1)
+				w1 = gload16(q + 16);
+			if (nch > 2)
+				w2 = gload16(q + 32);
 			for (uint32_t c = 0; c < nch; c++) {
-				uint4 nxt = cur;
-				if (c + 1 < nch)
-					nxt = gload16(q + 16 * (uintptr_t)(c + 1));
+				Chunk w3 = w2;
+				if (c + 3 < nch)
+					w3 = gload16(q + 16 * (uintptr_t)(c + 3));
 				const uint32_t s0 = s;
-				unsigned long long hits = 0;
-				const bool full = (c > 0 || skip == 0) && c * 16 + 16 <= end;
-				if (__all(full)) {
-#pragma unroll
-					for (int k = 0; k < 16; k++) {
-						s = T[(s << 8) | byte_of(cur, k)];
-						hits |= __ballot(s >= 254);
-					}
-				} else {
-#pragma unroll
-					for (int k = 0; k < 16; k++) {
-						const uint32_t pos = c * 16 + k;
-						const bool v = pos >= skip && pos < end;
-						const uint32_t sn = T[(s << 8) | byte_of(cur, k)];
-						hits |= __ballot(v && sn >= 254);
-						s = v ? sn : s;
-					}
-				}
-				if (chunk_track(di, sr, c, s0, s, (hits >> lane) & 1ull))
+				uint32_t m = 0;
+				const bool full = c * 16 >= skip && c * 16 + 16 <= end;
+				if (__all(full))
+					scan_chunk<true>(T, w0, s, m, c * 16, skip, end);
+				else
+					scan_chunk<false>(T, w0, s, m, c * 16, skip, end);
+				if (st_terminal(di, s)) {
+					sr.term = (c << 8) | s0;
+					sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
 					break;
-				cur = nxt;
+				}
+				chunk_track(di, sr, c, s, m >= 254);
+				w0 = w1;
+				w1 = w2;
+				w2 = w3;
 			}
-			fresh_finalize(LdsTable{T}, di, sr, s, p, skip, L, *(const uint32_t*)evb, flags, evb + 16, *d.ifs, fr);
+			const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP
+			uint8_t src[16];
+			__builtin_memcpy(src, &sv, 16);
+			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q}, skip, L, *(const uint32_t*)evb, flags, src, *d.ifs, fr);
 			if (fr.r.status == EBD_STATUS_FINISHED) {
 				d.keys[i] = fr.key;
 			} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
@@ -269,6 +310,10 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 		}
 	}
 	d.res[i] = fr.r;
+	if (fr.cip) {
+		const unsigned long long k = atomicAdd(&d.ctr[CTR_CIPQ], 1ull);
+		d.cipq[k] = i; // capacity n: at most one entry per event
+	}
 }
 
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
@@ -322,6 +367,54 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 			if (t < cnt)
 				fresh_event(d, T, base + perm[t]);
 		}
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// k_cip: client-IP token and class for the fast-path requests that carry a client-IP
+// header (queued by k_fresh).  Each lane copies the value's first kCipRaw bytes into its
+// own LDS row with 8-byte loads, then runs front_token / inet_pton there.
+// ---------------------------------------------------------------------------------
+constexpr int kCipThreads = 256;
+constexpr int kCipRaw = 64;
+constexpr int kCipStride = kCipRaw + 8; // rows 72 B apart: lanes spread over the banks
+
+__global__ __launch_bounds__(kCipThreads) void k_cip(Dev d) {
+	__shared__ __attribute__((aligned(8))) uint8_t rows[kCipThreads * kCipStride];
+	const unsigned long long nq = d.ctr[CTR_CIPQ];
+	uint8_t* row = rows + threadIdx.x * kCipStride;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nq; k += gridDim.x * blockDim.x) {
+		const uint32_t i = d.cipq[k];
+		ebd_event_result r = d.res[i];
+		const uint8_t* p = d.payload + d.off[i];
+		const uint32_t cs = r.u.span.cip_off, lim = r.consumed;
+		unsigned long long v[kCipRaw / 8];
+#pragma unroll
+		for (int h = 0; h < kCipRaw / 8; h++)
+			v[h] = gload8u(p + cs + 8 * h);
+#pragma unroll
+		for (int h = 0; h < kCipRaw / 8; h++)
+			*(unsigned long long*)(row + 8 * h) = v[h];
+		uint32_t tb, te;
+		uint8_t cls;
+		if (cs + kCipRaw < lim) { // value may run past the copy: decide on the copy if it ends inside
+			uint32_t e = 0;
+			while (e < kCipRaw && row[e] != ',' && row[e] != '\r')
+				e++;
+			if (e < kCipRaw) {
+				cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls);
+			} else {
+				cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls);
+				tb -= cs;
+				te -= cs;
+			}
+		} else {
+			cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, lim - cs, &tb, &te, &cls);
+		}
+		r.u.span.cip_off = (uint16_t)(cs + tb);
+		r.u.span.cip_len = (uint16_t)(te - tb);
+		r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+		d.res[i] = r;
 	}
 }
 
@@ -742,6 +835,10 @@ hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
 	const int grid = (int)(ntiles < (uint32_t)cus * 2 ? ntiles : (uint32_t)cus * 2);
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), kFreshLds, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_cip(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_cip, dim3(cus * 4), dim3(kCipThreads), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_carry_insert(const Dev& d, hipStream_t st) {

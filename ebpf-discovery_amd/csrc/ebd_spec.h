@@ -348,7 +348,16 @@ EBD_HD uint32_t gp_parse(GenParser& g, const KeyTrie* trie, ByteAt at, uint32_t 
 enum : uint8_t { CLS_NONE = 0, CLS_INTERNAL = 1, CLS_EXTERNAL = 2 };
 
 // glibc resolv/inet_pton.c inet_pton4 (the reference calls glibc inet_pton, A:66-74).
-EBD_HD bool inet_pton4(const uint8_t* s, uint32_t n, uint8_t out[4]) {
+// A byte source shifted by `off` (works for pointers and accessor views alike).
+template <typename Src>
+struct SrcOff {
+	const Src& s;
+	uint32_t off;
+	EBD_HD uint32_t operator[](uint32_t k) const { return (uint32_t)s[off + k]; }
+};
+
+template <typename Src>
+EBD_HD bool inet_pton4(const Src& s, uint32_t n, uint8_t out[4]) {
 	uint32_t saw_digit = 0, octets = 0, k = 0;
 	uint32_t tmp[4] = {0, 0, 0, 0};
 	for (uint32_t i = 0; i < n; i++) {
@@ -389,7 +398,8 @@ EBD_HD int hex_value(uint32_t ch) {
 }
 
 // glibc resolv/inet_pton.c inet_pton6 (glibc >= 2.26 form).
-EBD_HD bool inet_pton6(const uint8_t* s, uint32_t n, uint8_t out[16]) {
+template <typename Src>
+EBD_HD bool inet_pton6(const Src& s, uint32_t n, uint8_t out[16]) {
 	uint8_t tmp[16];
 	for (int i = 0; i < 16; i++)
 		tmp[i] = 0;
@@ -435,7 +445,7 @@ EBD_HD bool inet_pton6(const uint8_t* s, uint32_t n, uint8_t out[16]) {
 		}
 		if (ch == '.' && tp + 4 <= 16) {
 			uint8_t v4[4];
-			if (inet_pton4(s + curtok, n - curtok, v4)) {
+			if (inet_pton4(SrcOff<Src>{s, curtok}, n - curtok, v4)) {
 				for (int k = 0; k < 4; k++)
 					tmp[tp++] = v4[k];
 				xdigits = 0;
@@ -543,7 +553,8 @@ EBD_HD uint8_t classify_source(const Interfaces& ifs, uint8_t flags, const uint8
 // aggregator uses clientIp.front(), A:52-53).  `raw` = value bytes up to (excluding)
 // the first ',' (boost::split token_compress_on: the first token ends at the first
 // separator).  Returns the token as [*b, *e) inside raw.
-EBD_HD void front_token(const uint8_t* raw, uint32_t n, uint32_t* tb, uint32_t* te) {
+template <typename Src>
+EBD_HD void front_token(const Src& raw, uint32_t n, uint32_t* tb, uint32_t* te) {
 	uint32_t b = 0, e = n;
 	while (b < e && raw[b] == ' ') // boost::trim; only ' ' can occur in a header value
 		b++;
@@ -584,7 +595,8 @@ EBD_HD void front_token(const uint8_t* raw, uint32_t n, uint32_t* tb, uint32_t* 
 }
 
 // A:50-74 on clientIp.front(): >= 2 ':' selects AF_INET6, parse failure = no count.
-EBD_HD uint8_t classify_token(const Interfaces& ifs, const uint8_t* t, uint32_t n) {
+template <typename Src>
+EBD_HD uint8_t classify_token(const Interfaces& ifs, const Src& t, uint32_t n) {
 	uint32_t colons = 0;
 	for (uint32_t k = 0; k < n; k++)
 		colons += t[k] == ':';
@@ -648,54 +660,106 @@ EBD_HD uint64_t fmix64(uint64_t k) {
 	return k;
 }
 
+// 64 x 64 -> 128-bit multiply folded to 64 bits (the "mum" step of wyhash).
+EBD_HD uint64_t wymix(uint64_t a, uint64_t b) {
+	const unsigned __int128 r = (unsigned __int128)a * b;
+	return (uint64_t)r ^ (uint64_t)(r >> 64);
+}
+
+// The endpoint E = host + url is hashed in 16-byte blocks (two little-endian 64-bit
+// pieces, the last block zero-padded) by two independent wymix chains, then finished
+// with the length.  A block depends only on E's bytes, so every host/url split of the
+// same endpoint hashes alike.  The data-side constants have bytes >= 0x80, which no
+// host/url byte can have (HttpRequestParser.cpp:53-76 character classes), so no
+// block can zero a multiplier.
+constexpr uint64_t kEpP0 = 0xa0761d6478bd642full, kEpP1 = 0xe7037ed1a0b428dbull;
+constexpr uint64_t kEpP2 = 0x8ebc6af09c88c6e3ull, kEpP3 = 0x589965cc75374cc3ull;
+
 struct KeyHasher {
-	uint64_t h1, h2, acc;
-	uint32_t nacc, total;
+	uint64_t h1, h2, a, acc;
+	uint32_t total, has_a;
 	EBD_HD void init(uint32_t pid) {
-		h1 = 0x9368e53c2f6af274ull ^ ((uint64_t)pid * 0x9e3779b97f4a7c15ull);
-		h2 = 0x586dcd208f7cd3fdull ^ ((uint64_t)pid * 0xc2b2ae3d27d4eb4full);
-		acc = 0;
-		nacc = 0;
-		total = 0;
+		h1 = fmix64(0x9368e53c2f6af274ull ^ pid);
+		h2 = fmix64(0x586dcd208f7cd3fdull ^ ((uint64_t)pid << 32));
+		a = acc = 0;
+		total = has_a = 0;
 	}
-	EBD_HD void block(uint64_t k) {
-		uint64_t k1 = k * 0x87c37b91114253d5ull;
-		k1 = rotl64(k1, 31) * 0x4cf5ad432745937full;
-		h1 ^= k1;
-		h1 = rotl64(h1, 27) * 5 + 0x52dce729;
-		uint64_t k2 = k * 0x4cf5ad432745937full;
-		k2 = rotl64(k2, 33) * 0x87c37b91114253d5ull;
-		h2 ^= k2;
-		h2 = rotl64(h2, 31) * 5 + 0x38495ab5;
+	EBD_HD void block(uint64_t x, uint64_t y) {
+		h1 = wymix(x ^ kEpP0, y ^ h1);
+		h2 = wymix(y ^ kEpP1, x ^ h2);
+	}
+	// streaming form (session path, host code)
+	EBD_HD void piece(uint64_t v) {
+		if (has_a) {
+			block(a, v);
+			has_a = 0;
+		} else {
+			a = v;
+			has_a = 1;
+		}
 	}
 	EBD_HD void byte(uint32_t b) {
-		acc |= (uint64_t)(b & 0xff) << (8 * nacc);
+		acc |= (uint64_t)(b & 0xff) << (8 * (total & 7));
 		total++;
-		if (++nacc == 8) {
-			block(acc);
+		if ((total & 7) == 0) {
+			piece(acc);
 			acc = 0;
-			nacc = 0;
 		}
 	}
 	EBD_HD void bytes(const uint8_t* p, uint32_t n) {
 		for (uint32_t i = 0; i < n; i++)
 			byte(p[i]);
 	}
-	EBD_HD Hash128 finish() {
-		if (nacc)
-			block(acc ^ 0xa5a5a5a5a5a5a5a5ull);
-		uint64_t a = h1 ^ total, b = h2 ^ ((uint64_t)total << 32);
-		a += b;
-		b += a;
-		a = fmix64(a);
-		b = fmix64(b);
-		a += b;
-		b += a;
+	// after blocks fed directly (block form): n = endpoint length
+	EBD_HD Hash128 finish_blocks(uint32_t n) const {
+		uint64_t x = wymix(h1 ^ kEpP2, (uint64_t)n ^ kEpP3);
+		uint64_t y = wymix(h2 ^ kEpP3, ((uint64_t)n << 32) ^ kEpP2);
 		Hash128 r;
-		r.lo = a | 1ull; // 0 marks an empty slot
-		r.hi = b | 1ull;
+		r.lo = fmix64(x + y) | 1ull; // 0 marks an empty slot
+		r.hi = fmix64(y ^ rotl64(x, 29)) | 1ull;
 		return r;
 	}
+	EBD_HD Hash128 finish() {
+		if (total & 7)
+			piece(acc);
+		if (has_a)
+			block(a, 0);
+		return finish_blocks(total);
+	}
 };
+
+// Mask of the low `k` bytes of a 64-bit piece (k in [0, 8]).
+EBD_HD uint64_t low_bytes(uint32_t k) { return k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1ull); }
+
+// Block form over E = buffer[hs, hs + hl) + buffer[us, us + ul), reading 8-byte pieces
+// through `ld8(offset)` (any alignment; bytes beyond a span are masked off).
+template <typename Ld8>
+EBD_HD Hash128 endpoint_key(uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us, uint32_t ul, Ld8 ld8) {
+	KeyHasher kh;
+	kh.init(pid);
+	const uint32_t n = hl + ul;
+	for (uint32_t o = 0; o < n; o += 16) {
+		uint64_t v[2];
+#pragma unroll
+		for (int h = 0; h < 2; h++) {
+			const uint32_t oo = o + 8 * h;
+			const int d = (int)hl - (int)oo; // host bytes left at this piece
+			uint64_t x = 0;
+			if (oo < n) {
+				if (d >= 8) {
+					x = ld8(hs + oo);
+				} else if (d <= 0) {
+					x = ld8(us + (uint32_t)(-d));
+				} else { // straddles host and url
+					x = (ld8(hs + oo) & low_bytes((uint32_t)d)) | (ld8(us) << (8 * d));
+				}
+				x &= low_bytes(n - oo);
+			}
+			v[h] = x;
+		}
+		kh.block(v[0], v[1]);
+	}
+	return kh.finish_blocks(n);
+}
 
 } // namespace ebd

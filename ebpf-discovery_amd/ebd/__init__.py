@@ -110,6 +110,7 @@ _SIGS = {
     "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_uint32]),
     "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "ebd_host_endpoint_key": (C.c_int, [C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
 }
 
 _lib = None
@@ -360,6 +361,13 @@ def host_classify_source(src16: bytes, flags, v4=(), v6=()):
     b = np.frombuffer(src16, np.uint8)
     v4, v6 = list(v4), list(v6)
     return lib().ebd_host_classify(_p(b), 16, 1, flags, _nets4(v4), len(v4), _nets6(v6), len(v6))
+
+
+def host_endpoint_key(pid: int, endpoint: bytes):
+    b = np.frombuffer(endpoint, np.uint8) if endpoint else np.zeros(1, np.uint8)
+    key = np.zeros(2, np.uint64)
+    _check(lib().ebd_host_endpoint_key(pid, _p(b), len(endpoint), _p(key)), "ebd_host_endpoint_key")
+    return int(key[0]), int(key[1])
 
 
 def host_pton(text: bytes, af6: bool):

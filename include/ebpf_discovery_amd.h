@@ -175,8 +175,10 @@ typedef struct ebd_config {
 typedef struct ebd_ctx ebd_ctx;
 
 /* Device-resident batch: every pointer is a device (HBM) pointer that stays valid
- * until the next ebd_sync.  payload reads are done in aligned 16-byte blocks, so the
- * allocation must be readable up to the next 16-byte boundary after each buffer. */
+ * until the next ebd_sync.  payload reads are done in aligned 16-byte blocks and 8-byte
+ * pieces, so the allocation must be readable from the 16-byte boundary at or below each
+ * buffer to EBD_PAYLOAD_PAD bytes past its end. */
+#define EBD_PAYLOAD_PAD 16u
 typedef struct ebd_device_batch {
 	const ebd_discovery_event* events;
 	const uint32_t* len;

@@ -34,6 +34,10 @@ int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t n
 int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t flags, const ebd_ipv4_network* v4,
 		uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6);
 
+/* Service key of (pid, endpoint) in its streaming form (the session path's): key[0] = lo,
+ * key[1] = hi.  The fast path computes the same key in 16-byte blocks. */
+int ebd_host_endpoint_key(uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]);
+
 /* inet_pton restatement used on the device: 1 = parsed. */
 int ebd_host_pton(int af6, const uint8_t* text, uint32_t len, uint8_t* out);
 

@@ -137,6 +137,38 @@ def test_fresh_generated_config3_sample():
             assert (r["info"] >> 4) & 3 == out["cls"][i], (i, buf)
 
 
+def test_fresh_key_is_streaming_key_of_endpoint():
+    """The fast path's block-form key equals the session path's streaming key of
+    host + url, for every alignment of the buffer (the key is split invariant)."""
+    ev, lens, offs, payload = ebd.generate_host(3, 5, 0, 1500)
+    pay = payload.tobytes()
+    for i in range(len(ev)):
+        buf = pay[int(offs[i]):int(offs[i]) + int(lens[i])]
+        pid = int(ev["pid"][i])
+        for shift in (0, 3, 13):
+            padded = bytearray(b"\0" * (shift + len(buf) + 32))
+            padded[shift:shift + len(buf)] = buf
+            arr = np.frombuffer(bytes(padded), np.uint8)
+            r, key = ebd.host_fresh(bytes(arr[shift:shift + len(buf)]), pid, int(ev["flags"][i]),
+                                    ev["sourceIP"][i].tobytes())
+            if r["status"] != ebd.STATUS_FINISHED:
+                continue
+            ep = buf[r["host_off"]:r["host_off"] + r["host_len"]] + buf[r["url_off"]:r["url_off"] + r["url_len"]]
+            assert key == ebd.host_endpoint_key(pid, ep), (i, shift)
+    # every host/url split of one endpoint gives one key
+    ep = b"svc-1.example.internal:8080/api/v1/items?id=123456789"
+    k0 = ebd.host_endpoint_key(7, ep)
+    for cut in range(len(ep) + 1):
+        req = b"GET " + ep[cut:] + b" HTTP/1.1\r\nHost: " + ep[:cut] + b"\r\n\r\n"
+        if not ep[cut:].startswith(b"/"):
+            continue
+        r, key = ebd.host_fresh(req, 7)
+        if r["status"] == ebd.STATUS_FINISHED and r["host_len"] == cut:
+            assert key == k0, cut
+    assert ebd.host_endpoint_key(7, ep) != ebd.host_endpoint_key(8, ep)
+    assert ebd.host_endpoint_key(7, b"") != ebd.host_endpoint_key(7, b"\0")
+
+
 def test_fresh_random_mutations():
     rng = random.Random(11)
     base = [b"GET /p/q?x=1 HTTP/1.1\r\nHost: svc.example.com:80\r\nX-Forwarded-For: 8.8.8.8:9, 10.0.0.1\r\n"
