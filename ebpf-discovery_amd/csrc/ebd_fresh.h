@@ -140,17 +140,9 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 		return;
 	}
 	const bool fin = s_final != di.inv, host = s_final == di.fin1, cip = fin && sr.cseen;
-	// every chunk finalize needs, loaded before any is used
-	const Chunk wt = mem.chunk(sr.term >> 8);
-	Chunk wu, wh, we, wc;
-	if (fin)
-		wu = mem.chunk(sr.url >> 8);
-	if (host) {
-		wh = mem.chunk(sr.host >> 8);
-		we = mem.chunk(sr.hend >> 8);
-	}
-	if (cip)
-		wc = mem.chunk(sr.cip >> 8);
+	// every chunk finalize may need, loaded unconditionally before any is used
+	const Chunk wt = mem.chunk(sr.term >> 8), wu = mem.chunk(sr.url >> 8), wh = mem.chunk(sr.host >> 8),
+	            we = mem.chunk(sr.hend >> 8), wc = mem.chunk(sr.cip >> 8);
 	const uint32_t consumed = rescan<RS_TERM>(T, di, sr.term, wt, skip, L) + 1;
 	r.consumed = (uint16_t)consumed;
 	if (!fin) {
@@ -180,7 +172,12 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	r.u.span.url_len = (uint16_t)url_len;
 	r.u.span.host_off = (uint16_t)host_start;
 	r.u.span.host_len = (uint16_t)host_len;
+#ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
+	out.key.lo = host_len * 31 + url_len;
+	out.key.hi = 1;
+#else
 	out.key = endpoint_key(pid, host_start, host_len, url_start, url_len, [&](uint32_t o) { return mem.ld8(o); });
+#endif
 }
 
 // Client-IP pass for one event (HttpRequestParser.cpp:370-407 parseClientIPValue on the

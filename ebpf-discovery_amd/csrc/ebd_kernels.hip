@@ -198,7 +198,8 @@ __device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
 struct DevMem {
 	const uint8_t* p;
 	uintptr_t q; // p rounded down to 16
-	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16(q + 16 * (uintptr_t)c); }
+	uint32_t last; // last chunk index of the buffer
+	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16(q + 16 * (uintptr_t)min(c, last)); }
 	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
 };
 
@@ -216,9 +217,9 @@ __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t w, int k) {
 __device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
 	const uint8_t flags = ((const uint8_t*)(d.ev + i))[32];
 	const uint32_t L = d.len[i];
+	const uint32_t skip = (uint32_t)(d.off[i] + (uintptr_t)d.payload) & 15u;
 	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || L > EBD_BUFFER_MAX_DATA_SIZE)
 		return 0;
-	const uint32_t skip = (uint32_t)(d.off[i] + (uintptr_t)d.payload) & 15u;
 	const uint32_t ch = (skip + L + 15) >> 4;
 	return ch < kBins ? ch : kBins - 1;
 }
@@ -244,10 +245,25 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 	}
 }
 
+// Partial chunk (buffer start or end inside it): compact loop, it is rare.
+__device__ __forceinline__ void scan_chunk_masked(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m,
+		uint32_t pos0, uint32_t skip, uint32_t end) {
+	const uint32_t w0 = w.w[0], w1 = w.w[1], w2 = w.w[2], w3 = w.w[3];
+#pragma unroll 1
+	for (int k = 0; k < 16; k++) {
+		const uint32_t wk = k < 4 ? w0 : k < 8 ? w1 : k < 12 ? w2 : w3;
+		const uint32_t sn = T[(s << 8) | ((wk >> (8 * (k & 3))) & 0xffu)];
+		const bool v = pos0 + k >= skip && pos0 + k < end;
+		s = v ? sn : s;
+		m = max(m, v ? sn : 0u);
+	}
+}
+
 __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint32_t i) {
 	const uint8_t* evb = (const uint8_t*)(d.ev + i);
 	const uint8_t flags = evb[32];
 	const uint32_t L = d.len[i];
+	const uint64_t boff = d.off[i]; // loaded with flags and len, before they are tested
 	FreshResult fr;
 	fr.r.consumed = 0;
 	fr.r.status = EBD_STATUS_NONE;
@@ -260,7 +276,7 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 			set_error(d, EBD_ERR_BAD_INPUT);
 		} else {
 			const DfaInfo& di = d.di;
-			const uint8_t* p = d.payload + d.off[i];
+			const uint8_t* p = d.payload + boff;
 			const uintptr_t pa = (uintptr_t)p;
 			const uintptr_t q = pa & ~(uintptr_t)15;
 			const uint32_t skip = (uint32_t)(pa & 15);
@@ -269,37 +285,73 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 			ScanRec sr;
 			rec_init(di, sr);
 			uint32_t s = di.init;
-			// three chunks in flight ahead of the one being scanned
-			Chunk w0 = gload16(q), w1 = w0, w2 = w0;
-			if (nch > 1)
-				w1 = gload16(q + 16);
-			if (nch > 2)
-				w2 = gload16(q + 32);
-			for (uint32_t c = 0; c < nch; c++) {
-				Chunk w3 = w2;
-				if (c + 3 < nch)
-					w3 = gload16(q + 16 * (uintptr_t)(c + 3));
-				const uint32_t s0 = s;
-				uint32_t m = 0;
+			// The buffer is read in windows of 8 chunks (128 B): a lane's 8 loads of a window
+			// are issued back to back, so each 128-B line is used right after it arrives
+			// (16-B reads spread over time let the ~32k concurrent streams of an XCD evict
+			// lines between reads).  The next window is in flight while one is scanned; two
+			// register windows with fixed roles (a register copy of a loaded chunk, or a load
+			// behind a branch, would make the wave wait for every load).  Loads past the
+			// buffer re-read its last chunk.
+			const uint32_t last = nch ? nch - 1 : 0;
+			Chunk A[8], B[8];
+			auto ldw = [&](Chunk(&w)[8], uint32_t j) {
+#pragma unroll
+				for (int k = 0; k < 8; k++)
+					w[k] = gload16(q + 16 * (uintptr_t)min(8 * j + k, last));
+			};
+			bool live = nch > 0;
+			// One chunk for every lane (a no-op for lanes already done): DFA steps, then the
+			// trackers.  The only exits are uniform.
+			auto step = [&](const Chunk& w, uint32_t c) {
+				uint32_t sx = s, m = 0;
 				const bool full = c * 16 >= skip && c * 16 + 16 <= end;
 				if (__all(full))
-					scan_chunk<true>(T, w0, s, m, c * 16, skip, end);
+					scan_chunk<true>(T, w, sx, m, c * 16, skip, end);
 				else
-					scan_chunk<false>(T, w0, s, m, c * 16, skip, end);
-				if (st_terminal(di, s)) {
-					sr.term = (c << 8) | s0;
-					sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
-					break;
+					scan_chunk_masked(T, w, sx, m, c * 16, skip, end);
+				if (live) {
+					if (st_terminal(di, sx)) {
+						sr.term = (c << 8) | s;
+						sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
+						live = false;
+					} else {
+						chunk_track(di, sr, c, sx, m >= 254);
+						live = c + 1 < nch;
+					}
+					s = sx;
 				}
-				chunk_track(di, sr, c, s, m >= 254);
-				w0 = w1;
-				w1 = w2;
-				w2 = w3;
+			};
+			ldw(A, 0);
+			for (uint32_t j = 0;; j += 2) {
+				ldw(B, j + 1);
+#pragma unroll
+				for (int k = 0; k < 8; k++) {
+					step(A[k], 8 * j + k);
+					if (!__any(live))
+						break;
+				}
+				if (!__any(live))
+					break;
+				ldw(A, j + 2);
+#pragma unroll
+				for (int k = 0; k < 8; k++) {
+					step(B[k], 8 * (j + 1) + k);
+					if (!__any(live))
+						break;
+				}
+				if (!__any(live))
+					break;
 			}
+#ifdef EBD_EXP_SCANONLY // experiment: scan cost alone (results are wrong)
+			fr.r.consumed = (uint16_t)s;
+			fr.r.u.span.url_off = (uint16_t)(sr.url ^ sr.host ^ sr.hend ^ sr.cip ^ sr.term ^ sr.cseen);
+			d.res[i] = fr.r;
+			return;
+#endif
 			const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP
 			uint8_t src[16];
 			__builtin_memcpy(src, &sv, 16);
-			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q}, skip, L, *(const uint32_t*)evb, flags, src, *d.ifs, fr);
+			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q, last}, skip, L, *(const uint32_t*)evb, flags, src, *d.ifs, fr);
 			if (fr.r.status == EBD_STATUS_FINISHED) {
 				d.keys[i] = fr.key;
 			} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
@@ -316,11 +368,15 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 	}
 }
 
+#ifdef EBD_EXP_LB8 // experiment: two workgroups per CU
+__global__ __launch_bounds__(kFreshThreads, 8) void k_fresh(Dev d) {
+#else
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
-	extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-	uint8_t* T = lds;
-	uint16_t* perm = (uint16_t*)(lds + 65536);
-	uint32_t* hist = (uint32_t*)(lds + 65536 + kTile * 2);
+#endif
+	// static LDS: the table sits at LDS address 0, so a step's index is its address
+	__shared__ __attribute__((aligned(16))) uint8_t T[65536];
+	__shared__ uint16_t perm[kTile];
+	__shared__ uint32_t hist[kBins];
 	for (uint32_t k = threadIdx.x * 16u; k < 65536u; k += kFreshThreads * 16u)
 		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -337,7 +393,13 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #pragma unroll
 		for (int k = 0; k < kPer; k++) {
 			const uint32_t t = threadIdx.x + k * kFreshThreads;
-			bin[k] = t < cnt ? event_bin(d, base + t) : 0;
+			bin[k] = event_bin(d, base + (t < cnt ? t : 0)); // unconditional loads, all in flight
+		}
+#pragma unroll
+		for (int k = 0; k < kPer; k++) {
+			const uint32_t t = threadIdx.x + k * kFreshThreads;
+			if (t >= cnt)
+				bin[k] = 0;
 			rank[k] = t < cnt ? atomicAdd(&hist[bin[k]], 1u) : 0;
 		}
 		__syncthreads();
@@ -834,7 +896,7 @@ static int grid_for(uint64_t items, int block, int cap) {
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
 	const int grid = (int)(ntiles < (uint32_t)cus * 2 ? ntiles : (uint32_t)cus * 2);
-	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), kFreshLds, st, d);
+	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_cip(const Dev& d, hipStream_t st, int cus) {

@@ -744,18 +744,11 @@ EBD_HD Hash128 endpoint_key(uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us,
 		for (int h = 0; h < 2; h++) {
 			const uint32_t oo = o + 8 * h;
 			const int d = (int)hl - (int)oo; // host bytes left at this piece
-			uint64_t x = 0;
-			if (oo < n) {
-				if (d >= 8) {
-					x = ld8(hs + oo);
-				} else if (d <= 0) {
-					x = ld8(us + (uint32_t)(-d));
-				} else { // straddles host and url
-					x = (ld8(hs + oo) & low_bytes((uint32_t)d)) | (ld8(us) << (8 * d));
-				}
-				x &= low_bytes(n - oo);
-			}
-			v[h] = x;
+			// both candidate loads, unconditionally (no load behind a branch)
+			const uint64_t A = ld8(hs + (d > 0 ? oo : 0));
+			const uint64_t B = ld8(us + ((d <= 0 && oo < n) ? (uint32_t)(-d) : 0u));
+			uint64_t x = d >= 8 ? A : (d <= 0 ? B : ((A & low_bytes((uint32_t)d)) | (B << (8 * (d & 7)))));
+			v[h] = oo < n ? (x & low_bytes(n - oo)) : 0;
 		}
 		kh.block(v[0], v[1]);
 	}

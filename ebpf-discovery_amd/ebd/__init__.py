@@ -14,7 +14,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_DIR = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_DIR, "libebd_amd.so")
+# EBD_LIB selects another build of the same sources (tools/perf_fresh.py experiment variants)
+LIB_PATH = os.environ.get("EBD_LIB") or os.path.join(PKG_DIR, "libebd_amd.so")
 
 FLAG_IPV4, FLAG_IPV6, FLAG_UNENCRYPTED, FLAG_SSL, FLAG_NEW_DATA, FLAG_DATA_END = 2, 4, 8, 16, 32, 64
 NO_BUFFER = 0xFFFFFFFF

@@ -236,10 +236,6 @@ int ebd_clear(ebd_ctx* ctx);
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
 
-/* --- multi-GPU: compact service table export / merge (RCCL carries the bytes) --------- */
-/* Export this context's services as packed device records for an owner-partitioned
- * exchange; see ebd_export_* in INTEGRATION.md.  (Round 1: host-side merge helper.) */
-
 /* --- synthetic traces, identical on host and device ---------- */
 typedef struct ebd_trace_config {
 	uint32_t config; /* 1, 2, 3 (single-buffer); 4 (fragmented, keep-alive) */
