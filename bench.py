@@ -152,7 +152,6 @@ def main():
 
     # algorithmic bytes of one batch: sum(consumed + 40) per data event
     res = ctx.results()
-    ev_h = ev_t[: 36 * 1].cpu()  # noqa: F841 (events are all NEW_DATA in configs 1-3)
     data_events = int((res["status"] != ebd.STATUS_NONE).sum())
     alg_bytes = int(res["consumed"].astype(np.uint64).sum()) + 40 * data_events
     fresh_launches, fresh_ms = kt["k_fresh"]
@@ -168,35 +167,17 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
 
-    # the final per-(pid, endpoint) counter merge across GPUs (RCCL all-gather), once
+    # the final per-(pid, endpoint) merge across GPUs, once, after the timed steps: owner-
+    # partitioned all_to_all over RCCL (ebd.shard); seq numbers are already global
     merge_ms = None
-    services = ctx.services(with_seq=world > 1)
     if world > 1:
-        import pickle
+        from ebd import shard
         tm = time.perf_counter()
-        blob = np.frombuffer(pickle.dumps(services), np.uint8)
-        n_t = torch.tensor([blob.size], dtype=torch.int64, device=dev)
-        sizes = [torch.zeros_like(n_t) for _ in range(world)]
-        torch.distributed.all_gather(sizes, n_t)
-        mx = int(max(s.item() for s in sizes))
-        buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
-        buf[: blob.size] = torch.from_numpy(blob.copy()).to(dev)
-        outs = [torch.zeros(mx, dtype=torch.uint8, device=dev) for _ in range(world)]
-        torch.distributed.all_gather(outs, buf)
-        if rank == 0:
-            merged = {}
-            for r, o in enumerate(outs):
-                for (pid, ep, dom, sch, i, e, seq) in pickle.loads(o[: int(sizes[r].item())].cpu().numpy().tobytes()):
-                    m = merged.get((pid, ep))
-                    if m is None:
-                        merged[(pid, ep)] = [dom, sch, i, e, seq]
-                    else:
-                        m[2] = (m[2] + i) & 0xFFFFFFFF
-                        m[3] = (m[3] + e) & 0xFFFFFFFF
-                        if seq < m[4]:
-                            m[0], m[1], m[4] = dom, sch, seq
-            services = merged
+        merged = shard.exchange_merge(shard.ServiceTable.from_context(ctx), device=dev)
+        n_services = merged.rec.size if merged is not None else None
         merge_ms = (time.perf_counter() - tm) * 1e3
+    else:
+        n_services = st["services"]
 
     if rank != 0:
         torch.distributed.destroy_process_group()
@@ -228,7 +209,7 @@ def main():
         "step_gbps_alg": alg_bytes * world * args.steps / elapsed / 1e9,
         "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items()},
         "measured_stream_read_gbps": peak_read,
-        "services": len(services),
+        "services": n_services,
         "errors": st["error_names"],
         "merge_ms": merge_ms,
     }

@@ -271,9 +271,10 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		std::fprintf(stderr, "ebd: DFA construction failed (%d)\n", rc);
 		return fail(-EIO);
 	}
-	const size_t tbytes = sizeof(c->dfa_host->next);
-	CTX_TRY(hipMalloc(&c->d_dfa, tbytes));
-	CTX_TRY(hipMemcpy(c->d_dfa, c->dfa_host->next, tbytes, hipMemcpyHostToDevice));
+	std::vector<uint8_t> image(kLdsTableBytes); // the table as k_fresh keeps it in LDS
+	build_lds_image(c->dfa_host, image.data());
+	CTX_TRY(hipMalloc(&c->d_dfa, kLdsTableBytes));
+	CTX_TRY(hipMemcpy(c->d_dfa, image.data(), kLdsTableBytes, hipMemcpyHostToDevice));
 	CTX_TRY(hipMalloc(&c->d_trie, sizeof(KeyTrie)));
 	CTX_TRY(hipMemcpy(c->d_trie, &c->trie_host, sizeof(KeyTrie), hipMemcpyHostToDevice));
 	std::memset(&c->ifs_host, 0, sizeof(Interfaces));

@@ -36,6 +36,22 @@ struct DfaTable {
 	uint8_t next[256 * 256]; // next[s * 256 + byte]
 };
 
+// The table as the kernel keeps it in LDS.  Rows are kLdsRow = 260 bytes apart (65 dwords,
+// so consecutive states start one bank apart), and byte b of a row sits at column lds_col(b),
+// which moves b's low 5 bits to bits 6..2: the bank of entry (s, b) is (s + b[4:0]) mod 32.
+// Lanes in the same state never conflict (the 4 ASCII bytes that share b[4:0] share one
+// dword), and different states spread over the banks.  The plain (s << 8) | b layout puts
+// all lower-case letters on 7 banks (tools/ubench_lds.hip measures both).
+#ifndef EBD_LDS_PLAIN
+constexpr uint32_t kLdsRow = 260;
+EBD_HD constexpr uint32_t lds_col(uint32_t b) { return ((b & 0x1fu) << 2) | ((b >> 5) & 3u) | (b & 0x80u); }
+#else // experiment: the plain layout
+constexpr uint32_t kLdsRow = 256;
+EBD_HD constexpr uint32_t lds_col(uint32_t b) { return b; }
+#endif
+constexpr uint32_t kLdsTableBytes = 256 * kLdsRow;
+void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes
+
 void build_key_trie(KeyTrie* t);
 // Returns 0, or a negative value when an internal consistency check fails.
 int build_dfa(const KeyTrie* trie, DfaTable* out);

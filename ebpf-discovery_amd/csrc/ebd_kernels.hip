@@ -171,9 +171,10 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 // Per byte: extract, table step, one wave ballot (client-IP value state); per chunk: the
 // crossing trackers of ebd_fresh.h.
 // ---------------------------------------------------------------------------------
+// Logical index (s << 8) | b into the LDS image (ebd_dfa.h kLdsRow / lds_col).
 struct LdsTable {
 	const uint8_t* t;
-	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i >> 8) * kLdsRow + lds_col(i & 0xffu)]; }
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -206,12 +207,23 @@ struct DevMem {
 constexpr int kFreshThreads = 1024;
 constexpr int kTile = 4096;
 constexpr int kBins = 128;
-constexpr size_t kFreshLds = 65536 + kTile * 2 + kBins * 4;
 
-// (s << 8) | byte k of w in one v_perm_b32: result byte 0 = byte (k & 3) of w,
-// byte 1 = byte 0 of s, bytes 2-3 = 0.
-__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t w, int k) {
-	return __builtin_amdgcn_perm(s, w, 0x0c0c0400u | (uint32_t)(k & 3));
+// A chunk word with every byte b replaced by lds_col(b) (5 VALU per 4 bytes).
+__device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
+#ifndef EBD_LDS_PLAIN
+	return ((w << 2) & 0x7c7c7c7cu) | ((w >> 5) & 0x03030303u) | (w & 0x80808080u);
+#else
+	return w;
+#endif
+}
+
+// LDS address of entry (s, byte k of the column-mapped word wc).
+__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
+#ifndef EBD_LDS_PLAIN
+	return s * kLdsRow + __builtin_amdgcn_ubfe(wc, 8 * (k & 3), 8); // v_bfe + v_mad_u32_u24
+#else
+	return __builtin_amdgcn_perm(s, wc, 0x0c0c0400u | (uint32_t)(k & 3)); // (s << 8) | byte
+#endif
 }
 
 __device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
@@ -228,9 +240,10 @@ __device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
 template <bool kFull>
 __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t pos0,
 		uint32_t skip, uint32_t end) {
+	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
-		const uint32_t sn = T[tab_index(s, w.w[k >> 2], k)];
+		const uint32_t sn = T[tab_index(s, wc[k >> 2], k)];
 		if (kFull) {
 			s = sn;
 			if (k & 1)
@@ -252,7 +265,7 @@ __device__ __forceinline__ void scan_chunk_masked(const uint8_t* T, const Chunk&
 #pragma unroll 1
 	for (int k = 0; k < 16; k++) {
 		const uint32_t wk = k < 4 ? w0 : k < 8 ? w1 : k < 12 ? w2 : w3;
-		const uint32_t sn = T[(s << 8) | ((wk >> (8 * (k & 3))) & 0xffu)];
+		const uint32_t sn = T[s * kLdsRow + lds_col((wk >> (8 * (k & 3))) & 0xffu)];
 		const bool v = pos0 + k >= skip && pos0 + k < end;
 		s = v ? sn : s;
 		m = max(m, v ? sn : 0u);
@@ -374,10 +387,10 @@ __global__ __launch_bounds__(kFreshThreads, 8) void k_fresh(Dev d) {
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #endif
 	// static LDS: the table sits at LDS address 0, so a step's index is its address
-	__shared__ __attribute__((aligned(16))) uint8_t T[65536];
+	__shared__ __attribute__((aligned(16))) uint8_t T[kLdsTableBytes];
 	__shared__ uint16_t perm[kTile];
 	__shared__ uint32_t hist[kBins];
-	for (uint32_t k = threadIdx.x * 16u; k < 65536u; k += kFreshThreads * 16u)
+	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kFreshThreads * 16u)
 		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 	constexpr int kPer = kTile / kFreshThreads;
@@ -860,6 +873,8 @@ __global__ void k_collect(const Slot* slots, uint32_t n, ebd_service* out, unsig
 		v.domain_len = s.dom >> 16;
 		v.pad2_ = 0;
 		v.first_seq = s.min_seq;
+		v.key_lo = s.tag;
+		v.key_hi = s.hi;
 		out[at] = v;
 	}
 }

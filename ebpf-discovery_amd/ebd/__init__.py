@@ -35,9 +35,10 @@ SESSION_REQ_DTYPE = np.dtype([("seq", "<u8"), ("pid", "<u4"), ("str_off", "<u4")
                               ("status", "u1"), ("pad", "<u2"), ("pad2", "<u4")])
 SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4"), ("https", "u1"),
                           ("pad", "u1", (3,)), ("endpoint_off", "<u8"), ("endpoint_len", "<u4"),
-                          ("domain_off", "<u4"), ("domain_len", "<u4"), ("pad2", "<u4"), ("first_seq", "<u8")])
+                          ("domain_off", "<u4"), ("domain_len", "<u4"), ("pad2", "<u4"), ("first_seq", "<u8"),
+                          ("key_lo", "<u8"), ("key_hi", "<u8")])
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
-assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 48
+assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 64
 CFG_TIMING = 2
 
 
@@ -243,6 +244,16 @@ class Context:
         _check(lib().ebd_fetch_session_requests(self.h, _p(out), n.value, C.byref(n), _p(buf), buf.size,
                                                 C.byref(sl)), "ebd_fetch_session_requests")
         return out, buf[:sl.value].tobytes()
+
+    def services_raw(self):
+        """ebd_collect_services as (SERVICE_DTYPE records, endpoint bytes)."""
+        n, sl = C.c_uint32(), C.c_uint64()
+        _check(lib().ebd_collect_services(self.h, None, 0, C.byref(n), None, 0, C.byref(sl)), "collect")
+        out = np.zeros(max(n.value, 1), SERVICE_DTYPE)
+        buf = np.zeros(max(sl.value, 1), np.uint8)
+        _check(lib().ebd_collect_services(self.h, _p(out), out.size, C.byref(n), _p(buf), buf.size, C.byref(sl)),
+               "ebd_collect_services")
+        return out[:n.value].copy(), buf[:sl.value].copy()
 
     def services(self, with_seq=False):
         """[(pid, endpoint, domain, scheme, internal, external)] sorted by (pid, endpoint);

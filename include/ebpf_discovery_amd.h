@@ -138,7 +138,9 @@ typedef struct ebd_service {
 	uint32_t domain_len;
 	uint32_t pad2_;
 	uint64_t first_seq; /* global order of the request that created it (first arrival) */
-} ebd_service; /* 48 bytes */
+	uint64_t key_lo, key_hi; /* 128-bit hash of (pid, endpoint): identical on every GPU, so
+	                            shards merge and pick owners by it without comparing strings */
+} ebd_service; /* 64 bytes */
 
 typedef struct ebd_stats {
 	uint64_t events;            /* events submitted */

@@ -569,6 +569,18 @@ int orc_inet_pton6(const char* src, size_t len, uint8_t out[16]) {
 	return 1;
 }
 
+static char* put_u64(char* o, uint64_t v) {
+	char b[24];
+	int k = 0;
+	do {
+		b[k++] = (char)('0' + v % 10);
+		v /= 10;
+	} while (v);
+	while (k)
+		*o++ = b[--k];
+	return o;
+}
+
 static char* put_u(char* o, unsigned v) {
 	char b[12];
 	int k = 0;
@@ -813,6 +825,7 @@ typedef struct svc {
 	uint32_t pid;
 	dstr endpoint, domain, scheme;
 	uint32_t internal, external; /* uint32, wraps like Service.h:53-54 */
+	uint64_t first;              /* index of the event whose request created it (first arrival) */
 	struct svc* hnext;
 } svc;
 
@@ -838,6 +851,7 @@ struct orc_ctx {
 	int use_mock;
 	dstr blob;
 	orc_stats st;
+	uint64_t cur_event; /* index of the event being handled, over all orc_process calls */
 };
 
 static void free_parser_value(void* v) {
@@ -1084,6 +1098,7 @@ static int agg_new_request(orc_ctx* c, const orc_request* r, uint32_t pid, uint8
 	svc* s = (svc*)calloc(1, sizeof(svc));
 	s->pid = pid;
 	s->endpoint = ep;
+	s->first = c->cur_event;
 	/* A:117-125 domain */
 	const char* h = r->host.p;
 	size_t hn = r->host.n;
@@ -1162,7 +1177,12 @@ static int svc_cmp(const void* a, const void* b) {
 
 uint64_t orc_service_count(orc_ctx* c) { return c->nsvc; }
 
-uint64_t orc_services_dump(orc_ctx* c, char* buf, uint64_t cap) {
+static uint64_t services_dump(orc_ctx* c, char* buf, uint64_t cap, int with_first);
+
+uint64_t orc_services_dump(orc_ctx* c, char* buf, uint64_t cap) { return services_dump(c, buf, cap, 0); }
+uint64_t orc_services_dump_first(orc_ctx* c, char* buf, uint64_t cap) { return services_dump(c, buf, cap, 1); }
+
+static uint64_t services_dump(orc_ctx* c, char* buf, uint64_t cap, int with_first) {
 	svc** v = (svc**)malloc((c->nsvc ? c->nsvc : 1) * sizeof(svc*));
 	memcpy(v, c->list, c->nsvc * sizeof(svc*));
 	qsort(v, c->nsvc, sizeof(svc*), svc_cmp);
@@ -1190,6 +1210,12 @@ uint64_t orc_services_dump(orc_ctx* c, char* buf, uint64_t cap) {
 		e = put_u(num, s->external);
 		for (char* q = num; q < e; q++)
 			ds_push(&out, *q);
+		if (with_first) {
+			ds_push(&out, '\t');
+			e = put_u64(num, s->first);
+			for (char* q = num; q < e; q++)
+				ds_push(&out, *q);
+		}
 		ds_push(&out, '\n');
 	}
 	free(v);
@@ -1288,7 +1314,7 @@ static void handle_new_session(orc_ctx* c, const uint8_t* buf, size_t len, const
 
 int orc_process(orc_ctx* c, const orc_event* ev, const uint32_t* len, const uint64_t* off, const uint8_t* payload, uint32_t n,
 		orc_event_result* out) {
-	for (uint32_t i = 0; i < n; i++) {
+	for (uint32_t i = 0; i < n; i++, c->cur_event++) {
 		const orc_event* e = &ev[i];
 		orc_event_result* o = &out[i];
 		memset(o, 0, sizeof(*o));

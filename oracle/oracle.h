@@ -102,6 +102,9 @@ void orc_get_stats(orc_ctx* c, orc_stats* s);
 /* Services sorted by (pid, endpoint); one line each:
  * pid \t endpoint \t domain \t scheme \t internal \t external \n.  Returns bytes needed. */
 uint64_t orc_services_dump(orc_ctx* c, char* buf, uint64_t cap);
+/* The same with a 7th column: the index (over all orc_process calls) of the event whose
+ * request created the service — the first arrival that fixed its domain and scheme. */
+uint64_t orc_services_dump_first(orc_ctx* c, char* buf, uint64_t cap);
 uint64_t orc_service_count(orc_ctx* c);
 void orc_clear(orc_ctx* c);
 

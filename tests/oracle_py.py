@@ -54,6 +54,8 @@ def lib():
         L.orc_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.orc_services_dump.argtypes = [vp, vp, C.c_uint64]
         L.orc_services_dump.restype = C.c_uint64
+        L.orc_services_dump_first.argtypes = [vp, vp, C.c_uint64]
+        L.orc_services_dump_first.restype = C.c_uint64
         L.orc_service_count.argtypes = [vp]
         L.orc_service_count.restype = C.c_uint64
         L.orc_clear.argtypes = [vp]
@@ -224,6 +226,19 @@ class Oracle:
         buf = C.create_string_buffer(max(n, 1))
         lib().orc_services_dump(self.h, buf, n)
         return parse_services(buf.raw[:n])
+
+    def services_first(self):
+        """services() rows with a 7th field: index of the event that created the service."""
+        n = lib().orc_services_dump_first(self.h, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        lib().orc_services_dump_first(self.h, buf, n)
+        rows = []
+        for line in buf.raw[:n].split(b"\n"):
+            if not line:
+                continue
+            f = line.split(b"\t")
+            rows.append((int(f[0]), f[1], f[2], f[3], int(f[4]), int(f[5]), int(f[6])))
+        return rows
 
     def stats(self):
         s = Stats()

@@ -35,7 +35,7 @@ def test_struct_layouts_match_header():
     assert ebd.EVENT_DTYPE.itemsize == 36          # DiscoveryEvent, Types.h:201-205
     assert ebd.RESULT_DTYPE.itemsize == 16
     assert ebd.SESSION_REQ_DTYPE.itemsize == 32
-    assert ebd.SERVICE_DTYPE.itemsize == 48
+    assert ebd.SERVICE_DTYPE.itemsize == 64
     assert C.sizeof(ebd.Config) == 40
     assert C.sizeof(ebd.Stats) == 72
 

@@ -179,3 +179,20 @@ def test_large_config3_against_oracle():
     assert st["errors"] == 0 and st["hash_collisions"] == 0
     assert gs == os_
     assert gv == ov
+
+
+def test_sharded_contexts_merge_to_whole_trace():
+    """Multi-GPU flow on one GPU: connection shards in separate contexts (as separate GPUs
+    would run them), first arrival mapped to trace positions, merged by ebd.shard: equals
+    the oracle over the whole trace.  Covers the 128-bit key export (ebd_service.key_lo/hi)."""
+    from ebd import shard
+    for ev, lens, offs, payload in (ebd.generate_host(3, 21, 0, 30000), T.fragmented_trace(400, seed=23, window=64)):
+        tables = []
+        for idx in shard.shard_indices(ev, 3):
+            ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size)
+            ctx.submit(ev[idx], lens[idx], offs[idx], payload)
+            assert ctx.stats()["errors"] == 0
+            tables.append(shard.ServiceTable.from_context(ctx, global_index=idx))
+        got = shard.merge_tables(tables).packed().rows()
+        _, want, _ = run_oracle(ev, lens, offs, payload)
+        assert got == want

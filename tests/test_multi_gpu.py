@@ -1,0 +1,104 @@
+"""Multi-GPU path on CPU: connection sharding + the owner-partitioned service merge
+(ebd.shard) over a world_size-2 gloo group.
+
+Each rank takes its connection shard of a trace (ebd.shard.shard_indices), replays it with
+the oracle (the stand-in for that rank's GPU context: this test has no GPU), keys its
+services with the product's 128-bit endpoint key, and merges through
+ebd.shard.exchange_merge.  Rank 0's merged table must equal the oracle over the whole trace:
+(pid, endpoint, domain, scheme, internal, external), bit-exact.
+"""
+import datetime
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import ebd
+from ebd import shard
+import oracle_py as O
+import traces
+
+
+def _trace(kind):
+    if kind == "config3":
+        return ebd.generate_host(3, 7, 0, 6000)
+    return traces.fragmented_trace(300, seed=9, window=64)
+
+
+def _shard_table(ev, lens, offs, payload, idx):
+    """One rank's services, from the oracle over its shard (trace order kept)."""
+    o = O.Oracle()
+    o.process(ev[idx], lens[idx], offs[idx], payload)
+    rows = []
+    for (pid, ep, dom, sch, i, e, first) in o.services_first():
+        rows.append((pid, ep, dom, sch, i, e, int(idx[first])))  # local order -> trace position
+    keys = [ebd.host_endpoint_key(r[0], r[1]) for r in rows]
+    return shard.ServiceTable.from_rows(rows, keys)
+
+
+def _worker(rank, world, port, kind, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    try:
+        ev, lens, offs, payload = _trace(kind)
+        idx = shard.shard_indices(ev, world)[rank]
+        table = _shard_table(ev, lens, offs, payload, idx)
+        merged = shard.exchange_merge(table, device="cpu")
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump([[p, ep.decode("latin-1"), dom.decode("latin-1"), sch.decode(), i, e]
+                           for (p, ep, dom, sch, i, e) in merged.rows()], f)
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("kind", ["config3", "fragmented"])
+def test_two_rank_merge_equals_whole_trace(kind, tmp_path):
+    out_path = str(tmp_path / "merged.json")
+    mp.start_processes(_worker, args=(2, _free_port(), kind, out_path), nprocs=2, join=True, start_method="spawn")
+    with open(out_path) as f:
+        merged = [(p, ep.encode("latin-1"), dom.encode("latin-1"), sch.encode(), i, e) for p, ep, dom, sch, i, e in
+                  json.load(f)]
+    ev, lens, offs, payload = _trace(kind)
+    o = O.Oracle()
+    o.process(ev, lens, offs, payload)
+    want = sorted(o.services(), key=lambda t: (t[0], t[1]))
+    assert len(merged) == len(want)
+    assert merged == want
+
+
+def test_shards_keep_connections_and_order():
+    ev, lens, offs, payload = _trace("fragmented")
+    parts = shard.shard_indices(ev, 4)
+    allidx = np.sort(np.concatenate(parts))
+    assert np.array_equal(allidx, np.arange(len(ev), dtype=np.uint64))
+    owner = {}
+    for r, p in enumerate(parts):
+        assert np.all(np.diff(p.astype(np.int64)) > 0)  # trace order inside a shard
+        for i in p:
+            k = (int(ev["pid"][i]), int(ev["fd"][i]), int(ev["sessionID"][i]))
+            assert owner.setdefault(k, r) == r  # a connection lives on one shard
+
+
+def test_local_merge_rules():
+    """Counters add mod 2^32; domain / scheme / pid come from the earliest creator."""
+    rows = [(7, b"h:1/a", b"h", b"http", 0xFFFFFFFF, 3, 50),
+            (7, b"h:1/a", b"h", b"https", 2, 1, 10),
+            (8, b"h:1/a", b"h", b"http", 1, 1, 5)]
+    keys = [ebd.host_endpoint_key(r[0], r[1]) for r in rows]
+    t = shard.merge_tables([shard.ServiceTable.from_rows(rows[:1], keys[:1]),
+                            shard.ServiceTable.from_rows(rows[1:], keys[1:])])
+    got = t.packed().rows()
+    assert got == [(7, b"h:1/a", b"h", b"https", 1, 4), (8, b"h:1/a", b"h", b"http", 1, 1)]
