@@ -824,8 +824,9 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
-	fresh_finalize(HostTab{t->next}, t->info, sr, s, HostMem{buf, skip, len}, skip, len, pid, flags, src16 ? src16 : zero,
-			ifs, fr);
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, HostMem{buf, skip, len}, skip, len, pid, flags, fr);
+	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
+		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
 	if (fr.cip) { // what k_cip does for this event
 		uint32_t tb, te;
 		uint8_t cls;

@@ -122,13 +122,14 @@ struct FreshResult {
 	bool cip; // client class pending: decided by the client-IP pass (k_cip)
 };
 
-// Turns a scan into the per-event result and the service key.  Mem supplies
+// Turns a scan into the per-event result and the service key (the client class is decided
+// later: k_cip for a client-IP header, else k_agg_fast by source address).  Mem supplies
 // chunk(c) (the buffer's c-th aligned 16-byte chunk) and ld8(off) (8 bytes at buffer
 // offset off, any alignment; bytes past a span are masked by the caller).
-// pid / flags / src come from the DiscoveryEvent (Discovery.cpp:136, 157).
+// pid / flags come from the DiscoveryEvent (Discovery.cpp:136, 157).
 template <typename Tab, typename Mem>
 EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, const Mem& mem, uint32_t skip,
-		uint32_t L, uint32_t pid, uint8_t flags, const uint8_t* src, const Interfaces& ifs, FreshResult& out) {
+		uint32_t L, uint32_t pid, uint8_t flags, FreshResult& out) {
 	ebd_event_result& r = out.r;
 	r.info = 0;
 	r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
@@ -164,9 +165,7 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 		r.u.span.cip_off = (uint16_t)rescan<RS_CIP>(T, di, sr.cip, wc, skip, L);
 		info |= EBD_INFO_CIP;
 		out.cip = true;
-	} else {
-		info |= (uint8_t)(classify_source(ifs, flags, src) << EBD_INFO_CLASS_SHIFT);
-	}
+	} // else the class comes from the source address (k_agg_fast reads the event)
 	r.info = info;
 	r.u.span.url_off = (uint16_t)url_start;
 	r.u.span.url_len = (uint16_t)url_len;

@@ -166,10 +166,11 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 // k_fresh: one lane per event, DFA table in LDS.
 //
 // A workgroup takes tiles of kTile events and counting-sorts each tile by its number of
-// 16-byte chunks (LDS histogram), so a wave scans 64 buffers of nearly equal length and
-// its lanes finish together.  Buffers are read with 16-byte global loads, one chunk ahead.
-// Per byte: extract, table step, one wave ballot (client-IP value state); per chunk: the
-// crossing trackers of ebd_fresh.h.
+// 16-byte chunks (LDS histogram), longest first, so a wave scans 64 buffers of nearly equal
+// length and its lanes finish together; waves take groups from an LDS counter.  A lane
+// reads its buffer one 128-byte line at a time (8 chunks, the next line in flight).  Per byte:
+// one table step (v_mad_u32_u24 + ds_read_u8) and a running maximum; per chunk: the
+// branch-free crossing trackers of ebd_fresh.h.
 // ---------------------------------------------------------------------------------
 // Logical index (s << 8) | b into the LDS image (ebd_dfa.h kLdsRow / lds_col).
 struct LdsTable {
@@ -226,20 +227,46 @@ __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
 #endif
 }
 
-__device__ __forceinline__ uint32_t event_bin(const Dev& d, uint32_t i) {
-	const uint8_t flags = ((const uint8_t*)(d.ev + i))[32];
+// What fresh_event needs of an event, read once (coalesced) while a tile is binned and kept
+// in LDS in sorted order, so the scan issues no scattered metadata loads.
+struct TileEv {
+	unsigned long long off_idx; // buffer offset (bits 0..47), tile-relative event index (48..63)
+	uint32_t pid;
+	uint16_t len;
+	uint8_t flags;
+	uint8_t kind; // TE_*
+};
+static_assert(sizeof(TileEv) == 16, "tile record is 16 bytes");
+enum : uint8_t { TE_PARSE = 0, TE_SKIP = 1, TE_BAD = 2 };
+
+// Loads one event's record fields; the bin is its chunk count as fresh_event chunks it.
+__device__ __forceinline__ TileEv tile_ev(const Dev& d, uint32_t i, uint32_t t, uint32_t* bin) {
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint8_t flags = evb[32];
+	const uint32_t pid = *(const uint32_t*)evb;
 	const uint32_t L = d.len[i];
-	const uint32_t skip = (uint32_t)(d.off[i] + (uintptr_t)d.payload) & 15u;
-	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || L > EBD_BUFFER_MAX_DATA_SIZE)
-		return 0;
+	const uint64_t off = d.off[i];
+	TileEv te;
+	te.off_idx = (off & 0xffffffffffffull) | ((unsigned long long)t << 48);
+	te.pid = pid;
+	te.flags = flags;
+	te.len = (uint16_t)(L <= EBD_BUFFER_MAX_DATA_SIZE ? L : 0);
+	te.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? TE_SKIP
+	        : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 48) ? TE_BAD : TE_PARSE;
+	const uint32_t skip = (uint32_t)(off + (uintptr_t)d.payload) & 127u;
 	const uint32_t ch = (skip + L + 15) >> 4;
-	return ch < kBins ? ch : kBins - 1;
+	*bin = te.kind != TE_PARSE ? 0 : (ch < kBins ? ch : kBins - 1);
+	return te;
 }
 
 // 16 DFA steps over one chunk; m collects the maximum next state.
 template <bool kFull>
 __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t pos0,
 		uint32_t skip, uint32_t end) {
+#ifdef EBD_EXP_MEMONLY // experiment: the loads without the DFA (results are wrong)
+	m ^= w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
+	return;
+#endif
 	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
@@ -258,25 +285,30 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 	}
 }
 
-// Partial chunk (buffer start or end inside it): compact loop, it is rare.
+// Partial chunk (the buffer starts or ends inside it, or lies outside it): the steps at
+// positions [lo, hi) of the chunk count, the others leave the state alone.
 __device__ __forceinline__ void scan_chunk_masked(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m,
 		uint32_t pos0, uint32_t skip, uint32_t end) {
-	const uint32_t w0 = w.w[0], w1 = w.w[1], w2 = w.w[2], w3 = w.w[3];
-#pragma unroll 1
+#ifdef EBD_EXP_MEMONLY
+	m ^= w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
+	return;
+#endif
+	const int lo = (int)skip - (int)pos0, hi = (int)end - (int)pos0;
+	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
+#pragma unroll
 	for (int k = 0; k < 16; k++) {
-		const uint32_t wk = k < 4 ? w0 : k < 8 ? w1 : k < 12 ? w2 : w3;
-		const uint32_t sn = T[s * kLdsRow + lds_col((wk >> (8 * (k & 3))) & 0xffu)];
-		const bool v = pos0 + k >= skip && pos0 + k < end;
+		const uint32_t sn = T[tab_index(s, wc[k >> 2], k)];
+		const bool v = k >= lo && k < hi;
 		s = v ? sn : s;
 		m = max(m, v ? sn : 0u);
 	}
 }
 
-__device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint32_t i) {
-	const uint8_t* evb = (const uint8_t*)(d.ev + i);
-	const uint8_t flags = evb[32];
-	const uint32_t L = d.len[i];
-	const uint64_t boff = d.off[i]; // loaded with flags and len, before they are tested
+__device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, const TileEv& te, uint32_t base) {
+	const uint32_t i = base + (uint32_t)(te.off_idx >> 48);
+	const uint8_t flags = te.flags;
+	const uint32_t L = te.len;
+	const uint64_t boff = te.off_idx & 0xffffffffffffull;
 	FreshResult fr;
 	fr.r.consumed = 0;
 	fr.r.status = EBD_STATUS_NONE;
@@ -284,25 +316,27 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 	fr.r.u.session.index = 0;
 	fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
 	fr.cip = false;
-	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER) {
-		if (L > EBD_BUFFER_MAX_DATA_SIZE) {
+	if (te.kind != TE_SKIP) {
+		if (te.kind == TE_BAD) {
 			set_error(d, EBD_ERR_BAD_INPUT);
 		} else {
 			const DfaInfo& di = d.di;
 			const uint8_t* p = d.payload + boff;
 			const uintptr_t pa = (uintptr_t)p;
-			const uintptr_t q = pa & ~(uintptr_t)15;
-			const uint32_t skip = (uint32_t)(pa & 15);
+			const uintptr_t q = pa & ~(uintptr_t)127; // the buffer's first 128-byte line
+			const uint32_t skip = (uint32_t)(pa & 127);
 			const uint32_t end = skip + L;
 			const uint32_t nch = (end + 15) >> 4;
 			ScanRec sr;
 			rec_init(di, sr);
 			uint32_t s = di.init;
-			// The buffer is read in windows of 8 chunks (128 B): a lane's 8 loads of a window
-			// are issued back to back, so each 128-B line is used right after it arrives
-			// (16-B reads spread over time let the ~32k concurrent streams of an XCD evict
-			// lines between reads).  The next window is in flight while one is scanned; two
-			// register windows with fixed roles (a register copy of a loaded chunk, or a load
+			// The buffer is read line by line: window j is the j-th 128-byte line from the
+			// one holding the buffer's first byte (8 chunks), its 8 loads issued back to back.
+			// Every 16-B lane load is its own L2 request, and ~32k lanes per XCD keep more
+			// lines in flight than the 4 MB L2 holds, so a line must be consumed by the loads
+			// issued together: windows that straddle lines re-fetched each line (measured
+			// 3.5 L2 misses per line).  The next line is in flight while one is scanned; two
+			// register windows keep fixed roles (a register copy of a loaded chunk, or a load
 			// behind a branch, would make the wave wait for every load).  Loads past the
 			// buffer re-read its last chunk.
 			const uint32_t last = nch ? nch - 1 : 0;
@@ -361,16 +395,14 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, uint
 			d.res[i] = fr.r;
 			return;
 #endif
-			const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP
-			uint8_t src[16];
-			__builtin_memcpy(src, &sv, 16);
-			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q, last}, skip, L, *(const uint32_t*)evb, flags, src, *d.ifs, fr);
+			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q, last}, skip, L, te.pid, flags, fr);
 			if (fr.r.status == EBD_STATUS_FINISHED) {
 				d.keys[i] = fr.key;
 			} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
 				// the session may be saved (Discovery.cpp:148-150): sequential path
+				const EventRec& ev = d.ev[i];
 				atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-				sset_insert(d, *(const uint32_t*)evb, *(const uint32_t*)(evb + 4), *(const uint32_t*)(evb + 8), 0);
+				sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
 			}
 		}
 	}
@@ -388,8 +420,9 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #endif
 	// static LDS: the table sits at LDS address 0, so a step's index is its address
 	__shared__ __attribute__((aligned(16))) uint8_t T[kLdsTableBytes];
-	__shared__ uint16_t perm[kTile];
+	__shared__ TileEv tev[kTile]; // the tile's events in scan order (longest first)
 	__shared__ uint32_t hist[kBins];
+	__shared__ uint32_t next_group;
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kFreshThreads * 16u)
 		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -398,21 +431,26 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
 		const uint32_t base = tile * kTile;
 		const uint32_t cnt = d.n - base < (uint32_t)kTile ? d.n - base : (uint32_t)kTile;
-		__syncthreads(); // previous tile's perm fully consumed; table loaded
+		__syncthreads(); // previous tile's records fully consumed; table loaded
 		if (threadIdx.x < kBins)
 			hist[threadIdx.x] = 0;
+		if (threadIdx.x == 0)
+			next_group = 0;
 		__syncthreads();
 		uint32_t bin[kPer], rank[kPer];
+		TileEv rec[kPer];
 #pragma unroll
 		for (int k = 0; k < kPer; k++) {
 			const uint32_t t = threadIdx.x + k * kFreshThreads;
-			bin[k] = event_bin(d, base + (t < cnt ? t : 0)); // unconditional loads, all in flight
+			rec[k] = tile_ev(d, base + (t < cnt ? t : 0), t, &bin[k]); // unconditional loads, all in flight
 		}
 #pragma unroll
 		for (int k = 0; k < kPer; k++) {
 			const uint32_t t = threadIdx.x + k * kFreshThreads;
-			if (t >= cnt)
-				bin[k] = 0;
+			bin[k] = t < cnt ? kBins - 1 - bin[k] : 0; // longest buffers first
+#ifdef EBD_EXP_NOSORT // experiment: memory order (a wave takes 64 adjacent buffers)
+			bin[k] = 0;
+#endif
 			rank[k] = t < cnt ? atomicAdd(&hist[bin[k]], 1u) : 0;
 		}
 		__syncthreads();
@@ -433,14 +471,27 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #pragma unroll
 		for (int k = 0; k < kPer; k++) {
 			const uint32_t t = threadIdx.x + k * kFreshThreads;
+#ifdef EBD_EXP_NOSORT
 			if (t < cnt)
-				perm[hist[bin[k]] + rank[k]] = (uint16_t)t;
+				tev[t] = rec[k];
+#else
+			if (t < cnt)
+				tev[hist[bin[k]] + rank[k]] = rec[k];
+#endif
 		}
 		__syncthreads();
-		for (uint32_t g = wave; g * 64 < cnt; g += kFreshThreads / 64) {
+		// groups of 64 in descending length; a wave takes the next one when it is free
+		// (longest-first greedy: the short groups at the end even out the waves)
+		for (;;) {
+			uint32_t g = 0;
+			if (lane == 0)
+				g = atomicAdd(&next_group, 1u);
+			g = __builtin_amdgcn_readfirstlane(g);
+			if (g * 64 >= cnt)
+				break;
 			const uint32_t t = g * 64 + lane;
 			if (t < cnt)
-				fresh_event(d, T, base + perm[t]);
+				fresh_event(d, T, tev[t], base);
 		}
 	}
 }
@@ -760,12 +811,21 @@ __global__ void k_carry_pass(Dev d) {
 	}
 }
 
+// Aggregator::newRequest for the fast-path requests, in event order (coalesced reads of the
+// results, keys and events).  A request without a client-IP header is classified here by the
+// session's source address (Aggregator.cpp:60-66, 85-88): k_fresh does not read events.
 __global__ void k_agg_fast(Dev d) {
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
 		const ebd_event_result r = d.res[i];
 		if (r.status != EBD_STATUS_FINISHED || (r.info & EBD_INFO_SESSION))
 			continue;
-		agg_insert(d, d.keys[i], d.seq_base + i, (r.info >> EBD_INFO_CLASS_SHIFT) & 3u);
+		uint32_t cls = (r.info >> EBD_INFO_CLASS_SHIFT) & 3u;
+		if (!(r.info & EBD_INFO_CIP)) {
+			const EventRec& ev = d.ev[i];
+			cls = classify_source(*d.ifs, ev.flags, ev.sourceIP);
+			((uint8_t*)(d.res + i))[3] = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT)); // ebd_event_result.info
+		}
+		agg_insert(d, d.keys[i], d.seq_base + i, cls);
 		atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
 	}
 }
