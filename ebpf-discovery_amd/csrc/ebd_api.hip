@@ -20,7 +20,6 @@ hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
-hipError_t launch_cip(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
@@ -78,7 +77,6 @@ struct ebd_ctx {
 	uint32_t max_events = 0;
 	ebd_event_result* d_res = nullptr;
 	Hash128* d_keys = nullptr;
-	uint32_t* d_cipq = nullptr;
 	SSlot* d_sset = nullptr;
 	uint32_t sset_cap = 0;
 	uint32_t* d_dirty = nullptr;
@@ -121,8 +119,8 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify", "k_cip"};
-enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_CIP, KT_N };
+		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_N };
 
 static hipEvent_t take_event(ebd_ctx* c) {
 	if (!c->free_events.empty()) {
@@ -169,7 +167,6 @@ static Dev make_dev(ebd_ctx* c) {
 	d.ifs = c->d_ifs;
 	d.res = c->d_res;
 	d.keys = c->d_keys;
-	d.cipq = c->d_cipq;
 	d.slots = c->d_slots;
 	d.slot_mask = c->slot_cap - 1;
 	d.new_slots = c->d_new_slots;
@@ -195,7 +192,7 @@ static Dev make_dev(ebd_ctx* c) {
 }
 
 static void ctx_free(ebd_ctx* c) {
-	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys, c->d_cipq,
+	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload};
 	for (void* p : ptrs)
@@ -294,7 +291,6 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	const uint64_t n = c->max_events;
 	CTX_TRY(hipMalloc(&c->d_res, n * sizeof(ebd_event_result)));
 	CTX_TRY(hipMalloc(&c->d_keys, n * sizeof(Hash128)));
-	CTX_TRY(hipMalloc(&c->d_cipq, n * sizeof(uint32_t)));
 	const uint32_t lru = cfg->lru_capacity ? cfg->lru_capacity : EBD_MAX_SESSIONS;
 	c->carry_cap = lru;
 	c->sset_cap = next_pow2(2 * (n + lru));
@@ -397,8 +393,6 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		if (c->n_carry)
 			HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
 	}
-	if (c->h_ctr[CTR_CIPQ])
-		HIP_TRY(timed(c, KT_CIP, [&] { return launch_cip(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_REPS, [&] { return launch_reps(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
@@ -827,7 +821,7 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 	fresh_finalize(HostTab{t->next}, t->info, sr, s, HostMem{buf, skip, len}, skip, len, pid, flags, fr);
 	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
 		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
-	if (fr.cip) { // what k_cip does for this event
+	if (fr.cip) { // what k_agg_fast (cip_classify) does for this event
 		uint32_t tb, te;
 		uint8_t cls;
 		cip_token(ifs, [buf](uint32_t b) { return (uint32_t)buf[b]; }, fr.r.u.span.cip_off, fr.r.consumed, &tb, &te, &cls);

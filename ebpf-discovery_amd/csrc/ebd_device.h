@@ -70,9 +70,8 @@ enum Ctr : uint32_t {
 	CTR_DIRTY,          // session-set slots claimed in this batch
 	CTR_INSERTS,        // LRU inserts in this batch
 	CTR_VERIFY,         // deferred service-key verifications
-	CTR_CIPQ,           // fast-path requests queued for the client-IP pass
-	CTR_BATCH_END = 10,
-	CTR_SARENA = 10,    // service string arena bytes used
+	CTR_BATCH_END = 9,
+	CTR_SARENA = 9,     // service string arena bytes used
 	CTR_ERRORS,         // EBD_ERR_* bitmask
 	CTR_COLLISIONS,
 	CTR_KDELETES,
@@ -102,7 +101,6 @@ struct Dev {
 	// per-event outputs
 	ebd_event_result* res;
 	Hash128* keys;
-	uint32_t* cipq; // events queued for k_cip (capacity n)
 	// service table
 	Slot* slots;
 	uint32_t slot_mask;

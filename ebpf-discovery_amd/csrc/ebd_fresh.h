@@ -119,11 +119,11 @@ EBD_HD uint32_t rescan(const Tab& T, const DfaInfo& di, uint32_t rec, const Chun
 struct FreshResult {
 	ebd_event_result r;
 	Hash128 key;
-	bool cip; // client class pending: decided by the client-IP pass (k_cip)
+	bool cip; // client class pending: decided from the client-IP token (k_agg_fast, cip_classify)
 };
 
 // Turns a scan into the per-event result and the service key (the client class is decided
-// later: k_cip for a client-IP header, else k_agg_fast by source address).  Mem supplies
+// later by k_agg_fast: the client-IP front token if there is one, else the source address).  Mem supplies
 // chunk(c) (the buffer's c-th aligned 16-byte chunk) and ld8(off) (8 bytes at buffer
 // offset off, any alignment; bytes past a span are masked by the caller).
 // pid / flags come from the DiscoveryEvent (Discovery.cpp:136, 157).
@@ -161,7 +161,7 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	}
 	uint8_t info = (uint8_t)((post ? EBD_INFO_POST : 0) | ((flags & 16) ? EBD_INFO_HTTPS : 0));
 	if (cip) {
-		// raw value start of the first client-IP header; token and class: k_cip
+		// raw value start of the first client-IP header; token and class: k_agg_fast
 		r.u.span.cip_off = (uint16_t)rescan<RS_CIP>(T, di, sr.cip, wc, skip, L);
 		info |= EBD_INFO_CIP;
 		out.cip = true;

@@ -43,9 +43,18 @@ __device__ __forceinline__ unsigned int rmw_read(unsigned int* p) { return atomi
 __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, uint32_t cls) {
 	uint32_t idx = (uint32_t)h.lo & d.slot_mask;
 	bool found = false;
+	unsigned long long seen_min = 0;
 	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
 		Slot* s = d.slots + idx;
-		unsigned long long t = ld_relaxed(&s->tag);
+		// One plain load pass over the slot's first 32 bytes.  tag and hi are written once
+		// (0 -> value), min_seq only decreases: a stale copy at worst shows 0 (resolved by
+		// the CAS below, or the coherent re-read of hi) or a larger min_seq (a redundant
+		// atomicMin).  Slot words are only ever written by atomics here, so no dirty line
+		// sits in L2 when the next kernel starts.
+		const ulonglong2 th = *(const ulonglong2*)&s->tag;
+		const ulonglong2 mo = *(const ulonglong2*)&s->min_seq;
+		seen_min = mo.x;
+		unsigned long long t = th.x;
 		bool claimed = false;
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, h.lo);
@@ -57,6 +66,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 				else
 					set_error(d, EBD_ERR_TABLE_FULL);
 				claimed = true;
+				seen_min = ~0ull;
 			}
 		}
 		if (claimed) {
@@ -64,7 +74,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 			break;
 		}
 		if (t == h.lo) {
-			unsigned long long hi = ld_relaxed(&s->hi);
+			unsigned long long hi = th.y;
 			if (hi == 0)
 				hi = rmw_read(&s->hi);
 			if (hi == 0) { // claimer's store not visible yet: verify after this kernel
@@ -95,7 +105,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 		atomicAdd(&s->internal_clients, 1u);
 	else if (cls == CLS_EXTERNAL)
 		atomicAdd(&s->external_clients, 1u);
-	if (seq < ld_relaxed(&s->min_seq))
+	if (seq < seen_min)
 		atomicMin(&s->min_seq, seq);
 	return idx;
 }
@@ -407,10 +417,6 @@ __device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, cons
 		}
 	}
 	d.res[i] = fr.r;
-	if (fr.cip) {
-		const unsigned long long k = atomicAdd(&d.ctr[CTR_CIPQ], 1ull);
-		d.cipq[k] = i; // capacity n: at most one entry per event
-	}
 }
 
 #ifdef EBD_EXP_LB8 // experiment: two workgroups per CU
@@ -497,51 +503,41 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 }
 
 // ---------------------------------------------------------------------------------
-// k_cip: client-IP token and class for the fast-path requests that carry a client-IP
-// header (queued by k_fresh).  Each lane copies the value's first kCipRaw bytes into its
-// own LDS row with 8-byte loads, then runs front_token / inet_pton there.
+// Client-IP token and class of a fast-path request that carries a client-IP header
+// (HttpRequestParser.cpp:370-407 on the first client-IP value, Aggregator.cpp:50-74 on its
+// front token).  k_fresh found where the value starts; the lane copies the value's first
+// kCipRaw bytes into its LDS row with 8-byte loads and parses the token there.
 // ---------------------------------------------------------------------------------
-constexpr int kCipThreads = 256;
+constexpr int kAggThreads = 256;
 constexpr int kCipRaw = 64;
 constexpr int kCipStride = kCipRaw + 8; // rows 72 B apart: lanes spread over the banks
 
-__global__ __launch_bounds__(kCipThreads) void k_cip(Dev d) {
-	__shared__ __attribute__((aligned(8))) uint8_t rows[kCipThreads * kCipStride];
-	const unsigned long long nq = d.ctr[CTR_CIPQ];
-	uint8_t* row = rows + threadIdx.x * kCipStride;
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nq; k += gridDim.x * blockDim.x) {
-		const uint32_t i = d.cipq[k];
-		ebd_event_result r = d.res[i];
-		const uint8_t* p = d.payload + d.off[i];
-		const uint32_t cs = r.u.span.cip_off, lim = r.consumed;
-		unsigned long long v[kCipRaw / 8];
+__device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_event_result& r, uint8_t* row) {
+	const uint8_t* p = d.payload + d.off[i];
+	const uint32_t cs = r.u.span.cip_off, lim = r.consumed; // the value ends before the final CRLF
+	unsigned long long v[kCipRaw / 8];
 #pragma unroll
-		for (int h = 0; h < kCipRaw / 8; h++)
-			v[h] = gload8u(p + cs + 8 * h);
+	for (int h = 0; h < kCipRaw / 8; h++) // past the request: re-read its last byte (stays in the buffer)
+		v[h] = gload8u(p + min(cs + 8 * h, lim - 1));
 #pragma unroll
-		for (int h = 0; h < kCipRaw / 8; h++)
-			*(unsigned long long*)(row + 8 * h) = v[h];
-		uint32_t tb, te;
-		uint8_t cls;
-		if (cs + kCipRaw < lim) { // value may run past the copy: decide on the copy if it ends inside
-			uint32_t e = 0;
-			while (e < kCipRaw && row[e] != ',' && row[e] != '\r')
-				e++;
-			if (e < kCipRaw) {
-				cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls);
-			} else {
-				cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls);
-				tb -= cs;
-				te -= cs;
-			}
-		} else {
-			cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, lim - cs, &tb, &te, &cls);
-		}
-		r.u.span.cip_off = (uint16_t)(cs + tb);
-		r.u.span.cip_len = (uint16_t)(te - tb);
-		r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
-		d.res[i] = r;
+	for (int h = 0; h < kCipRaw / 8; h++)
+		*(unsigned long long*)(row + 8 * h) = v[h];
+	uint32_t tb, te;
+	uint8_t cls;
+	const uint32_t avail = lim - cs < (uint32_t)kCipRaw ? lim - cs : (uint32_t)kCipRaw; // valid bytes in the row
+	uint32_t e = 0;
+	while (e < avail && row[e] != ',' && row[e] != '\r')
+		e++;
+	if (e < avail || avail == lim - cs) {
+		cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls);
+	} else { // a value longer than the copy without ',' or CR in it: parse from the buffer
+		cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls);
+		tb -= cs;
+		te -= cs;
 	}
+	r.u.span.cip_off = (uint16_t)(cs + tb);
+	r.u.span.cip_len = (uint16_t)(te - tb);
+	return cls;
 }
 
 __global__ void k_carry_insert(Dev d) {
@@ -812,22 +808,40 @@ __global__ void k_carry_pass(Dev d) {
 }
 
 // Aggregator::newRequest for the fast-path requests, in event order (coalesced reads of the
-// results, keys and events).  A request without a client-IP header is classified here by the
-// session's source address (Aggregator.cpp:60-66, 85-88): k_fresh does not read events.
-__global__ void k_agg_fast(Dev d) {
+// results, keys and events).  The client class comes from the client-IP header's front token
+// when k_fresh found one (cip_classify), else from the session's source address
+// (Aggregator.cpp:60-66, 85-88).  Requests are counted per block: one global atomic each.
+__global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
+	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
+	__shared__ unsigned long long nreq;
+	uint8_t* row = rows + threadIdx.x * kCipStride;
+	if (threadIdx.x == 0)
+		nreq = 0;
+	__syncthreads();
+	uint32_t cnt = 0;
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
-		const ebd_event_result r = d.res[i];
+		ebd_event_result r = d.res[i];
 		if (r.status != EBD_STATUS_FINISHED || (r.info & EBD_INFO_SESSION))
 			continue;
-		uint32_t cls = (r.info >> EBD_INFO_CLASS_SHIFT) & 3u;
-		if (!(r.info & EBD_INFO_CIP)) {
-			const EventRec& ev = d.ev[i];
-			cls = classify_source(*d.ifs, ev.flags, ev.sourceIP);
-			((uint8_t*)(d.res + i))[3] = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT)); // ebd_event_result.info
+		uint32_t cls;
+		if (r.info & EBD_INFO_CIP) {
+			cls = cip_classify(d, i, r, row);
+		} else {
+			const uint8_t* evb = (const uint8_t*)(d.ev + i);
+			const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
+			uint8_t src[16];
+			__builtin_memcpy(src, &sv, 16);
+			cls = classify_source(*d.ifs, evb[32], src);
 		}
+		r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+		d.res[i] = r;
 		agg_insert(d, d.keys[i], d.seq_base + i, cls);
-		atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
+		cnt++;
 	}
+	atomicAdd(&nreq, (unsigned long long)cnt);
+	__syncthreads();
+	if (threadIdx.x == 0 && nreq)
+		atomicAdd(&d.ctr[CTR_REQUESTS], nreq);
 }
 
 // First-arrival representative of every service created in this batch (Aggregator.cpp:
@@ -974,10 +988,6 @@ hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
-hipError_t launch_cip(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_cip, dim3(cus * 4), dim3(kCipThreads), 0, st, d);
-	return hipGetLastError();
-}
 hipError_t launch_carry_insert(const Dev& d, hipStream_t st) {
 	hipLaunchKernelGGL(k_carry_insert, dim3(grid_for(d.n_carry_in, 256, 256)), dim3(256), 0, st, d);
 	return hipGetLastError();
@@ -995,7 +1005,7 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
 	return hipGetLastError();
 }
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_agg_fast, dim3(grid_for(d.n, 256, cus * 8)), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_agg_fast, dim3(grid_for(d.n, kAggThreads, cus * 8)), dim3(kAggThreads), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus) {
