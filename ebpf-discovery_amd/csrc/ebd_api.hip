@@ -584,6 +584,7 @@ int ebd_clear(ebd_ctx* c) {
 	HIP_TRY(hipSetDevice(c->device));
 	HIP_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
@@ -603,6 +604,7 @@ int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 	s->live_sessions = c->n_carry;
 	s->max_live_sessions = c->max_live;
 	s->hash_collisions = c->h_ctr[CTR_COLLISIONS];
+	s->services = c->h_ctr[CTR_SERVICES];
 	s->errors = c->h_ctr[CTR_ERRORS];
 	return 0;
 }

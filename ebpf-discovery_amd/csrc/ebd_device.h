@@ -77,6 +77,7 @@ enum Ctr : uint32_t {
 	CTR_KDELETES,
 	CTR_REQUESTS,
 	CTR_SESSION_EVENTS,
+	CTR_SERVICES,       // services in the table (sum of CTR_NEW over batches)
 	CTR_COUNT = 16,
 };
 

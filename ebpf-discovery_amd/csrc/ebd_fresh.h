@@ -145,6 +145,13 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	const Chunk wt = mem.chunk(sr.term >> 8), wu = mem.chunk(sr.url >> 8), wh = mem.chunk(sr.host >> 8),
 	            we = mem.chunk(sr.hend >> 8), wc = mem.chunk(sr.cip >> 8);
 	const uint32_t consumed = rescan<RS_TERM>(T, di, sr.term, wt, skip, L) + 1;
+	if (consumed > L) {
+		// the device scans whole chunks: a terminal state reached only past the buffer's
+		// last byte is an unfinished parse (HttpRequestParser.cpp:85-106 stops at L)
+		r.status = EBD_STATUS_UNFINISHED;
+		r.consumed = (uint16_t)L;
+		return;
+	}
 	r.consumed = (uint16_t)consumed;
 	if (!fin) {
 		r.status = EBD_STATUS_INVALID;

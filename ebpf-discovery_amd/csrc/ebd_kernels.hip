@@ -173,14 +173,27 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 }
 
 // ---------------------------------------------------------------------------------
-// k_fresh: one lane per event, DFA table in LDS.
+// k_fresh: one lane per event, DFA table in LDS, events pulled from a workgroup queue.
 //
-// A workgroup takes tiles of kTile events and counting-sorts each tile by its number of
-// 16-byte chunks (LDS histogram), longest first, so a wave scans 64 buffers of nearly equal
-// length and its lanes finish together; waves take groups from an LDS counter.  A lane
-// reads its buffer one 128-byte line at a time (8 chunks, the next line in flight).  Per byte:
-// one table step (v_mad_u32_u24 + ds_read_u8) and a running maximum; per chunk: the
-// branch-free crossing trackers of ebd_fresh.h.
+// Memory layout decides this kernel's speed (tools/ubench_mem2.hip): buffers read a 64-B
+// window at a time, the four lanes of a quad loading 64 contiguous bytes of one member's
+// window per instruction (4 instructions = one window for each member), then a 4x4 block
+// transpose inside the quad (DPP) hands every lane its own window.  Each workgroup owns a
+// contiguous range of the batch and its lanes take the next event from an LDS counter when
+// they finish one, so the chip streams the payload roughly in memory order and no lane waits
+// for a longer neighbour.  The next window is loaded while the current one is scanned; it is
+// predicted as "the same buffer's next window, or the lane's next event's first window", and
+// a buffer that terminates early (POST body, invalid byte) costs one idle window.
+//
+// Chunks are event-relative (chunk c = bytes [16c, 16c + 16) of the buffer, unaligned loads):
+// there is no leading skip.  The last chunk may extend past the buffer; the DFA steps over
+// those bytes too, which can only change states at positions >= L: a terminal position >= L
+// is an unfinished parse (fresh_finalize), and every other tracked position is < L.
+//
+// Per byte: one table step (v_mad_u32_u24 + ds_read_u8) and a running maximum; per chunk:
+// the branch-free crossing trackers of ebd_fresh.h.  A lane that finishes a buffer appends
+// its scan record to the wave's queue in LDS; 64 records are finalized together (rescans,
+// spans, key), so the finalize code always runs on a full wave.
 // ---------------------------------------------------------------------------------
 // Logical index (s << 8) | b into the LDS image (ebd_dfa.h kLdsRow / lds_col).
 struct LdsTable {
@@ -189,10 +202,11 @@ struct LdsTable {
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef v4u v4u_a1 __attribute__((aligned(1)));
 typedef unsigned long long u64a1 __attribute__((aligned(1)));
-// 16-byte load through a global (not flat) pointer: global_load_dwordx4
+// 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
 __device__ __forceinline__ Chunk gload16(uintptr_t a) {
-	const v4u v = *(const __attribute__((address_space(1))) v4u*)a;
+	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
 	Chunk c;
 	c.w[0] = v.x;
 	c.w[1] = v.y;
@@ -205,19 +219,19 @@ __device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
 	return *(const __attribute__((address_space(1))) u64a1*)a;
 }
 
-// Buffer access for fresh_finalize on the device.  The payload must stay readable up to
-// the next 16-byte boundary after each buffer plus 8 bytes (ebd_api.hip pads it).
+// Buffer access for fresh_finalize on the device: chunk c = bytes [16c, 16c + 16) of the
+// buffer (clamped to its last chunk).  The payload stays readable EBD_PAYLOAD_PAD bytes past
+// each buffer (ebd_api.hip pads it).
 struct DevMem {
 	const uint8_t* p;
-	uintptr_t q; // p rounded down to 16
 	uint32_t last; // last chunk index of the buffer
-	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16(q + 16 * (uintptr_t)min(c, last)); }
+	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16((uintptr_t)p + 16 * (uintptr_t)min(c, last)); }
 	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
 };
 
 constexpr int kFreshThreads = 1024;
-constexpr int kTile = 4096;
-constexpr int kBins = 128;
+constexpr int kFreshWaves = kFreshThreads / 64;
+constexpr uint32_t kQueue = 128; // finalize records per wave (<= 63 waiting + 64 pushed)
 
 // A chunk word with every byte b replaced by lds_col(b) (5 VALU per 4 bytes).
 __device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
@@ -237,42 +251,8 @@ __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
 #endif
 }
 
-// What fresh_event needs of an event, read once (coalesced) while a tile is binned and kept
-// in LDS in sorted order, so the scan issues no scattered metadata loads.
-struct TileEv {
-	unsigned long long off_idx; // buffer offset (bits 0..47), tile-relative event index (48..63)
-	uint32_t pid;
-	uint16_t len;
-	uint8_t flags;
-	uint8_t kind; // TE_*
-};
-static_assert(sizeof(TileEv) == 16, "tile record is 16 bytes");
-enum : uint8_t { TE_PARSE = 0, TE_SKIP = 1, TE_BAD = 2 };
-
-// Loads one event's record fields; the bin is its chunk count as fresh_event chunks it.
-__device__ __forceinline__ TileEv tile_ev(const Dev& d, uint32_t i, uint32_t t, uint32_t* bin) {
-	const uint8_t* evb = (const uint8_t*)(d.ev + i);
-	const uint8_t flags = evb[32];
-	const uint32_t pid = *(const uint32_t*)evb;
-	const uint32_t L = d.len[i];
-	const uint64_t off = d.off[i];
-	TileEv te;
-	te.off_idx = (off & 0xffffffffffffull) | ((unsigned long long)t << 48);
-	te.pid = pid;
-	te.flags = flags;
-	te.len = (uint16_t)(L <= EBD_BUFFER_MAX_DATA_SIZE ? L : 0);
-	te.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? TE_SKIP
-	        : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 48) ? TE_BAD : TE_PARSE;
-	const uint32_t skip = (uint32_t)(off + (uintptr_t)d.payload) & 127u;
-	const uint32_t ch = (skip + L + 15) >> 4;
-	*bin = te.kind != TE_PARSE ? 0 : (ch < kBins ? ch : kBins - 1);
-	return te;
-}
-
 // 16 DFA steps over one chunk; m collects the maximum next state.
-template <bool kFull>
-__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t pos0,
-		uint32_t skip, uint32_t end) {
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m) {
 #ifdef EBD_EXP_MEMONLY // experiment: the loads without the DFA (results are wrong)
 	m ^= w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
 	return;
@@ -280,224 +260,314 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
-		const uint32_t sn = T[tab_index(s, wc[k >> 2], k)];
-		if (kFull) {
-			s = sn;
-			if (k & 1)
-				m = max(m, s);
-			else
-				m = max(m, sn); // pairs fold into v_max3
-		} else {
-			const bool v = pos0 + k >= skip && pos0 + k < end;
-			s = v ? sn : s;
-			m = max(m, v ? sn : 0u);
-		}
+		s = T[tab_index(s, wc[k >> 2], k)];
+		m = max(m, s); // pairs fold into v_max3
 	}
 }
 
-// Partial chunk (the buffer starts or ends inside it, or lies outside it): the steps at
-// positions [lo, hi) of the chunk count, the others leave the state alone.
-__device__ __forceinline__ void scan_chunk_masked(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m,
-		uint32_t pos0, uint32_t skip, uint32_t end) {
-#ifdef EBD_EXP_MEMONLY
-	m ^= w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
-	return;
-#endif
-	const int lo = (int)skip - (int)pos0, hi = (int)end - (int)pos0;
-	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
+// quad_perm DPP: the value of `v` held by quad lane P's pattern
+template <int P>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, P, 0xf, 0xf, true); }
+constexpr int kQX2 = 2 | (3 << 2) | (0 << 4) | (1 << 6); // lane r takes lane r ^ 2
+constexpr int kQX1 = 1 | (0 << 2) | (3 << 4) | (2 << 6); // lane r takes lane r ^ 1
+template <int K>
+__device__ __forceinline__ uint32_t qbcast(uint32_t v) { return qperm<K | (K << 2) | (K << 4) | (K << 6)>(v); }
+template <int K>
+__device__ __forceinline__ unsigned long long qbcast64(unsigned long long v) {
+	return (unsigned long long)qbcast<K>((uint32_t)v) | ((unsigned long long)qbcast<K>((uint32_t)(v >> 32)) << 32);
+}
+
+// 4x4 transpose of 16-B blocks among the 4 lanes of a quad: lane r holds X[k] = piece r of
+// member k's window; afterwards it holds piece k of its own window.
+__device__ __forceinline__ void transpose_quad(Chunk (&X)[4], uint32_t r) {
+	const bool lo2 = r < 2, lo1 = (r & 1) == 0;
 #pragma unroll
-	for (int k = 0; k < 16; k++) {
-		const uint32_t sn = T[tab_index(s, wc[k >> 2], k)];
-		const bool v = k >= lo && k < hi;
-		s = v ? sn : s;
-		m = max(m, v ? sn : 0u);
-	}
+	for (int k = 0; k < 2; k++)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t recv = qperm<kQX2>(lo2 ? X[k + 2].w[d] : X[k].w[d]);
+			X[k + 2].w[d] = lo2 ? recv : X[k + 2].w[d];
+			X[k].w[d] = lo2 ? X[k].w[d] : recv;
+		}
+#pragma unroll
+	for (int k = 0; k < 4; k += 2)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t recv = qperm<kQX1>(lo1 ? X[k + 1].w[d] : X[k].w[d]);
+			X[k + 1].w[d] = lo1 ? recv : X[k + 1].w[d];
+			X[k].w[d] = lo1 ? X[k].w[d] : recv;
+		}
 }
 
-__device__ __forceinline__ void fresh_event(const Dev& d, const uint8_t* T, const TileEv& te, uint32_t base) {
-	const uint32_t i = base + (uint32_t)(te.off_idx >> 48);
-	const uint8_t flags = te.flags;
-	const uint32_t L = te.len;
-	const uint64_t boff = te.off_idx & 0xffffffffffffull;
+// An event as a lane holds it.  kind: EK_PARSE (a buffer to scan), EK_SKIP (no parse:
+// not NEW_DATA or the saved buffer is missing, Discovery.cpp:99-110), EK_BAD (length or
+// offset out of range), EK_NONE (the workgroup's range is exhausted).
+enum : uint32_t { EK_PARSE = 0, EK_SKIP = 1, EK_BAD = 2, EK_NONE = 3 };
+struct LaneEv {
+	uint32_t idx;
+	uint32_t L;       // buffer length (0 unless EK_PARSE)
+	uint32_t kind;
+	const uint8_t* p; // buffer (a harmless valid address unless EK_PARSE)
+};
+
+__device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end) {
+	LaneEv e;
+	e.idx = i;
+	if (i >= end) {
+		e.kind = EK_NONE;
+		e.L = 0;
+		e.p = d.payload;
+		return e;
+	}
+	const uint32_t flags = ((const uint8_t*)(d.ev + i))[32];
+#ifdef EBD_EXP_L2ONLY // experiment: every event parses one of the first 4096 buffers (L2-resident)
+	const uint32_t L = d.len[i & 4095];
+	const uint64_t off = d.off[i & 4095];
+#else
+	const uint32_t L = d.len[i];
+	const uint64_t off = d.off[i];
+#endif
+	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 48) ? EK_BAD : EK_PARSE;
+	e.L = e.kind == EK_PARSE ? L : 0;
+	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
+	return e;
+}
+
+// A finished scan waiting for fresh_finalize (40 B).
+struct FinRec {
+	unsigned long long pl; // buffer address (bits 0..47) | L << 48
+	uint32_t idx;
+	uint32_t sf;           // final state | cseen << 8
+	uint32_t url, host, hend, cip, term;
+	uint32_t pad;
+};
+static_assert(sizeof(FinRec) == 40, "finalize record is 40 bytes");
+
+__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q) {
+	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
+	const uint32_t L = (uint32_t)(q.pl >> 48);
+	const uint32_t i = q.idx;
+#ifdef EBD_EXP_FINWRITE // experiment: finalize writes a placeholder result (results are wrong)
+	{
+		ebd_event_result r;
+		r.consumed = (uint16_t)L;
+		r.status = EBD_STATUS_INVALID;
+		r.info = (uint8_t)q.sf;
+		r.u.session.index = q.url ^ q.host ^ q.hend ^ q.cip ^ q.term;
+		r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
+		d.res[i] = r;
+		return;
+	}
+#endif
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint8_t flags = evb[32];
+	const uint32_t pid = *(const uint32_t*)evb;
+	ScanRec sr;
+	sr.url = q.url;
+	sr.host = q.host;
+	sr.hend = q.hend;
+	sr.cip = q.cip;
+	sr.term = q.term;
+	sr.cseen = (q.sf >> 8) & 1u;
 	FreshResult fr;
-	fr.r.consumed = 0;
-	fr.r.status = EBD_STATUS_NONE;
-	fr.r.info = 0;
-	fr.r.u.session.index = 0;
-	fr.r.u.session.pad_[0] = fr.r.u.session.pad_[1] = 0;
-	fr.cip = false;
-	if (te.kind != TE_SKIP) {
-		if (te.kind == TE_BAD) {
-			set_error(d, EBD_ERR_BAD_INPUT);
-		} else {
-			const DfaInfo& di = d.di;
-			const uint8_t* p = d.payload + boff;
-			const uintptr_t pa = (uintptr_t)p;
-			const uintptr_t q = pa & ~(uintptr_t)127; // the buffer's first 128-byte line
-			const uint32_t skip = (uint32_t)(pa & 127);
-			const uint32_t end = skip + L;
-			const uint32_t nch = (end + 15) >> 4;
-			ScanRec sr;
-			rec_init(di, sr);
-			uint32_t s = di.init;
-			// The buffer is read line by line: window j is the j-th 128-byte line from the
-			// one holding the buffer's first byte (8 chunks), its 8 loads issued back to back.
-			// Every 16-B lane load is its own L2 request, and ~32k lanes per XCD keep more
-			// lines in flight than the 4 MB L2 holds, so a line must be consumed by the loads
-			// issued together: windows that straddle lines re-fetched each line (measured
-			// 3.5 L2 misses per line).  The next line is in flight while one is scanned; two
-			// register windows keep fixed roles (a register copy of a loaded chunk, or a load
-			// behind a branch, would make the wave wait for every load).  Loads past the
-			// buffer re-read its last chunk.
-			const uint32_t last = nch ? nch - 1 : 0;
-			Chunk A[8], B[8];
-			auto ldw = [&](Chunk(&w)[8], uint32_t j) {
-#pragma unroll
-				for (int k = 0; k < 8; k++)
-					w[k] = gload16(q + 16 * (uintptr_t)min(8 * j + k, last));
-			};
-			bool live = nch > 0;
-			// One chunk for every lane (a no-op for lanes already done): DFA steps, then the
-			// trackers.  The only exits are uniform.
-			auto step = [&](const Chunk& w, uint32_t c) {
-				uint32_t sx = s, m = 0;
-				const bool full = c * 16 >= skip && c * 16 + 16 <= end;
-				if (__all(full))
-					scan_chunk<true>(T, w, sx, m, c * 16, skip, end);
-				else
-					scan_chunk_masked(T, w, sx, m, c * 16, skip, end);
-				if (live) {
-					if (st_terminal(di, sx)) {
-						sr.term = (c << 8) | s;
-						sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
-						live = false;
-					} else {
-						chunk_track(di, sr, c, sx, m >= 254);
-						live = c + 1 < nch;
-					}
-					s = sx;
-				}
-			};
-			ldw(A, 0);
-			for (uint32_t j = 0;; j += 2) {
-				ldw(B, j + 1);
-#pragma unroll
-				for (int k = 0; k < 8; k++) {
-					step(A[k], 8 * j + k);
-					if (!__any(live))
-						break;
-				}
-				if (!__any(live))
-					break;
-				ldw(A, j + 2);
-#pragma unroll
-				for (int k = 0; k < 8; k++) {
-					step(B[k], 8 * (j + 1) + k);
-					if (!__any(live))
-						break;
-				}
-				if (!__any(live))
-					break;
-			}
-#ifdef EBD_EXP_SCANONLY // experiment: scan cost alone (results are wrong)
-			fr.r.consumed = (uint16_t)s;
-			fr.r.u.span.url_off = (uint16_t)(sr.url ^ sr.host ^ sr.hend ^ sr.cip ^ sr.term ^ sr.cseen);
-			d.res[i] = fr.r;
-			return;
-#endif
-			fresh_finalize(LdsTable{T}, di, sr, s, DevMem{p, q, last}, skip, L, te.pid, flags, fr);
-			if (fr.r.status == EBD_STATUS_FINISHED) {
-				d.keys[i] = fr.key;
-			} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
-				// the session may be saved (Discovery.cpp:148-150): sequential path
-				const EventRec& ev = d.ev[i];
-				atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-				sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
-			}
-		}
+	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, DevMem{p, L ? (L - 1) / 16 : 0}, 0, L, pid, flags, fr);
+	if (fr.r.status == EBD_STATUS_FINISHED) {
+		d.keys[i] = fr.key;
+	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+		// the session may be saved (Discovery.cpp:148-150): sequential path
+		const EventRec& ev = d.ev[i];
+		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
 	}
 	d.res[i] = fr.r;
 }
 
-#ifdef EBD_EXP_LB8 // experiment: two workgroups per CU
-__global__ __launch_bounds__(kFreshThreads, 8) void k_fresh(Dev d) {
-#else
+__device__ __forceinline__ void write_none(const Dev& d, uint32_t i) {
+	ebd_event_result r;
+	r.consumed = 0;
+	r.status = EBD_STATUS_NONE;
+	r.info = 0;
+	r.u.session.index = 0;
+	r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
+	d.res[i] = r;
+}
+
+// A NEW_DATA event with an empty buffer: a fresh parser consumes nothing and is left
+// unfinished, so the session may be saved (Discovery.cpp:141-159).
+__device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
+	ebd_event_result r;
+	r.consumed = 0;
+	r.status = EBD_STATUS_UNFINISHED;
+	r.info = 0;
+	r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
+	d.res[i] = r;
+	const EventRec& ev = d.ev[i];
+	atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
+}
+
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
-#endif
 	// static LDS: the table sits at LDS address 0, so a step's index is its address
 	__shared__ __attribute__((aligned(16))) uint8_t T[kLdsTableBytes];
-	__shared__ TileEv tev[kTile]; // the tile's events in scan order (longest first)
-	__shared__ uint32_t hist[kBins];
-	__shared__ uint32_t next_group;
+	__shared__ FinRec fq[kFreshWaves][kQueue];
+	__shared__ uint32_t next_ev;
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 3;
+	// this workgroup's contiguous share of the batch
+	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
+	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per);
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kFreshThreads * 16u)
 		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
-	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-	constexpr int kPer = kTile / kFreshThreads;
-	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
-	for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-		const uint32_t base = tile * kTile;
-		const uint32_t cnt = d.n - base < (uint32_t)kTile ? d.n - base : (uint32_t)kTile;
-		__syncthreads(); // previous tile's records fully consumed; table loaded
-		if (threadIdx.x < kBins)
-			hist[threadIdx.x] = 0;
-		if (threadIdx.x == 0)
-			next_group = 0;
-		__syncthreads();
-		uint32_t bin[kPer], rank[kPer];
-		TileEv rec[kPer];
-#pragma unroll
-		for (int k = 0; k < kPer; k++) {
-			const uint32_t t = threadIdx.x + k * kFreshThreads;
-			rec[k] = tile_ev(d, base + (t < cnt ? t : 0), t, &bin[k]); // unconditional loads, all in flight
-		}
-#pragma unroll
-		for (int k = 0; k < kPer; k++) {
-			const uint32_t t = threadIdx.x + k * kFreshThreads;
-			bin[k] = t < cnt ? kBins - 1 - bin[k] : 0; // longest buffers first
-#ifdef EBD_EXP_NOSORT // experiment: memory order (a wave takes 64 adjacent buffers)
-			bin[k] = 0;
+	if (threadIdx.x == 0)
+		next_ev = rb + kFreshThreads * 2;
+	__syncthreads();
+	const DfaInfo& di = d.di;
+	FinRec* const q = fq[wave];
+	uint32_t qn = 0; // records waiting in q (wave-uniform)
+
+	auto grab = [&]() -> uint32_t { return atomicAdd(&next_ev, 1u); };
+	// the lane's current event (e0) and the next one (e1, whose record arrives early)
+	LaneEv e0 = lane_ev(d, rb + threadIdx.x, re);
+	LaneEv e1 = lane_ev(d, rb + kFreshThreads + threadIdx.x, re);
+	uint32_t w0 = 0; // e0's window to scan next
+	uint32_t s = di.init, live = 0;
+	ScanRec sr;
+	rec_init(di, sr);
+
+	// Finalize the first min(qn, 64) queued records (one per lane) and move the rest down.
+	auto flush = [&]() {
+		const uint32_t cnt = qn < 64 ? qn : 64;
+#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
+		if (lane < cnt)
+			finalize_rec(d, T, q[lane]);
 #endif
-			rank[k] = t < cnt ? atomicAdd(&hist[bin[k]], 1u) : 0;
+		if (qn > 64 && lane < qn - 64) {
+			const FinRec t = q[64 + lane];
+			q[lane] = t;
 		}
-		__syncthreads();
-		if (wave == 0) { // exclusive scan of the 128 bins, two per lane
-			const uint32_t a = hist[2 * lane], b = hist[2 * lane + 1];
-			uint32_t x = a + b;
-#pragma unroll
-			for (int o = 1; o < 64; o <<= 1) {
-				const uint32_t y = __shfl_up(x, o);
-				if ((int)lane >= o)
-					x += y;
-			}
-			const uint32_t excl = x - a - b;
-			hist[2 * lane] = excl;
-			hist[2 * lane + 1] = excl + a;
+		qn -= cnt;
+	};
+	// Appends e0's record when `done` (the scan of e0 is over).
+	auto push = [&](bool done) {
+		const unsigned long long b = __ballot(done);
+		if (done) {
+			const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+			FinRec t;
+			t.pl = (unsigned long long)(uintptr_t)e0.p | ((unsigned long long)e0.L << 48);
+			t.idx = e0.idx;
+			t.sf = s | (sr.cseen << 8);
+			t.pad = 0;
+			t.url = sr.url;
+			t.host = sr.host;
+			t.hend = sr.hend;
+			t.cip = sr.cip;
+			t.term = sr.term;
+			q[at] = t;
 		}
-		__syncthreads();
-#pragma unroll
-		for (int k = 0; k < kPer; k++) {
-			const uint32_t t = threadIdx.x + k * kFreshThreads;
-#ifdef EBD_EXP_NOSORT
-			if (t < cnt)
-				tev[t] = rec[k];
-#else
-			if (t < cnt)
-				tev[hist[bin[k]] + rank[k]] = rec[k];
-#endif
-		}
-		__syncthreads();
-		// groups of 64 in descending length; a wave takes the next one when it is free
-		// (longest-first greedy: the short groups at the end even out the waves)
+		qn += (uint32_t)__popcll(b);
+	};
+	// Moves on while e0 needs no scan: such events are resolved here.
+	auto resolve = [&]() {
 		for (;;) {
-			uint32_t g = 0;
-			if (lane == 0)
-				g = atomicAdd(&next_group, 1u);
-			g = __builtin_amdgcn_readfirstlane(g);
-			if (g * 64 >= cnt)
+			if (e0.kind == EK_SKIP) {
+				write_none(d, e0.idx);
+			} else if (e0.kind == EK_BAD) {
+				set_error(d, EBD_ERR_BAD_INPUT);
+				write_none(d, e0.idx);
+			} else if (e0.kind == EK_PARSE && e0.L == 0) {
+				write_empty(d, e0.idx);
+			} else {
 				break;
-			const uint32_t t = g * 64 + lane;
-			if (t < cnt)
-				fresh_event(d, T, tev[t], base);
+			}
+			e0 = e1;
+			e1 = lane_ev(d, grab(), re);
+		}
+		w0 = 0;
+		s = di.init;
+		rec_init(di, sr);
+		live = e0.kind == EK_PARSE ? 1u : 0u;
+	};
+	resolve();
+
+	// The window in flight: (tidx, tw) names what W holds for this lane.
+	auto nwin = [](uint32_t L) { return (L + 63) >> 6; };
+	Chunk W[4];
+	uint32_t tidx, tw;
+	auto issue = [&](const uint8_t* p, uint32_t L, uint32_t w) {
+		// member k's window: pieces p + 16 * min(4w + j, last), j = 0..3; this lane loads piece r
+		const uint32_t last = L ? (L - 1) >> 4 : 0;
+		const unsigned long long a = (unsigned long long)(uintptr_t)p;
+		const uint32_t pc = (w << 2) | (last << 16); // window's first chunk | last chunk
+		unsigned long long ak[4];
+		uint32_t pk[4];
+		ak[0] = qbcast64<0>(a), pk[0] = qbcast<0>(pc);
+		ak[1] = qbcast64<1>(a), pk[1] = qbcast<1>(pc);
+		ak[2] = qbcast64<2>(a), pk[2] = qbcast<2>(pc);
+		ak[3] = qbcast64<3>(a), pk[3] = qbcast<3>(pc);
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const uint32_t c = min((pk[k] & 0xffffu) + r, pk[k] >> 16);
+			W[k] = gload16((uintptr_t)(ak[k] + 16ull * c));
+		}
+	};
+	tidx = e0.idx;
+	tw = 0;
+	issue(e0.p, e0.L, 0);
+
+	for (;;) {
+		const bool any_active = __any(e0.kind != EK_NONE);
+		if (qn >= 64 || (!any_active && qn > 0)) {
+			flush();
+			continue;
+		}
+		if (!any_active)
+			break;
+		// is the window in flight the one e0 needs?
+		const bool act = e0.kind == EK_PARSE;
+		const bool valid = act && tidx == e0.idx && tw == w0;
+		Chunk X[4] = {W[0], W[1], W[2], W[3]};
+		// predict and load the next window
+		{
+			const uint8_t* np;
+			uint32_t nL, ni, nw;
+			if (!valid) {
+				np = e0.p, nL = e0.L, ni = e0.idx, nw = w0;
+			} else if (w0 + 1 < nwin(e0.L)) {
+				np = e0.p, nL = e0.L, ni = e0.idx, nw = w0 + 1;
+			} else {
+				np = e1.p, nL = e1.L, ni = e1.idx, nw = 0;
+			}
+			issue(np, nL, nw);
+			tidx = ni;
+			tw = nw;
+		}
+		transpose_quad(X, r);
+		bool done = false;
+		if (valid) {
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				uint32_t sx = s, m = 0;
+				scan_chunk(T, X[k], sx, m);
+				if (live) {
+					const uint32_t c = 4 * w0 + k;
+					if (st_terminal(di, sx)) {
+						sr.term = (c << 8) | s;
+						sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
+						live = 0;
+					} else {
+						chunk_track(di, sr, c, sx, m >= 254);
+						live = 16 * (c + 1) < e0.L ? 1u : 0u;
+					}
+					s = sx;
+				}
+			}
+			w0++;
+			done = !live;
+		}
+		push(done);
+		if (done) {
+			e0 = e1;
+			e1 = lane_ev(d, grab(), re);
+			resolve();
 		}
 	}
 }
@@ -849,6 +919,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 __global__ void k_reps(Dev d) {
 	const unsigned long long nn = d.ctr[CTR_NEW];
 	const uint32_t n_new = (uint32_t)(nn < d.new_cap ? nn : d.new_cap);
+	if (blockIdx.x == 0 && threadIdx.x == 0 && nn)
+		atomicAdd(&d.ctr[CTR_SERVICES], nn);
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_new; k += gridDim.x * blockDim.x) {
 		Slot* s = d.slots + d.new_slots[k];
 		const unsigned long long seq = s->min_seq;
@@ -983,8 +1055,9 @@ static int grid_for(uint64_t items, int block, int cap) {
 }
 
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
-	const uint32_t ntiles = (d.n + kTile - 1) / kTile;
-	const int grid = (int)(ntiles < (uint32_t)cus * 2 ? ntiles : (uint32_t)cus * 2);
+	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
+	const uint64_t groups = ((uint64_t)d.n + kFreshThreads * 4 - 1) / (kFreshThreads * 4);
+	const int grid = (int)(groups < (uint64_t)cus ? groups : (uint64_t)cus);
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
