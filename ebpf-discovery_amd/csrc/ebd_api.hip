@@ -782,25 +782,28 @@ struct HostTab {
 	uint32_t operator[](uint32_t i) const { return t[i]; }
 };
 
-// fresh_finalize's buffer access on the host: bytes outside the buffer read as 0 (the
-// device reads whatever follows; those bytes are masked off either way).
+// Bytes past a buffer as the host emulation sees them.  The device reads whatever follows
+// the buffer; "\r\n" repeated is the most hostile filler (it can complete a request), so
+// the host twin uses it to show that nothing past L leaks into a result.
+struct HostPast {
+	uint32_t operator()(uint32_t k) const { return (k & 1) ? '\n' : '\r'; }
+};
+
+// fresh_finalize's buffer access on the host (bytes past the buffer: HostPast).
 struct HostMem {
 	const uint8_t* p;
-	uint32_t skip, L;
-	Chunk chunk(uint32_t c) const {
-		Chunk ch{};
-		for (uint32_t k = 0; k < 16; k++) {
-			const int pos = (int)(c * 16 + k) - (int)skip;
-			if (pos >= 0 && (uint32_t)pos < L)
-				ch.w[k >> 2] |= (uint32_t)p[pos] << (8 * (k & 3));
-		}
-		return ch;
+	uint32_t L;
+	uint32_t at(uint32_t o) const { return o < L ? p[o] : HostPast{}(o - L); }
+	uint32_t ld4(uint32_t o) const {
+		uint32_t v = 0;
+		for (uint32_t b = 0; b < 4; b++)
+			v |= at(o + b) << (8 * b);
+		return v;
 	}
 	unsigned long long ld8(uint32_t o) const {
 		unsigned long long v = 0;
 		for (uint32_t b = 0; b < 8; b++)
-			if (o + b < L)
-				v |= (unsigned long long)p[o + b] << (8 * b);
+			v |= (unsigned long long)at(o + b) << (8 * b);
 		return v;
 	}
 };
@@ -815,12 +818,12 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 	static Interfaces ifs;
 	fill_ifs(ifs, v4, n4, v6, n6);
 	ScanRec sr;
-	const uint32_t skip = (uint32_t)((uintptr_t)buf & 15u);
-	const uint32_t s = fresh_scan_host(HostTab{t->next}, t->info, buf, skip, len, sr);
+	const uint32_t s = fresh_scan_host(HostTab{t->next}, t->info, buf, len, HostPast{}, sr);
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
-	fresh_finalize(HostTab{t->next}, t->info, sr, s, HostMem{buf, skip, len}, skip, len, pid, flags, fr);
+	const bool post = len > 0 && buf[0] == 'P';
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, post, HostMem{buf, len}, len, pid, flags, fr);
 	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
 		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
 	if (fr.cip) { // what k_agg_fast (cip_classify) does for this event

@@ -133,7 +133,7 @@ GenParser represent(const KeyTrie* t, const AState& a, int variant) {
 
 void build_lds_image(const DfaTable* t, uint8_t* out) {
 	std::memset(out, 0, kLdsTableBytes);
-	for (uint32_t st = 0; st < 256; st++)
+	for (uint32_t st = 0; st < kLdsRows; st++)
 		for (uint32_t b = 0; b < 256; b++)
 			out[st * kLdsRow + lds_col(b)] = t->next[st * 256 + b];
 }
@@ -214,32 +214,36 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 			return gx < gy;
 		return rank(states[x]) < rank(states[y]);
 	});
-	// HV(client) states leave their groups for ids 254 / 255
+	// HV(client) states leave their groups for the two ids after the terminal states, so
+	// that "s >= hvc0" (one compare) tells a client-IP value state
 	std::vector<int> newid(n, -1);
-	int next_id = 0, hvc_seen = 0;
+	int next_id = 0, hvc_seen = 0, hvc_idx[2] = {-1, -1};
 	for (int i = 0; i < n; i++) {
 		const AState& a = states[order[i]];
 		if (a.state == ST_HDR_VAL && a.kt == KT_CLIENT0) {
-			newid[order[i]] = a.host ? 255 : 254;
+			hvc_idx[a.host ? 1 : 0] = order[i];
 			hvc_seen++;
 		} else {
 			newid[order[i]] = next_id++;
 		}
 	}
-	if (hvc_seen != 2 || next_id > 254)
+	if (hvc_seen != 2 || hvc_idx[0] < 0 || hvc_idx[1] < 0 || next_id + 2 > (int)kLdsRows)
 		return -2;
+	const int hvc_base = next_id;
+	newid[hvc_idx[0]] = hvc_base;
+	newid[hvc_idx[1]] = hvc_base + 1;
 
 	std::memset(out, 0, sizeof(*out));
 	DfaInfo& in = out->info;
-	in.nstates = 256;
+	in.nstates = (uint32_t)hvc_base + 2;
 	in.init = (uint32_t)newid[0];
 	in.url_id = in.g2 = in.g3 = in.g4 = in.hvh = in.fin0 = in.fin1 = in.inv = 0xffffffffu;
-	in.hvc0 = 254;
-	in.hvc1 = 255;
+	in.hvc0 = (uint32_t)hvc_base;
+	in.hvc1 = (uint32_t)hvc_base + 1;
 	for (int i = 0; i < n; i++) {
 		const AState& a = states[i];
 		const uint32_t id = (uint32_t)newid[i];
-		if (id >= 254)
+		if (id >= in.hvc0)
 			continue;
 		if (a.state == ST_URL)
 			in.url_id = id;
@@ -253,7 +257,7 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 	uint32_t first[5] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 	for (int i = 0; i < n; i++) {
 		const uint32_t id = (uint32_t)newid[i];
-		if (id >= 254)
+		if (id >= in.hvc0)
 			continue;
 		const int g = group(states[i]);
 		if (id < first[g])

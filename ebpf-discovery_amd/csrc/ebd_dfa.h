@@ -10,9 +10,9 @@
 //   G2 [g2, g3)           header section, Host not seen yet
 //   G3 [g3, g4)           header section, Host seen; HV(host) = hvh
 //   G4 = [g4, g4 + 3)     FINISHED (no host), FINISHED (host), INVALID
-//   254, 255              HV(client) without / with Host seen (hvc0, hvc1): one compare
-//                         (s >= 254) tells "inside a client-IP header value"
-// Rows between the used ids and 254 are unreachable (filled with INVALID).
+//   hvc0 = g4 + 3, hvc1   HV(client) without / with Host seen: one compare (s >= hvc0)
+//                         tells "inside a client-IP header value"; they are the last ids
+// Rows past the used ids are unreachable (filled with INVALID).
 // Phases are monotone: the group of the state never decreases (HV(client) counts as the
 // header group of its world), which lets the kernel find every span from per-chunk
 // crossings and a 16-byte rescan.
@@ -25,8 +25,8 @@ namespace ebd {
 struct DfaInfo {
 	uint32_t nstates;
 	uint32_t url_id, g2, g3, g4;
-	uint32_t hvc0, hvh;            // HV(client, no host) = 254, HV(host) in G3
-	uint32_t hvc1;                 // HV(client, host seen) = 255
+	uint32_t hvc0, hvh;            // HV(client, no host) = g4 + 3, HV(host) in G3
+	uint32_t hvc1;                 // HV(client, host seen) = hvc0 + 1 = nstates - 1
 	uint32_t fin0, fin1, inv;
 	uint32_t init;                 // reset state (METHOD, empty)
 };
@@ -49,7 +49,8 @@ EBD_HD constexpr uint32_t lds_col(uint32_t b) { return ((b & 0x1fu) << 2) | ((b 
 constexpr uint32_t kLdsRow = 256;
 EBD_HD constexpr uint32_t lds_col(uint32_t b) { return b; }
 #endif
-constexpr uint32_t kLdsTableBytes = 256 * kLdsRow;
+constexpr uint32_t kLdsRows = 200; // >= nstates (ebd_build_dfa checks)
+constexpr uint32_t kLdsTableBytes = kLdsRows * kLdsRow;
 void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes
 
 void build_key_trie(KeyTrie* t);

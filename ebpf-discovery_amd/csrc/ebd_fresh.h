@@ -1,19 +1,24 @@
 // ebd_fresh.h — fast path for one event parsed by a fresh parser (Discovery.cpp:141-159
 // handleNewSession), written once for the GPU kernel and its host emulation.
 //
-// The byte scan runs the projected DFA (ebd_dfa.h) over the buffer in 16-byte chunks.
-// Per byte it only does the table step and keeps the chunk's maximum state (a state
-// >= 254 is a client-IP value state).  Along a fresh parse these predicates of the state
-// are monotone (false ... false, true ... true; ebd_dfa.h phase groups):
+// The byte scan runs the projected DFA (ebd_dfa.h) over the buffer in 16-byte chunks,
+// chunk c = bytes [16c, 16c + 16) of the buffer.  The last chunk may run past the buffer;
+// the scan steps over those bytes too, which only changes states at positions >= L, so a
+// terminal position >= L is an unfinished parse and every other tracked position is < L.
+// Per byte the scan only does the table step and keeps the chunk's maximum next state (a
+// state >= hvc0 is a client-IP value state).  Along a fresh parse these predicates of the
+// state are monotone (false ... false, true ... true; ebd_dfa.h phase groups):
 //   URL   s > url_id                        the URL has ended
 //   HOST  Host seen                          the first Host value byte was consumed
 //   HEND  Host seen and s != HV(host)        the Host value has ended
 //   TERM  FINISHED / INVALID                 parse() returns
-// so a tracker that keeps "(next chunk << 8) | state at its start" while its predicate is
-// still false ends up naming the chunk in which the predicate flips.  The client-IP value
-// start (first byte whose next state is >= 254) is tracked the same way with a sticky
-// "seen" bit.  Finalize re-runs the DFA over each named chunk (16 bytes, from registers)
-// and counts the steps before the flip: that count is the exact position.
+// A tracker keeps the last chunk whose start state still fails its predicate, so it ends
+// up naming the chunk in which the predicate flips, together with the states at the
+// starts of that chunk's four 4-byte quarters.  The client-IP value start (first byte
+// whose next state is >= hvc0) is tracked the same way, with the running maxima after 4, 8
+// and 12 steps, until a chunk has seen such a state.  Finalize picks the quarter in which
+// the predicate flips from those states and re-runs the DFA over its 4 bytes: the steps
+// before the flip give the exact position.
 #pragma once
 
 #include "../../include/ebpf_discovery_amd.h"
@@ -24,9 +29,16 @@ namespace ebd {
 
 constexpr uint32_t kNone = 0xffffffffu;
 
+// The chunk in which a predicate flips, and the states at the starts of its quarters
+// (qs = s0 | s4 << 8 | s8 << 16 | s12 << 24).
+struct Trk {
+	uint32_t c, qs;
+};
+
 struct ScanRec {
-	uint32_t url, host, hend, cip, term; // (chunk << 8) | state at the chunk's start
-	uint32_t cseen;                      // a client-IP value byte was seen
+	Trk url, host, hend, cip, term; // term: the last chunk scanned
+	uint32_t cqm;                   // cip chunk: running max next state after 4, 8, 12 steps (bytes 0..2)
+	uint32_t cseen;                 // a client-IP value state was reached (the cip tracker is frozen)
 };
 
 enum { RS_URL, RS_HOST, RS_HEND, RS_TERM, RS_CIP };
@@ -47,129 +59,153 @@ EBD_HD bool st_pred(const DfaInfo& di, uint32_t s) {
 }
 
 EBD_HD void rec_init(const DfaInfo& di, ScanRec& r) {
-	r.url = r.host = r.hend = r.cip = r.term = di.init;
+	const Trk t{0, di.init * 0x01010101u};
+	r.url = r.host = r.hend = r.cip = r.term = t;
+	r.cqm = 0;
 	r.cseen = 0;
 }
 
-// After chunk c (ended in s1; hit = some byte's next state was >= 254), not terminal.
-EBD_HD void chunk_track(const DfaInfo& di, ScanRec& r, uint32_t c, uint32_t s1, bool hit) {
-	const uint32_t nxt = ((c + 1) << 8) | s1;
-	r.url = st_pred<RS_URL>(di, s1) ? r.url : nxt;
-	r.host = st_pred<RS_HOST>(di, s1) ? r.host : nxt;
-	r.hend = st_pred<RS_HEND>(di, s1) ? r.hend : nxt;
-	r.cseen |= hit ? 1u : 0u;
-	r.cip = r.cseen ? r.cip : nxt;
+// After chunk c: s0 = its start state, qs = its quarter-start states, qm = running maxima
+// after 4/8/12 steps, m = the chunk's maximum next state.
+EBD_HD void chunk_update(const DfaInfo& di, ScanRec& r, uint32_t c, uint32_t s0, uint32_t qs, uint32_t qm, uint32_t m) {
+	const Trk t{c, qs};
+	r.url = st_pred<RS_URL>(di, s0) ? r.url : t;
+	r.host = st_pred<RS_HOST>(di, s0) ? r.host : t;
+	r.hend = st_pred<RS_HEND>(di, s0) ? r.hend : t;
+	const bool open = r.cseen == 0;
+	r.cip = open ? t : r.cip;
+	r.cqm = open ? qm : r.cqm;
+	r.cseen |= m >= di.hvc0 ? 1u : 0u;
+	r.term = t;
 }
 
-// Host emulation of the device scan: identical chunking (skip = buffer address mod 16).
-template <typename Tab>
-inline uint32_t fresh_scan_host(const Tab& T, const DfaInfo& di, const uint8_t* p, uint32_t skip, uint32_t L, ScanRec& r) {
+// Byte k of a packed word.
+EBD_HD uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xffu; }
+
+// Quarter of the tracker's chunk in which W's predicate flips (3 when no quarter start
+// after the first satisfies it).
+template <int W>
+EBD_HD uint32_t flip_quarter(const DfaInfo& di, const Trk& t, uint32_t cqm) {
+	if (W == RS_CIP)
+		return byte_of(cqm, 0) >= di.hvc0 ? 0u : byte_of(cqm, 1) >= di.hvc0 ? 1u : byte_of(cqm, 2) >= di.hvc0 ? 2u : 3u;
+	return st_pred<W>(di, byte_of(t.qs, 1)) ? 0u : st_pred<W>(di, byte_of(t.qs, 2)) ? 1u : st_pred<W>(di, byte_of(t.qs, 3)) ? 2u : 3u;
+}
+
+// Steps over the 4 bytes of `w` from state s before W's predicate holds (RS_CIP: before the
+// first step whose next state is >= hvc0); 4 if it never does.
+template <int W, typename Tab>
+EBD_HD uint32_t rescan4(const Tab& T, const DfaInfo& di, uint32_t s, uint32_t w) {
+	uint32_t before = 0, hit = 0;
+#pragma unroll
+	for (int k = 0; k < 4; k++) {
+		s = T[(s << 8) | byte_of(w, (uint32_t)k)];
+		const bool p = W == RS_CIP ? s >= di.hvc0 : st_pred<W>(di, s);
+		hit |= p ? 1u : 0u;
+		before += hit ? 0u : 1u;
+	}
+	return before;
+}
+
+// Position (in the buffer) of the first byte after which W's predicate holds.
+template <int W, typename Tab>
+EBD_HD uint32_t flip_pos(const Tab& T, const DfaInfo& di, const Trk& t, uint32_t q, uint32_t w4) {
+	return 16 * t.c + 4 * q + rescan4<W>(T, di, byte_of(t.qs, q), w4);
+}
+
+// Host emulation of the device scan: the same chunks, and bytes past the buffer taken from
+// `past(k)` (the device reads whatever follows the buffer).
+template <typename Tab, typename Past>
+inline uint32_t fresh_scan_host(const Tab& T, const DfaInfo& di, const uint8_t* p, uint32_t L, Past past, ScanRec& r) {
 	rec_init(di, r);
 	uint32_t s = di.init;
-	const uint32_t nch = (skip + L + 15) / 16;
+	const uint32_t nch = (L + 15) / 16;
 	for (uint32_t c = 0; c < nch; c++) {
 		const uint32_t s0 = s;
-		uint32_t m = 0;
+		uint32_t m = 0, qs = s0, qm = 0;
 		for (uint32_t k = 0; k < 16; k++) {
-			const int pos = (int)(c * 16 + k) - (int)skip;
-			if (pos < 0 || (uint32_t)pos >= L)
-				continue;
-			s = T[(s << 8) | p[pos]];
+			const uint32_t pos = c * 16 + k;
+			s = T[(s << 8) | (pos < L ? p[pos] : past(pos - L))];
 			m = m > s ? m : s;
+			if (k == 3 || k == 7 || k == 11) {
+				qs |= s << (8 * ((k + 1) / 4));
+				qm |= m << (8 * (k / 4));
+			}
 		}
-		if (st_terminal(di, s)) {
-			r.term = (c << 8) | s0;
-			r.cseen |= m >= 254 ? 1u : 0u; // r.cip already names this chunk
+		chunk_update(di, r, c, s0, qs, qm, m);
+		if (st_terminal(di, s))
 			break;
-		}
-		chunk_track(di, r, c, s, m >= 254);
 	}
 	return s;
-}
-
-// One 16-byte chunk as 4 little-endian words.
-struct Chunk {
-	uint32_t w[4];
-};
-
-EBD_HD uint32_t chunk_byte(const Chunk& ch, int k) { return (ch.w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
-
-// Position (relative to the buffer) of the first byte in the recorded chunk whose next
-// state satisfies W's predicate (RS_CIP: is a client-IP value state).
-template <int W, typename Tab>
-EBD_HD uint32_t rescan(const Tab& T, const DfaInfo& di, uint32_t rec, const Chunk& ch, uint32_t skip, uint32_t L) {
-	const uint32_t c = rec >> 8;
-	uint32_t s = rec & 0xffu;
-	uint32_t before = 0, seen = 0;
-	for (int k = 0; k < 16; k++) {
-		const int pos = (int)(c * 16 + k) - (int)skip;
-		const bool valid = pos >= 0 && (uint32_t)pos < L;
-		const uint32_t sn = valid ? (uint32_t)T[(s << 8) | chunk_byte(ch, k)] : s;
-		if (W == RS_CIP) {
-			seen |= (valid && sn >= 254) ? 1u : 0u;
-			before += seen ? 0u : 1u;
-		} else {
-			before += st_pred<W>(di, sn) ? 0u : 1u;
-		}
-		s = sn;
-	}
-	return c * 16 + before - skip;
 }
 
 struct FreshResult {
 	ebd_event_result r;
 	Hash128 key;
-	bool cip; // client class pending: decided from the client-IP token (k_agg_fast, cip_classify)
+	bool cip;  // client class pending: decided from the client-IP token (k_agg_fast, cip_classify)
+	bool keyed; // FINISHED: the key over (pid, host + url) is still to be computed
 };
 
-// Turns a scan into the per-event result and the service key (the client class is decided
-// later by k_agg_fast: the client-IP front token if there is one, else the source address).  Mem supplies
-// chunk(c) (the buffer's c-th aligned 16-byte chunk) and ld8(off) (8 bytes at buffer
-// offset off, any alignment; bytes past a span are masked by the caller).
-// pid / flags come from the DiscoveryEvent (Discovery.cpp:136, 157).
-template <typename Tab, typename Mem>
-EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, const Mem& mem, uint32_t skip,
-		uint32_t L, uint32_t pid, uint8_t flags, FreshResult& out) {
+// The flip quarter of every tracker and the 4 buffer bytes a rescan of it needs.
+struct FinLoads {
+	uint32_t qt, qu, qh, qe, qc;
+	uint32_t wt, wu, wh, we, wc;
+};
+
+// Mem supplies ld4(off) (4 bytes at buffer offset off, any alignment) and ld8(off); every
+// load is issued before any is used.
+template <typename Mem>
+EBD_HD void fresh_loads(const DfaInfo& di, const ScanRec& sr, const Mem& mem, FinLoads& f) {
+	f.qt = flip_quarter<RS_TERM>(di, sr.term, 0);
+	f.qu = flip_quarter<RS_URL>(di, sr.url, 0);
+	f.qh = flip_quarter<RS_HOST>(di, sr.host, 0);
+	f.qe = flip_quarter<RS_HEND>(di, sr.hend, 0);
+	f.qc = flip_quarter<RS_CIP>(di, sr.cip, sr.cqm);
+	f.wt = mem.ld4(16 * sr.term.c + 4 * f.qt);
+	f.wu = mem.ld4(16 * sr.url.c + 4 * f.qu);
+	f.wh = mem.ld4(16 * sr.host.c + 4 * f.qh);
+	f.we = mem.ld4(16 * sr.hend.c + 4 * f.qe);
+	f.wc = mem.ld4(16 * sr.cip.c + 4 * f.qc);
+}
+
+// Turns a scan into the per-event result (the client class is decided later by k_agg_fast:
+// the client-IP front token if there is one, else the source address).  `post`: the
+// buffer's first byte is 'P'.  flags come from the DiscoveryEvent (Discovery.cpp:136, 157).
+// A FINISHED result leaves out.keyed set: the key is endpoint_key over its spans.
+template <typename Tab>
+EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, bool post, const FinLoads& f,
+		uint32_t L, uint8_t flags, FreshResult& out) {
 	ebd_event_result& r = out.r;
 	r.info = 0;
 	r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
 	out.key.lo = out.key.hi = 0;
 	out.cip = false;
-	if (!st_terminal(di, s_final)) {
-		r.status = EBD_STATUS_UNFINISHED;
-		r.consumed = (uint16_t)L;
-		return;
-	}
-	const bool fin = s_final != di.inv, host = s_final == di.fin1, cip = fin && sr.cseen;
-	// every chunk finalize may need, loaded unconditionally before any is used
-	const Chunk wt = mem.chunk(sr.term >> 8), wu = mem.chunk(sr.url >> 8), wh = mem.chunk(sr.host >> 8),
-	            we = mem.chunk(sr.hend >> 8), wc = mem.chunk(sr.cip >> 8);
-	const uint32_t consumed = rescan<RS_TERM>(T, di, sr.term, wt, skip, L) + 1;
-	if (consumed > L) {
-		// the device scans whole chunks: a terminal state reached only past the buffer's
-		// last byte is an unfinished parse (HttpRequestParser.cpp:85-106 stops at L)
+	out.keyed = false;
+	const uint32_t consumed = flip_pos<RS_TERM>(T, di, sr.term, f.qt, f.wt) + 1;
+	if (!st_terminal(di, s_final) || consumed > L) {
+		// not terminal, or terminal only past the buffer's last byte: parse() stops at L
+		// (HttpRequestParser.cpp:85-106), unfinished
 		r.status = EBD_STATUS_UNFINISHED;
 		r.consumed = (uint16_t)L;
 		return;
 	}
 	r.consumed = (uint16_t)consumed;
+	const bool fin = s_final != di.inv, host = s_final == di.fin1, cip = fin && sr.cseen;
 	if (!fin) {
 		r.status = EBD_STATUS_INVALID;
 		return;
 	}
 	r.status = EBD_STATUS_FINISHED;
-	const bool post = (mem.ld8(0) & 0xff) == 'P';
 	const uint32_t url_start = post ? 5 : 4;
-	const uint32_t url_len = rescan<RS_URL>(T, di, sr.url, wu, skip, L) - url_start;
+	const uint32_t url_len = flip_pos<RS_URL>(T, di, sr.url, f.qu, f.wu) - url_start;
 	uint32_t host_start = 0, host_len = 0;
 	if (host) {
-		host_start = rescan<RS_HOST>(T, di, sr.host, wh, skip, L);
-		host_len = rescan<RS_HEND>(T, di, sr.hend, we, skip, L) - host_start;
+		host_start = flip_pos<RS_HOST>(T, di, sr.host, f.qh, f.wh);
+		host_len = flip_pos<RS_HEND>(T, di, sr.hend, f.qe, f.we) - host_start;
 	}
 	uint8_t info = (uint8_t)((post ? EBD_INFO_POST : 0) | ((flags & 16) ? EBD_INFO_HTTPS : 0));
 	if (cip) {
 		// raw value start of the first client-IP header; token and class: k_agg_fast
-		r.u.span.cip_off = (uint16_t)rescan<RS_CIP>(T, di, sr.cip, wc, skip, L);
+		r.u.span.cip_off = (uint16_t)flip_pos<RS_CIP>(T, di, sr.cip, f.qc, f.wc);
 		info |= EBD_INFO_CIP;
 		out.cip = true;
 	} // else the class comes from the source address (k_agg_fast reads the event)
@@ -178,12 +214,26 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	r.u.span.url_len = (uint16_t)url_len;
 	r.u.span.host_off = (uint16_t)host_start;
 	r.u.span.host_len = (uint16_t)host_len;
+	out.keyed = true;
+}
+
+// The whole finalize for one event (the host twin; the device interleaves the steps of
+// several events).  pid: the DiscoveryEvent's (Discovery.cpp:136, 157).
+template <typename Tab, typename Mem>
+EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, bool post, const Mem& mem,
+		uint32_t L, uint32_t pid, uint8_t flags, FreshResult& out) {
+	FinLoads f;
+	fresh_loads(di, sr, mem, f);
+	fresh_spans(T, di, sr, s_final, post, f, L, flags, out);
+	if (out.keyed) {
+		const auto& sp = out.r.u.span;
 #ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
-	out.key.lo = host_len * 31 + url_len;
-	out.key.hi = 1;
+		out.key.lo = sp.host_len * 31 + sp.url_len;
+		out.key.hi = 1;
 #else
-	out.key = endpoint_key(pid, host_start, host_len, url_start, url_len, [&](uint32_t o) { return mem.ld8(o); });
+		out.key = endpoint_key(pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
 #endif
+	}
 }
 
 // Client-IP pass for one event (HttpRequestParser.cpp:370-407 parseClientIPValue on the

@@ -201,9 +201,15 @@ struct LdsTable {
 	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i >> 8) * kLdsRow + lds_col(i & 0xffu)]; }
 };
 
+// One 16-byte chunk as 4 little-endian words.
+struct Chunk {
+	uint32_t w[4];
+};
+
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_a1 __attribute__((aligned(1)));
 typedef unsigned long long u64a1 __attribute__((aligned(1)));
+typedef unsigned int u32a1 __attribute__((aligned(1)));
 // 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
 __device__ __forceinline__ Chunk gload16(uintptr_t a) {
 	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
@@ -219,19 +225,24 @@ __device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
 	return *(const __attribute__((address_space(1))) u64a1*)a;
 }
 
-// Buffer access for fresh_finalize on the device: chunk c = bytes [16c, 16c + 16) of the
-// buffer (clamped to its last chunk).  The payload stays readable EBD_PAYLOAD_PAD bytes past
-// each buffer (ebd_api.hip pads it).
+// Buffer access for fresh_finalize on the device: 4 and 8 bytes at any buffer offset.  Every
+// offset it reads lies within the buffer's last 16-byte chunk, and the payload stays
+// readable EBD_PAYLOAD_PAD bytes past each buffer (ebd_api.hip pads it).
 struct DevMem {
 	const uint8_t* p;
-	uint32_t last; // last chunk index of the buffer
-	__device__ __forceinline__ Chunk chunk(uint32_t c) const { return gload16((uintptr_t)p + 16 * (uintptr_t)min(c, last)); }
+	__device__ __forceinline__ uint32_t ld4(uint32_t o) const { return *(const __attribute__((address_space(1))) u32a1*)(p + o); }
 	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
 };
 
 constexpr int kFreshThreads = 1024;
 constexpr int kFreshWaves = kFreshThreads / 64;
-constexpr uint32_t kQueue = 128; // finalize records per wave (<= 63 waiting + 64 pushed)
+constexpr int kScanWaves = 12;   // waves [0, kScanWaves) scan; the others finalize
+constexpr uint32_t kRing = 512;  // finalize records in flight per workgroup (power of two)
+#ifndef EBD_FINPER
+#define EBD_FINPER 0
+#endif
+// records per finalize lane at a time (0: one record, finalized only by the lanes that hold one)
+constexpr int kFinPer = EBD_FINPER > 0 ? EBD_FINPER : 1;
 
 // A chunk word with every byte b replaced by lds_col(b) (5 VALU per 4 bytes).
 __device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
@@ -251,17 +262,33 @@ __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
 #endif
 }
 
-// 16 DFA steps over one chunk; m collects the maximum next state.
-__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m) {
+// 16 DFA steps over one chunk: s advances, m = the maximum next state, qs = the states at
+// the quarter starts (s0 | s4 << 8 | s8 << 16 | s12 << 24), qm = running maxima after 4, 8
+// and 12 steps (ebd_fresh.h chunk_update).
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t& qs,
+		uint32_t& qm) {
+	qs = s;
 #ifdef EBD_EXP_MEMONLY // experiment: the loads without the DFA (results are wrong)
-	m ^= w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
+	m = w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
+	qm = 0;
 	return;
 #endif
 	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
+	m = 0;
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
 		s = T[tab_index(s, wc[k >> 2], k)];
 		m = max(m, s); // pairs fold into v_max3
+		if (k == 3) {
+			qs |= s << 8;
+			qm = m;
+		} else if (k == 7) {
+			qs |= s << 16;
+			qm |= m << 8;
+		} else if (k == 11) {
+			qs |= s << 24;
+			qm |= m << 16;
+		}
 	}
 }
 
@@ -307,6 +334,8 @@ struct LaneEv {
 	uint32_t idx;
 	uint32_t L;       // buffer length (0 unless EK_PARSE)
 	uint32_t kind;
+	uint32_t pf;      // pid (the DiscoveryEvent's, Discovery.cpp:136, 157)
+	uint32_t flags;
 	const uint8_t* p; // buffer (a harmless valid address unless EK_PARSE)
 };
 
@@ -316,10 +345,14 @@ __device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end
 	if (i >= end) {
 		e.kind = EK_NONE;
 		e.L = 0;
+		e.pf = e.flags = 0;
 		e.p = d.payload;
 		return e;
 	}
-	const uint32_t flags = ((const uint8_t*)(d.ev + i))[32];
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint32_t flags = evb[32];
+	e.pf = *(const uint32_t*)evb;
+	e.flags = flags;
 #ifdef EBD_EXP_L2ONLY // experiment: every event parses one of the first 4096 buffers (L2-resident)
 	const uint32_t L = d.len[i & 4095];
 	const uint64_t off = d.off[i & 4095];
@@ -333,54 +366,19 @@ __device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end
 	return e;
 }
 
-// A finished scan waiting for fresh_finalize (40 B).
+// A finished scan waiting for fresh_finalize (64 B).
 struct FinRec {
 	unsigned long long pl; // buffer address (bits 0..47) | L << 48
-	uint32_t idx;
-	uint32_t sf;           // final state | cseen << 8
-	uint32_t url, host, hend, cip, term;
-	uint32_t pad;
+	uint32_t idx, pid;
+	uint32_t sf;  // final state | flags << 8 | cseen << 16 | post << 17
+	uint32_t cqm;
+	uint32_t c01; // url.c | host.c << 16
+	uint32_t c23; // hend.c | cip.c << 16
+	uint32_t c4;  // term.c
+	uint32_t qs[5];
+	uint32_t pad[2];
 };
-static_assert(sizeof(FinRec) == 40, "finalize record is 40 bytes");
-
-__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q) {
-	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
-	const uint32_t L = (uint32_t)(q.pl >> 48);
-	const uint32_t i = q.idx;
-#ifdef EBD_EXP_FINWRITE // experiment: finalize writes a placeholder result (results are wrong)
-	{
-		ebd_event_result r;
-		r.consumed = (uint16_t)L;
-		r.status = EBD_STATUS_INVALID;
-		r.info = (uint8_t)q.sf;
-		r.u.session.index = q.url ^ q.host ^ q.hend ^ q.cip ^ q.term;
-		r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
-		d.res[i] = r;
-		return;
-	}
-#endif
-	const uint8_t* evb = (const uint8_t*)(d.ev + i);
-	const uint8_t flags = evb[32];
-	const uint32_t pid = *(const uint32_t*)evb;
-	ScanRec sr;
-	sr.url = q.url;
-	sr.host = q.host;
-	sr.hend = q.hend;
-	sr.cip = q.cip;
-	sr.term = q.term;
-	sr.cseen = (q.sf >> 8) & 1u;
-	FreshResult fr;
-	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, DevMem{p, L ? (L - 1) / 16 : 0}, 0, L, pid, flags, fr);
-	if (fr.r.status == EBD_STATUS_FINISHED) {
-		d.keys[i] = fr.key;
-	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
-		// the session may be saved (Discovery.cpp:148-150): sequential path
-		const EventRec& ev = d.ev[i];
-		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
-	}
-	d.res[i] = fr.r;
-}
+static_assert(sizeof(FinRec) == 64, "finalize record is 64 bytes");
 
 __device__ __forceinline__ void write_none(const Dev& d, uint32_t i) {
 	ebd_event_result r;
@@ -406,64 +404,242 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
 }
 
+// fresh_finalize for N records per lane, its steps interleaved so that the records' memory
+// round trips overlap: the quarter bytes of every record, then spans, then the endpoint
+// pieces of every record, 64 bytes of each per round trip.  have[n]: record n is real.
+template <int N>
+__device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, const FinRec (&q)[N], const bool (&have)[N]) {
+	const DfaInfo& di = d.di;
+	ScanRec sr[N];
+	FinLoads f[N];
+	const uint8_t* p[N];
+	uint32_t L[N];
+#pragma unroll
+	for (int n = 0; n < N; n++) {
+		p[n] = have[n] ? (const uint8_t*)(uintptr_t)(q[n].pl & 0xffffffffffffull) : d.payload;
+		L[n] = have[n] ? (uint32_t)(q[n].pl >> 48) : 0;
+		sr[n].url = Trk{q[n].c01 & 0xffffu, q[n].qs[0]};
+		sr[n].host = Trk{q[n].c01 >> 16, q[n].qs[1]};
+		sr[n].hend = Trk{q[n].c23 & 0xffffu, q[n].qs[2]};
+		sr[n].cip = Trk{q[n].c23 >> 16, q[n].qs[3]};
+		sr[n].term = Trk{q[n].c4, q[n].qs[4]};
+		sr[n].cqm = q[n].cqm;
+		sr[n].cseen = (q[n].sf >> 16) & 1u;
+		if (!have[n])
+			rec_init(di, sr[n]); // loads at offset 0 of a valid address
+		fresh_loads(di, sr[n], DevMem{p[n]}, f[n]);
+	}
+	FreshResult fr[N];
+#pragma unroll
+	for (int n = 0; n < N; n++)
+		fresh_spans(LdsTable{T}, di, sr[n], q[n].sf & 0xffu, ((q[n].sf >> 17) & 1u) != 0, f[n], L[n], (uint8_t)(q[n].sf >> 8), fr[n]);
+	// keys (ebd_spec.h endpoint_key, groups of 8 pieces, all records' loads issued together)
+	constexpr uint32_t kGroup = 8;
+	KeyHasher kh[N];
+	uint32_t hs[N], hl[N], us[N], ul[N], en[N], nmax = 0;
+#pragma unroll
+	for (int n = 0; n < N; n++) {
+		const bool k = have[n] && fr[n].keyed;
+		hs[n] = k ? fr[n].r.u.span.host_off : 0;
+		hl[n] = k ? fr[n].r.u.span.host_len : 0;
+		us[n] = k ? fr[n].r.u.span.url_off : 0;
+		ul[n] = k ? fr[n].r.u.span.url_len : 0;
+		en[n] = hl[n] + ul[n];
+		nmax = max(nmax, en[n]);
+		kh[n].init(q[n].pid);
+	}
+	for (uint32_t g = 0; g < nmax; g += 8 * kGroup) {
+		uint64_t A[N][kGroup], B[N][kGroup];
+#pragma unroll
+		for (int n = 0; n < N; n++)
+#pragma unroll
+			for (uint32_t k = 0; k < kGroup; k++) {
+				const uint32_t oo = g + 8 * k;
+				A[n][k] = gload8u(p[n] + hs[n] + (oo < hl[n] ? oo : 0));
+				B[n][k] = gload8u(p[n] + us[n] + ((oo > hl[n] && oo - hl[n] < ul[n]) ? oo - hl[n] : 0));
+			}
+#pragma unroll
+		for (int n = 0; n < N; n++)
+#pragma unroll
+			for (uint32_t k = 0; k < kGroup; k += 2) {
+				const uint32_t oo = g + 8 * k;
+				if (oo < en[n])
+					kh[n].block(endpoint_piece(hl[n], en[n], oo, A[n][k], B[n][k]),
+							endpoint_piece(hl[n], en[n], oo + 8, A[n][k + 1], B[n][k + 1]));
+			}
+	}
+#pragma unroll
+	for (int n = 0; n < N; n++) {
+		if (!have[n])
+			continue;
+		const uint32_t i = q[n].idx;
+		if (fr[n].r.status == EBD_STATUS_FINISHED) {
+#ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
+			d.keys[i] = Hash128{en[n], 1};
+#else
+			d.keys[i] = kh[n].finish_blocks(en[n]);
+#endif
+		} else if (fr[n].r.status == EBD_STATUS_UNFINISHED) {
+			// the session may be saved (Discovery.cpp:148-150): sequential path
+			const EventRec& ev = d.ev[i];
+			atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+			sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
+		}
+		d.res[i] = fr[n].r;
+	}
+}
+
+// fresh_finalize for one record (ebd_fresh.h), run only by the lanes that hold one.
+__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q) {
+	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
+	const uint32_t L = (uint32_t)(q.pl >> 48);
+	const uint32_t i = q.idx;
+	ScanRec sr;
+	sr.url = Trk{q.c01 & 0xffffu, q.qs[0]};
+	sr.host = Trk{q.c01 >> 16, q.qs[1]};
+	sr.hend = Trk{q.c23 & 0xffffu, q.qs[2]};
+	sr.cip = Trk{q.c23 >> 16, q.qs[3]};
+	sr.term = Trk{q.c4, q.qs[4]};
+	sr.cqm = q.cqm;
+	sr.cseen = (q.sf >> 16) & 1u;
+	FreshResult fr;
+	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, DevMem{p}, L, q.pid, (uint8_t)(q.sf >> 8), fr);
+	if (fr.r.status == EBD_STATUS_FINISHED) {
+		d.keys[i] = fr.key;
+	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+		// the session may be saved (Discovery.cpp:148-150): sequential path
+		const EventRec& ev = d.ev[i];
+		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
+	}
+	d.res[i] = fr.r;
+}
+
+__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
+	__hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Workgroup state shared by the scan and finalize waves.
+struct FreshShared {
+	FinRec ring[kRing];
+	uint32_t ready[kRing]; // position + 1 once ring[pos % kRing] is written
+	uint32_t freed[kRing]; // position + 1 once ring[pos % kRing] is finalized
+	uint32_t next_ev;      // next event of the workgroup's range
+	uint32_t tail;         // positions handed out to scan lanes
+	uint32_t claim;        // positions handed out to finalize waves
+	uint32_t scan_done;    // scan waves that finished
+};
+
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 	// static LDS: the table sits at LDS address 0, so a step's index is its address
 	__shared__ __attribute__((aligned(16))) uint8_t T[kLdsTableBytes];
-	__shared__ FinRec fq[kFreshWaves][kQueue];
-	__shared__ uint32_t next_ev;
+	__shared__ FreshShared sh;
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 3;
 	// this workgroup's contiguous share of the batch
 	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
 	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per);
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kFreshThreads * 16u)
 		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
-	if (threadIdx.x == 0)
-		next_ev = rb + kFreshThreads * 2;
+	for (uint32_t k = threadIdx.x; k < kRing; k += kFreshThreads)
+		sh.ready[k] = sh.freed[k] = 0;
+	if (threadIdx.x == 0) {
+		sh.next_ev = rb + kScanWaves * 64 * 2;
+		sh.tail = sh.claim = sh.scan_done = 0;
+	}
 	__syncthreads();
 	const DfaInfo& di = d.di;
-	FinRec* const q = fq[wave];
-	uint32_t qn = 0; // records waiting in q (wave-uniform)
 
-	auto grab = [&]() -> uint32_t { return atomicAdd(&next_ev, 1u); };
+	if (wave >= kScanWaves) {
+		// ---- finalize waves: kFinPer x 64 records at a time, in position order ----
+		for (;;) {
+			uint32_t c = 0;
+			if (lane == 0)
+				c = atomicAdd(&sh.claim, 64u * kFinPer);
+			c = __builtin_amdgcn_readfirstlane(c);
+			FinRec q[kFinPer];
+			bool have[kFinPer];
+#pragma unroll
+			for (int j = 0; j < kFinPer; j++) {
+				const uint32_t pos = c + 64 * j + lane, slot = pos & (kRing - 1);
+				have[j] = false;
+				for (;;) {
+					if (lds_load_acq(&sh.ready[slot]) == pos + 1) {
+						have[j] = true;
+						break;
+					}
+					if (lds_load_acq(&sh.scan_done) == (uint32_t)kScanWaves && pos >= lds_load_acq(&sh.tail))
+						break;
+					__builtin_amdgcn_s_sleep(2);
+				}
+				if (have[j]) {
+					q[j] = sh.ring[slot];
+					lds_store_rel(&sh.freed[slot], pos + 1);
+				} else {
+					q[j] = FinRec{};
+				}
+			}
+			if (!__any(have[0]))
+				break;
+#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
+#if EBD_FINPER == 0
+			if (have[0])
+				finalize_rec(d, T, q[0]);
+#else
+			finalize_recs<kFinPer>(d, T, q, have);
+#endif
+#endif
+		}
+		return;
+	}
+
+	// ---- scan waves ----
+	const uint32_t sl = wave * 64 + lane; // scan lane
+	constexpr uint32_t kScanLanes = kScanWaves * 64;
+	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
 	// the lane's current event (e0) and the next one (e1, whose record arrives early)
-	LaneEv e0 = lane_ev(d, rb + threadIdx.x, re);
-	LaneEv e1 = lane_ev(d, rb + kFreshThreads + threadIdx.x, re);
+	LaneEv e0 = lane_ev(d, rb + sl, re);
+	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
 	uint32_t w0 = 0; // e0's window to scan next
-	uint32_t s = di.init, live = 0;
+	uint32_t s = di.init, live = 0, post = 0;
 	ScanRec sr;
 	rec_init(di, sr);
 
-	// Finalize the first min(qn, 64) queued records (one per lane) and move the rest down.
-	auto flush = [&]() {
-		const uint32_t cnt = qn < 64 ? qn : 64;
-#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
-		if (lane < cnt)
-			finalize_rec(d, T, q[lane]);
-#endif
-		if (qn > 64 && lane < qn - 64) {
-			const FinRec t = q[64 + lane];
-			q[lane] = t;
-		}
-		qn -= cnt;
-	};
-	// Appends e0's record when `done` (the scan of e0 is over).
+	// Hands e0's scan record to the finalize waves when `done`.
 	auto push = [&](bool done) {
 		const unsigned long long b = __ballot(done);
+		if (b == 0)
+			return;
+		uint32_t base = 0;
+		if (lane == 0)
+			base = atomicAdd(&sh.tail, (uint32_t)__popcll(b));
+		base = __builtin_amdgcn_readfirstlane(base);
 		if (done) {
-			const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+			const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+			const uint32_t slot = pos & (kRing - 1);
+			if (pos >= kRing) // the slot's previous record must have been taken
+				while (lds_load_acq(&sh.freed[slot]) != pos - kRing + 1)
+					__builtin_amdgcn_s_sleep(1);
 			FinRec t;
 			t.pl = (unsigned long long)(uintptr_t)e0.p | ((unsigned long long)e0.L << 48);
 			t.idx = e0.idx;
-			t.sf = s | (sr.cseen << 8);
-			t.pad = 0;
-			t.url = sr.url;
-			t.host = sr.host;
-			t.hend = sr.hend;
-			t.cip = sr.cip;
-			t.term = sr.term;
-			q[at] = t;
+			t.pid = e0.pf;
+			t.sf = s | (e0.flags << 8) | (sr.cseen << 16) | (post << 17);
+			t.cqm = sr.cqm;
+			t.c01 = sr.url.c | (sr.host.c << 16);
+			t.c23 = sr.hend.c | (sr.cip.c << 16);
+			t.c4 = sr.term.c;
+			t.qs[0] = sr.url.qs;
+			t.qs[1] = sr.host.qs;
+			t.qs[2] = sr.hend.qs;
+			t.qs[3] = sr.cip.qs;
+			t.qs[4] = sr.term.qs;
+			t.pad[0] = t.pad[1] = 0;
+			sh.ring[slot] = t;
+			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
-		qn += (uint32_t)__popcll(b);
 	};
 	// Moves on while e0 needs no scan: such events are resolved here.
 	auto resolve = [&]() {
@@ -483,6 +659,7 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		}
 		w0 = 0;
 		s = di.init;
+		post = 0;
 		rec_init(di, sr);
 		live = e0.kind == EK_PARSE ? 1u : 0u;
 	};
@@ -513,17 +690,9 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 	tw = 0;
 	issue(e0.p, e0.L, 0);
 
-	for (;;) {
-		const bool any_active = __any(e0.kind != EK_NONE);
-		if (qn >= 64 || (!any_active && qn > 0)) {
-			flush();
-			continue;
-		}
-		if (!any_active)
-			break;
+	while (__any(e0.kind != EK_NONE)) {
 		// is the window in flight the one e0 needs?
-		const bool act = e0.kind == EK_PARSE;
-		const bool valid = act && tidx == e0.idx && tw == w0;
+		const bool valid = e0.kind == EK_PARSE && tidx == e0.idx && tw == w0;
 		Chunk X[4] = {W[0], W[1], W[2], W[3]};
 		// predict and load the next window
 		{
@@ -543,20 +712,16 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		transpose_quad(X, r);
 		bool done = false;
 		if (valid) {
+			if (w0 == 0)
+				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				uint32_t sx = s, m = 0;
-				scan_chunk(T, X[k], sx, m);
+				uint32_t sx = s, m, qs, qm;
+				scan_chunk(T, X[k], sx, m, qs, qm);
 				if (live) {
 					const uint32_t c = 4 * w0 + k;
-					if (st_terminal(di, sx)) {
-						sr.term = (c << 8) | s;
-						sr.cseen |= m >= 254 ? 1u : 0u; // sr.cip already names this chunk
-						live = 0;
-					} else {
-						chunk_track(di, sr, c, sx, m >= 254);
-						live = 16 * (c + 1) < e0.L ? 1u : 0u;
-					}
+					chunk_update(di, sr, c, s, qs, qm, m);
+					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
 					s = sx;
 				}
 			}
@@ -570,6 +735,8 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 			resolve();
 		}
 	}
+	if (lane == 0)
+		atomicAdd(&sh.scan_done, 1u);
 }
 
 // ---------------------------------------------------------------------------------

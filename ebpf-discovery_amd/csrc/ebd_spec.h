@@ -731,26 +731,39 @@ struct KeyHasher {
 // Mask of the low `k` bytes of a 64-bit piece (k in [0, 8]).
 EBD_HD uint64_t low_bytes(uint32_t k) { return k >= 8 ? ~0ull : ((1ull << (8 * k)) - 1ull); }
 
+// The 8-byte piece of E = host + url at E-offset oo, from A = 8 bytes at host offset oo and
+// B = 8 bytes at url offset oo - hl (either may be garbage when unused); n = |E|.
+EBD_HD uint64_t endpoint_piece(uint32_t hl, uint32_t n, uint32_t oo, uint64_t A, uint64_t B) {
+	const int d = (int)hl - (int)oo; // host bytes left at this piece
+	const uint64_t x = d >= 8 ? A : (d <= 0 ? B : ((A & low_bytes((uint32_t)d)) | (B << (8 * (d & 7)))));
+	return oo < n ? (x & low_bytes(n - oo)) : 0;
+}
+
 // Block form over E = buffer[hs, hs + hl) + buffer[us, us + ul), reading 8-byte pieces
-// through `ld8(offset)` (any alignment; bytes beyond a span are masked off).
+// through `ld8(offset)` (any alignment; bytes beyond a span are masked off).  The loads of
+// a group of 8 pieces (64 bytes of E) are all issued before any is used, so an endpoint of
+// up to 64 bytes costs one memory round trip.
 template <typename Ld8>
 EBD_HD Hash128 endpoint_key(uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us, uint32_t ul, Ld8 ld8) {
+	constexpr uint32_t kGroup = 8;
 	KeyHasher kh;
 	kh.init(pid);
 	const uint32_t n = hl + ul;
-	for (uint32_t o = 0; o < n; o += 16) {
-		uint64_t v[2];
+	for (uint32_t g = 0; g < n; g += 8 * kGroup) {
+		uint64_t A[kGroup], B[kGroup];
 #pragma unroll
-		for (int h = 0; h < 2; h++) {
-			const uint32_t oo = o + 8 * h;
-			const int d = (int)hl - (int)oo; // host bytes left at this piece
-			// both candidate loads, unconditionally (no load behind a branch)
-			const uint64_t A = ld8(hs + (d > 0 ? oo : 0));
-			const uint64_t B = ld8(us + ((d <= 0 && oo < n) ? (uint32_t)(-d) : 0u));
-			uint64_t x = d >= 8 ? A : (d <= 0 ? B : ((A & low_bytes((uint32_t)d)) | (B << (8 * (d & 7)))));
-			v[h] = oo < n ? (x & low_bytes(n - oo)) : 0;
+		for (uint32_t k = 0; k < kGroup; k++) {
+			const uint32_t oo = g + 8 * k;
+			// both candidate loads, unconditionally and at in-span offsets
+			A[k] = ld8(hs + (oo < hl ? oo : 0));
+			B[k] = ld8(us + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
 		}
-		kh.block(v[0], v[1]);
+#pragma unroll
+		for (uint32_t k = 0; k < kGroup; k += 2) {
+			const uint32_t oo = g + 8 * k;
+			if (oo < n)
+				kh.block(endpoint_piece(hl, n, oo, A[k], B[k]), endpoint_piece(hl, n, oo + 8, A[k + 1], B[k + 1]));
+		}
 	}
 	return kh.finish_blocks(n);
 }

@@ -22,9 +22,9 @@ def b(s):
 
 def test_dfa_layout():
     i = ebd.dfa_info()
-    assert i["nstates"] == 256  # 256 table rows; HV(client) states at 254 / 255
-    assert i["url_id"] < i["g2"] < i["g3"] < i["g4"] < i["g4"] + 3 <= 254
-    assert i["hvc0"] == 254
+    # HV(client) states are the last two ids, right after the terminal states
+    assert i["url_id"] < i["g2"] < i["g3"] < i["g4"]
+    assert i["hvc0"] == i["g4"] + 3 and i["nstates"] == i["g4"] + 5 <= 200  # kLdsRows
     assert (i["fin0"], i["fin1"], i["inv"]) == (i["g4"], i["g4"] + 1, i["g4"] + 2)
 
 

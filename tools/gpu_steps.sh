@@ -17,6 +17,11 @@ for spec in "$@"; do
 	echo "=== [$name] rc=$rc in $(( $(date +%s) - start ))s" | tee -a gpurun_out/steps.log
 	tail -n 5 "gpurun_out/$name.log"
 	if [ $rc -ne 0 ]; then status=$rc; fi
+	# a GPU fault reported as an ordinary failure (pytest exit 1) still ends the call
+	if grep -qE "illegal memory access|APERTURE_VIOLATION|Memory access fault" "gpurun_out/$name.log"; then
+		echo "=== stopping: step $name hit a GPU fault" | tee -a gpurun_out/steps.log
+		exit 99
+	fi
 	case $rc in
 		0|1|2|5) ;;
 		*) echo "=== stopping: step $name ended with $rc" | tee -a gpurun_out/steps.log; exit $rc ;;
