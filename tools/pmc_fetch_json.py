@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""HBM bytes per k_fresh launch from rocprofv3 counter passes, as bench.py reads them.
+
+  python tools/pmc_fetch_json.py --fetch <dir> [--write <dir>] --events N --config C --out profiles/x.json
+
+FETCH_SIZE and WRITE_SIZE are rocprofv3's derived counters in KiB.  On gfx950 FETCH_SIZE
+reports half the bytes of a wide streaming read (MI355X_MICROARCH.md, HBM / rocprofv3), so
+it is doubled; WRITE_SIZE is taken as is.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+
+
+def per_launch(d, counter, kernel):
+    vals = collections.defaultdict(float)
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel} under {d}")
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write")
+    ap.add_argument("--events", type=int, required=True)
+    ap.add_argument("--config", type=int, required=True)
+    ap.add_argument("--kernel", default="k_fresh")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    fkib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
+    out = {"kernel": a.kernel, "events": a.events, "config": a.config, "dispatches": nf,
+           "fetch_size_kib_per_launch": fkib, "hbm_read_bytes_per_launch": fkib * 1024 * 2}
+    total = out["hbm_read_bytes_per_launch"]
+    if a.write:
+        wkib, _ = per_launch(a.write, "WRITE_SIZE", a.kernel)
+        out["write_size_kib_per_launch"] = wkib
+        out["hbm_write_bytes_per_launch"] = wkib * 1024
+        total += wkib * 1024
+    out["hbm_bytes_per_launch"] = total
+    out["note"] = "FETCH_SIZE x 1024 x 2 (gfx950 correction) + WRITE_SIZE x 1024, averaged over the launches"
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
