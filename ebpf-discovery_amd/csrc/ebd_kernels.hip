@@ -101,10 +101,12 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 		return 0xffffffffu;
 	}
 	Slot* s = d.slots + idx;
+#ifndef EBD_EXP_AGG_NOATOMIC // experiment: no counter atomics (counts are wrong)
 	if (cls == CLS_INTERNAL)
 		atomicAdd(&s->internal_clients, 1u);
 	else if (cls == CLS_EXTERNAL)
 		atomicAdd(&s->external_clients, 1u);
+#endif
 	if (seq < seen_min)
 		atomicMin(&s->min_seq, seq);
 	return idx;
@@ -236,7 +238,10 @@ struct DevMem {
 
 constexpr int kFreshThreads = 1024;
 constexpr int kFreshWaves = kFreshThreads / 64;
-constexpr int kScanWaves = 12;   // waves [0, kScanWaves) scan; the others finalize
+#ifndef EBD_SCAN_WAVES
+#define EBD_SCAN_WAVES 12
+#endif
+constexpr int kScanWaves = EBD_SCAN_WAVES; // waves [0, kScanWaves) scan; the others finalize
 constexpr uint32_t kRing = 512;  // finalize records in flight per workgroup (power of two)
 #ifndef EBD_FINPER
 #define EBD_FINPER 0
@@ -255,7 +260,7 @@ __device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
 
 // LDS address of entry (s, byte k of the column-mapped word wc).
 __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
-#ifndef EBD_LDS_PLAIN
+#if !defined(EBD_LDS_PLAIN) && !defined(EBD_LDS_COLPERM)
 	return s * kLdsRow + __builtin_amdgcn_ubfe(wc, 8 * (k & 3), 8); // v_bfe + v_mad_u32_u24
 #else
 	return __builtin_amdgcn_perm(s, wc, 0x0c0c0400u | (uint32_t)(k & 3)); // (s << 8) | byte
@@ -494,6 +499,19 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
 	const uint32_t L = (uint32_t)(q.pl >> 48);
 	const uint32_t i = q.idx;
+#ifdef EBD_DBG_CHECK2 // debug build: a record that cannot be real raises bit 60 and is dropped
+	if (p < d.payload || p >= d.payload + (1ull << 36) || L > EBD_BUFFER_MAX_DATA_SIZE || i >= d.n) {
+		atomicOr(&d.ctr[CTR_ERRORS], 1ull << 60);
+		return;
+	}
+#endif
+#ifdef EBD_DBG_CHECK // debug build: a record that cannot be real is reported and dropped
+	if (p < d.payload || p >= d.payload + (1ull << 36) || L > EBD_BUFFER_MAX_DATA_SIZE || i >= d.n) {
+		printf("EBD_DBG fin: block %u thread %u idx %u n %u L %u p-payload %lld c4 %u sf %x\n", blockIdx.x, threadIdx.x, i, d.n,
+				L, (long long)(p - d.payload), q.c4, q.sf);
+		return;
+	}
+#endif
 	ScanRec sr;
 	sr.url = Trk{q.c01 & 0xffffu, q.qs[0]};
 	sr.host = Trk{q.c01 >> 16, q.qs[1]};
@@ -503,6 +521,22 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	sr.cqm = q.cqm;
 	sr.cseen = (q.sf >> 16) & 1u;
 	FreshResult fr;
+#ifdef EBD_DBG_CHECK
+	{
+		FinLoads f;
+		fresh_loads(d.di, sr, DevMem{p}, f);
+		fresh_spans(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, f, L, (uint8_t)(q.sf >> 8), fr);
+		const auto& sp = fr.r.u.span;
+		if (fr.keyed && (sp.host_off + sp.host_len > L || sp.url_off + sp.url_len > L)) {
+			printf("EBD_DBG span: idx %u L %u host %u+%u url %u+%u\n", i, L, sp.host_off, sp.host_len, sp.url_off, sp.url_len);
+			return;
+		}
+		if (16 * sr.term.c >= L + 16 || 16 * sr.url.c >= L + 16 || 16 * sr.host.c >= L + 16 || 16 * sr.cip.c >= L + 16) {
+			printf("EBD_DBG trk: idx %u L %u term %u url %u host %u cip %u\n", i, L, sr.term.c, sr.url.c, sr.host.c, sr.cip.c);
+			return;
+		}
+	}
+#endif
 	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, DevMem{p}, L, q.pid, (uint8_t)(q.sf >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
@@ -683,6 +717,19 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const uint32_t c = min((pk[k] & 0xffffu) + r, pk[k] >> 16);
+#ifdef EBD_DBG_CHECK2
+			if (ak[k] - (uintptr_t)d.payload >= (1ull << 36)) {
+				atomicOr(&d.ctr[CTR_ERRORS], 1ull << 61);
+				ak[k] = (uintptr_t)d.payload;
+			}
+#endif
+#ifdef EBD_DBG_CHECK
+			if (ak[k] < (uintptr_t)d.payload || ak[k] >= (uintptr_t)d.payload + (1ull << 36)) {
+				printf("EBD_DBG issue: block %u thread %u k %d a-payload %lld c %u\n", blockIdx.x, threadIdx.x, k,
+						(long long)(ak[k] - (uintptr_t)d.payload), c);
+				ak[k] = (uintptr_t)d.payload;
+			}
+#endif
 			W[k] = gload16((uintptr_t)(ak[k] + 16ull * c));
 		}
 	};
@@ -1044,37 +1091,84 @@ __global__ void k_carry_pass(Dev d) {
 	}
 }
 
-// Aggregator::newRequest for the fast-path requests, in event order (coalesced reads of the
-// results, keys and events).  The client class comes from the client-IP header's front token
-// when k_fresh found one (cip_classify), else from the session's source address
-// (Aggregator.cpp:60-66, 85-88).  Requests are counted per block: one global atomic each.
+// Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
+// and events).  The client class comes from the client-IP header's front token when k_fresh
+// found one (cip_classify), else from the session's source address (Aggregator.cpp:60-66,
+// 85-88).  A block walks a contiguous range of the batch 256 events at a time.  Requests
+// with a client-IP header (~30 % in config 3) are queued in LDS and parsed kAggThreads at a
+// time, so the token parse, the longest code path, runs on full waves instead of on the
+// few lanes of each wave that have one.  Aggregation is order-free (counters, atomicMin of
+// the first-arrival sequence), so queueing does not change the result.  Requests are counted
+// per block: one global atomic each.
+constexpr uint32_t kCipQueue = 2 * kAggThreads;
+
+__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row) {
+	ebd_event_result r = d.res[i];
+#ifdef EBD_EXP_NOCIP // experiment: no client-IP token parse (classes are wrong)
+	const uint32_t cls = CLS_NONE;
+#else
+	const uint32_t cls = cip_classify(d, i, r, row);
+#endif
+	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+	d.res[i] = r;
+#ifndef EBD_EXP_AGG_NOPROBE // experiment: no service table access (results are wrong)
+	agg_insert(d, d.keys[i], d.seq_base + i, cls);
+#endif
+}
+
 __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
+	__shared__ uint32_t q[kCipQueue]; // queued client-IP requests
+	__shared__ uint32_t qn;
 	__shared__ unsigned long long nreq;
 	uint8_t* row = rows + threadIdx.x * kCipStride;
-	if (threadIdx.x == 0)
+	if (threadIdx.x == 0) {
 		nreq = 0;
+		qn = 0;
+	}
 	__syncthreads();
 	uint32_t cnt = 0;
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
-		ebd_event_result r = d.res[i];
-		if (r.status != EBD_STATUS_FINISHED || (r.info & EBD_INFO_SESSION))
-			continue;
-		uint32_t cls;
-		if (r.info & EBD_INFO_CIP) {
-			cls = cip_classify(d, i, r, row);
-		} else {
-			const uint8_t* evb = (const uint8_t*)(d.ev + i);
-			const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
-			uint8_t src[16];
-			__builtin_memcpy(src, &sv, 16);
-			cls = classify_source(*d.ifs, evb[32], src);
+	const uint32_t steps = (d.n + kAggThreads - 1) / kAggThreads;
+	const uint32_t per = (steps + gridDim.x - 1) / gridDim.x;
+	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
+	for (uint32_t st = s0; st < s1; st++) { // uniform trip count: the barriers below are safe
+		const uint32_t i = st * kAggThreads + threadIdx.x;
+		if (i < d.n) {
+			ebd_event_result r = d.res[i];
+			if (r.status == EBD_STATUS_FINISHED && !(r.info & EBD_INFO_SESSION)) {
+				cnt++;
+				if (r.info & EBD_INFO_CIP) {
+					q[atomicAdd(&qn, 1u)] = i;
+				} else {
+					const uint8_t* evb = (const uint8_t*)(d.ev + i);
+					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
+					uint8_t src[16];
+					__builtin_memcpy(src, &sv, 16);
+					const uint32_t cls = classify_source(*d.ifs, evb[32], src);
+					r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+					d.res[i] = r;
+#ifndef EBD_EXP_AGG_NOPROBE
+					agg_insert(d, d.keys[i], d.seq_base + i, cls);
+#endif
+				}
+			}
 		}
-		r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
-		d.res[i] = r;
-		agg_insert(d, d.keys[i], d.seq_base + i, cls);
-		cnt++;
+		__syncthreads();
+		const uint32_t m = qn; // < kCipQueue: below kAggThreads before this step, + at most kAggThreads
+		__syncthreads();       // every thread has read qn before a push or the drain changes it
+		if (m >= kAggThreads) {
+			agg_cip_one(d, q[threadIdx.x], row);
+			__syncthreads();
+			if (threadIdx.x < m - kAggThreads) // [kAggThreads, m) -> [0, m - kAggThreads): disjoint
+				q[threadIdx.x] = q[kAggThreads + threadIdx.x];
+			if (threadIdx.x == 0)
+				qn = m - kAggThreads;
+			__syncthreads();
+		}
 	}
+	__syncthreads();
+	if (threadIdx.x < qn)
+		agg_cip_one(d, q[threadIdx.x], row);
 	atomicAdd(&nreq, (unsigned long long)cnt);
 	__syncthreads();
 	if (threadIdx.x == 0 && nreq)
