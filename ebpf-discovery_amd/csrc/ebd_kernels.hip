@@ -242,7 +242,10 @@ constexpr int kFreshWaves = kFreshThreads / 64;
 #define EBD_SCAN_WAVES 12
 #endif
 constexpr int kScanWaves = EBD_SCAN_WAVES; // waves [0, kScanWaves) scan; the others finalize
-constexpr uint32_t kRing = 512;  // finalize records in flight per workgroup (power of two)
+#ifndef EBD_RING
+#define EBD_RING 128
+#endif
+constexpr uint32_t kRing = EBD_RING; // finalize records in flight per workgroup (power of two)
 #ifndef EBD_FINPER
 #define EBD_FINPER 0
 #endif
@@ -710,10 +713,23 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		const uint32_t pc = (w << 2) | (last << 16); // window's first chunk | last chunk
 		unsigned long long ak[4];
 		uint32_t pk[4];
+#ifdef EBD_BPERM_ADDR // experiment: quad broadcast through ds_bpermute instead of DPP
+		{
+			const int qb = (int)((threadIdx.x & 63u) & ~3u) * 4;
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)(uint32_t)a);
+				const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)(uint32_t)(a >> 32));
+				ak[k] = (unsigned long long)lo | ((unsigned long long)hi << 32);
+				pk[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)pc);
+			}
+		}
+#else
 		ak[0] = qbcast64<0>(a), pk[0] = qbcast<0>(pc);
 		ak[1] = qbcast64<1>(a), pk[1] = qbcast<1>(pc);
 		ak[2] = qbcast64<2>(a), pk[2] = qbcast<2>(pc);
 		ak[3] = qbcast64<3>(a), pk[3] = qbcast<3>(pc);
+#endif
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const uint32_t c = min((pk[k] & 0xffffu) + r, pk[k] >> 16);
