@@ -3,9 +3,11 @@
 
   python tools/pmc_fetch_json.py --fetch <dir> [--write <dir>] --events N --config C --out profiles/x.json
 
-FETCH_SIZE and WRITE_SIZE are rocprofv3's derived counters in KiB.  On gfx950 FETCH_SIZE
-reports half the bytes of a wide streaming read (MI355X_MICROARCH.md, HBM / rocprofv3), so
-it is doubled; WRITE_SIZE is taken as is.
+FETCH_SIZE and WRITE_SIZE are rocprofv3's derived counters in KiB.  The guide's gfx950 x2
+correction (MI355X_MICROARCH.md, HBM / rocprofv3) is calibrated for wide coalesced streaming
+reads; it does not hold for k_fresh's access pattern: the scan-only build (EBD_EXP_NOFIN)
+reports a raw FETCH_SIZE equal to the bytes it must read (payload + event metadata), so the
+default scale here is 1 (--fetch-scale 2 applies the guide's correction).
 """
 import argparse
 import collections
@@ -33,10 +35,12 @@ def main():
     ap.add_argument("--config", type=int, required=True)
     ap.add_argument("--kernel", default="k_fresh")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--fetch-scale", type=float, default=1.0)
     a = ap.parse_args()
     fkib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
     out = {"kernel": a.kernel, "events": a.events, "config": a.config, "dispatches": nf,
-           "fetch_size_kib_per_launch": fkib, "hbm_read_bytes_per_launch": fkib * 1024 * 2}
+           "fetch_size_kib_per_launch": fkib, "fetch_scale": a.fetch_scale,
+           "hbm_read_bytes_per_launch": fkib * 1024 * a.fetch_scale}
     total = out["hbm_read_bytes_per_launch"]
     if a.write:
         wkib, _ = per_launch(a.write, "WRITE_SIZE", a.kernel)
@@ -44,7 +48,8 @@ def main():
         out["hbm_write_bytes_per_launch"] = wkib * 1024
         total += wkib * 1024
     out["hbm_bytes_per_launch"] = total
-    out["note"] = "FETCH_SIZE x 1024 x 2 (gfx950 correction) + WRITE_SIZE x 1024, averaged over the launches"
+    out["note"] = ("FETCH_SIZE x 1024 x fetch_scale + WRITE_SIZE x 1024, averaged over the launches; scale 1 is "
+                   "calibrated on this kernel: the scan-only build's raw FETCH_SIZE equals its payload + metadata bytes")
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
