@@ -497,8 +497,40 @@ __device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, co
 	}
 }
 
-// fresh_finalize for one record (ebd_fresh.h), run only by the lanes that hold one.
-__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q) {
+// Leading buffer bytes a scan record carries in LDS (window 0 and half of window 1), so that
+// finalize reads the request line and usually the Host header from LDS instead of reloading
+// lines that left L2 while the lane scanned the rest of the buffer.
+#ifndef EBD_STAGE
+#define EBD_STAGE 64
+#endif
+constexpr uint32_t kStage = EBD_STAGE;
+static_assert(kStage == 0 || kStage == 64 || kStage == 96 || kStage == 128, "whole or half windows");
+
+// Buffer bytes for fresh_finalize: offsets [0, lim) from the staged LDS copy `s` (4-B aligned,
+// readable 4 bytes past lim), the rest from the buffer in global memory.
+struct StagedMem {
+	const uint8_t* p;
+	const uint32_t* s;
+	uint32_t lim;
+	__device__ __forceinline__ uint32_t lds4(uint32_t o) const {
+		return __builtin_amdgcn_alignbyte(s[(o >> 2) + 1], s[o >> 2], o & 3u);
+	}
+	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
+		if (o + 4 <= lim)
+			return lds4(o);
+		return *(const __attribute__((address_space(1))) u32a1*)(p + o);
+	}
+	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const {
+		if (o + 8 <= lim)
+			return (unsigned long long)lds4(o) | ((unsigned long long)lds4(o + 4) << 32);
+		return gload8u(p + o);
+	}
+};
+
+// fresh_finalize for one record (ebd_fresh.h), run only by the lanes that hold one.  `stage`:
+// the record's staged leading bytes (pad[0] of the record = how many are valid).
+template <typename Mem>
+__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q, const Mem& mem) {
 	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
 	const uint32_t L = (uint32_t)(q.pl >> 48);
 	const uint32_t i = q.idx;
@@ -540,7 +572,7 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 		}
 	}
 #endif
-	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, DevMem{p}, L, q.pid, (uint8_t)(q.sf >> 8), fr);
+	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, mem, L, q.pid, (uint8_t)(q.sf >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
@@ -564,6 +596,11 @@ struct FreshShared {
 	FinRec ring[kRing];
 	uint32_t ready[kRing]; // position + 1 once ring[pos % kRing] is written
 	uint32_t freed[kRing]; // position + 1 once ring[pos % kRing] is finalized
+#if EBD_STAGE
+	uint32_t rdata[kRing * (kStage / 4) + 4];      // staged leading bytes of ring[slot] (+4: lds4 slack)
+	uint32_t stage[kScanWaves * 64 * (kStage / 4)]; // a scan lane's current buffer, as scanned
+	uint32_t fstage[(kFreshWaves - kScanWaves) * 64 * (kStage / 4) + 4]; // a finalize lane's record's bytes
+#endif
 	uint32_t next_ev;      // next event of the workgroup's range
 	uint32_t tail;         // positions handed out to scan lanes
 	uint32_t claim;        // positions handed out to finalize waves
@@ -613,6 +650,15 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 				}
 				if (have[j]) {
 					q[j] = sh.ring[slot];
+#if EBD_STAGE && EBD_FINPER == 0
+					{ // the staged bytes move to this lane's row, so the slot is free at once
+						const uint4* src = (const uint4*)(sh.rdata + slot * (kStage / 4));
+						uint4* dst = (uint4*)(sh.fstage + ((wave - kScanWaves) * 64 + lane) * (kStage / 4));
+#pragma unroll
+						for (uint32_t k = 0; k < kStage / 16; k++)
+							dst[k] = src[k];
+					}
+#endif
 					lds_store_rel(&sh.freed[slot], pos + 1);
 				} else {
 					q[j] = FinRec{};
@@ -622,8 +668,14 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 				break;
 #ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
 #if EBD_FINPER == 0
-			if (have[0])
-				finalize_rec(d, T, q[0]);
+			if (have[0]) {
+#if EBD_STAGE
+				finalize_rec(d, T, q[0], StagedMem{(const uint8_t*)(uintptr_t)(q[0].pl & 0xffffffffffffull),
+						sh.fstage + ((wave - kScanWaves) * 64 + lane) * (kStage / 4), q[0].pad[0]});
+#else
+				finalize_rec(d, T, q[0], DevMem{(const uint8_t*)(uintptr_t)(q[0].pl & 0xffffffffffffull)});
+#endif
+			}
 #else
 			finalize_recs<kFinPer>(d, T, q, have);
 #endif
@@ -660,6 +712,19 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 				while (lds_load_acq(&sh.freed[slot]) != pos - kRing + 1)
 					__builtin_amdgcn_s_sleep(1);
 			FinRec t;
+#if EBD_STAGE
+			{ // staged bytes equal the buffer's up to the scanned windows and the last chunk's end
+				const uint4* src = (const uint4*)(sh.stage + sl * (kStage / 4));
+				uint4* dst = (uint4*)(sh.rdata + slot * (kStage / 4));
+#pragma unroll
+				for (uint32_t k = 0; k < kStage / 16; k++)
+					dst[k] = src[k];
+				const uint32_t scanned = min(64u * w0, kStage), chunks_end = (e0.L + 15u) & ~15u;
+				t.pad[0] = min(scanned, chunks_end);
+			}
+#else
+			t.pad[0] = 0;
+#endif
 			t.pl = (unsigned long long)(uintptr_t)e0.p | ((unsigned long long)e0.L << 48);
 			t.idx = e0.idx;
 			t.pid = e0.pf;
@@ -673,7 +738,7 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 			t.qs[2] = sr.hend.qs;
 			t.qs[3] = sr.cip.qs;
 			t.qs[4] = sr.term.qs;
-			t.pad[0] = t.pad[1] = 0;
+			t.pad[1] = 0;
 			sh.ring[slot] = t;
 			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
@@ -777,6 +842,15 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		if (valid) {
 			if (w0 == 0)
 				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
+#if EBD_STAGE
+			if (64 * w0 < kStage) { // this window's chunks into the lane's staging row
+				uint4* st = (uint4*)(sh.stage + sl * (kStage / 4)) + 4 * w0;
+#pragma unroll
+				for (int k = 0; k < 4; k++)
+					if (64 * w0 + 16 * k < kStage)
+						st[k] = make_uint4(X[k].w[0], X[k].w[1], X[k].w[2], X[k].w[3]);
+			}
+#endif
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
