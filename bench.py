@@ -47,6 +47,10 @@ def parse_args():
     ap.add_argument("--service-capacity", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=("cold", "warm"), default="cold",
+                    help="cold: every step is one report interval, the service table cleared before the batch "
+                         "(every service of the batch is created inside the timed step); warm: the table keeps "
+                         "the services of earlier steps (all hits after the first batch)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fetch_config3.json"),
                     help="rocprofv3 FETCH_SIZE summary giving HBM traffic per k_fresh launch")
     return ap.parse_args()
@@ -124,31 +128,43 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] generated {E} events, {size / 1e9:.2f} GB payload in {time.perf_counter() - t0:.1f} s")
 
-    def step(k):
+    def step(k, cold):
+        if cold:
+            ctx.clear()  # Aggregator::clear after the previous interval's report (Aggregator.cpp:136-153)
         ctx.set_seq_base(k * world * E + first)  # global trace order of this shard's events
         ctx.submit_device(ev_t, len_t, off_t, pay_t, E)
 
+    def timed_steps(k0, cold):
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(k0, k0 + args.steps):
+            step(k, cold)
+        ctx.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            el = float(tt.item())
+        return el
+
+    cold = args.mode == "cold"
     for k in range(args.warmup):
-        step(k)
+        step(k, cold)
     ctx.sync()
     ctx.reset_kernel_times()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t
+    elapsed = timed_steps(args.warmup, cold)
     kt = ctx.kernel_times()
     st = ctx.stats()
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    # the other mode, reported beside (same batch, same number of steps)
+    other_mode = "warm" if cold else "cold"
+    ctx.reset_kernel_times()
+    other_elapsed = timed_steps(args.warmup + args.steps, not cold)
+    other_kt = ctx.kernel_times()
 
     # algorithmic bytes of one batch: sum(consumed + 40) per data event
     res = ctx.results()
@@ -162,8 +178,10 @@ def main():
         try:
             with open(args.pmc) as f:
                 pm = json.load(f)
-            if pm.get("events") == E and pm.get("config") == cfg:
+            if pm.get("events") == E and pm.get("config") == cfg and pm.get("build_id") == ebd.build_id():
                 traffic = pm["hbm_bytes_per_launch"]
+            else:
+                log(f"[bench] {args.pmc} is for build {pm.get('build_id')} / {pm.get('events')} events: traffic null")
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -212,6 +230,10 @@ def main():
         "services": n_services,
         "errors": st["error_names"],
         "merge_ms": merge_ms,
+        "mode": args.mode,
+        other_mode: {"value": total_events / other_elapsed, "ms_per_step": other_elapsed / args.steps * 1e3,
+                     "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in other_kt.items()}},
+        "build_id": ebd.build_id(),
     }
     print(json.dumps(out), flush=True)
 

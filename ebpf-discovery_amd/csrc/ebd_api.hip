@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <sys/random.h>
 #include <vector>
 
 #include "ebd_device.h"
@@ -24,7 +25,9 @@ hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
-hipError_t launch_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt, hipStream_t st);
+hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out,
+		hipStream_t st, int cus);
+hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
 		unsigned long long* alen, hipStream_t st);
 hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, EventRec* ev,
@@ -33,6 +36,11 @@ void build_gen_tables(GenTables* T);
 } // namespace ebd
 
 using namespace ebd;
+
+// the layouts the Python binding (ebd/__init__.py) and tests/test_abi.py assume
+static_assert(sizeof(ebd_config) == 56, "ebd_config layout");
+static_assert(sizeof(ebd_stats) == 72, "ebd_stats layout");
+static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 64, "result layouts");
 
 #define HIP_TRY(x)                                                                                                   \
 	do {                                                                                                             \
@@ -56,6 +64,7 @@ struct ebd_ctx {
 	int cus = 256;
 	hipStream_t stream = nullptr;
 	ebd_config cfg{};
+	HashKey hkey{};
 	// tables
 	DfaTable* dfa_host = nullptr;
 	KeyTrie trie_host{};
@@ -119,8 +128,9 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify"};
-enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY, KT_N };
+		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify", "k_clear_used"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY,
+	KT_CLEAR, KT_N };
 
 static hipEvent_t take_event(ebd_ctx* c) {
 	if (!c->free_events.empty()) {
@@ -165,6 +175,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.di = c->dfa_host->info;
 	d.trie = c->d_trie;
 	d.ifs = c->d_ifs;
+	d.hkey = c->hkey;
 	d.res = c->d_res;
 	d.keys = c->d_keys;
 	d.slots = c->d_slots;
@@ -214,6 +225,11 @@ static void ctx_free(ebd_ctx* c) {
 
 extern "C" {
 
+#ifndef EBD_BUILD_ID
+#define EBD_BUILD_ID "unknown"
+#endif
+const char* ebd_build_id(void) { return EBD_BUILD_ID; }
+
 const char* ebd_strerror(int err) {
 	switch (-err) {
 	case 0: return "success";
@@ -242,6 +258,17 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	if (hipSetDevice(c->device) != hipSuccess) {
 		ctx_free(c);
 		return -EIO;
+	}
+	c->hkey = HashKey{cfg->hash_key[0], cfg->hash_key[1]};
+	if (c->hkey.k0 == 0 && c->hkey.k1 == 0) {
+		uint64_t k[2] = {0, 0};
+		if (getrandom(k, sizeof(k), 0) != (ssize_t)sizeof(k)) {
+			ctx_free(c);
+			return -EIO;
+		}
+		c->hkey = HashKey{k[0], k[1]};
+		c->cfg.hash_key[0] = k[0];
+		c->cfg.hash_key[1] = k[1];
 	}
 	hipDeviceProp_t prop;
 	if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -281,12 +308,12 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	c->slot_cap = next_pow2(cfg->service_capacity ? cfg->service_capacity : (1u << 22));
 	CTX_TRY(hipMalloc(&c->d_slots, (size_t)c->slot_cap * sizeof(Slot)));
 	CTX_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
-	c->new_cap = c->max_events < c->slot_cap ? c->max_events : c->slot_cap;
+	c->new_cap = c->slot_cap; // claimed-slot list, cumulative until ebd_clear
 	CTX_TRY(hipMalloc(&c->d_new_slots, (size_t)c->new_cap * sizeof(uint32_t)));
 	c->verify_cap = c->max_events;
 	CTX_TRY(hipMalloc(&c->d_verify, (size_t)c->verify_cap * sizeof(VerifyRec)));
 	c->sarena_cap = cfg->string_arena ? cfg->string_arena : (256ull << 20);
-	CTX_TRY(hipMalloc(&c->d_sarena, c->sarena_cap));
+	CTX_TRY(hipMalloc(&c->d_sarena, c->sarena_cap + 64)); // k_reps stores whole 8-byte words
 	// per-batch buffers
 	const uint64_t n = c->max_events;
 	CTX_TRY(hipMalloc(&c->d_res, n * sizeof(ebd_event_result)));
@@ -310,7 +337,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		c->sstr_cap = 64ull << 20;
 	if (c->sstr_cap > (4ull << 30))
 		c->sstr_cap = 4ull << 30;
-	CTX_TRY(hipMalloc(&c->d_sstr, c->sstr_cap));
+	CTX_TRY(hipMalloc(&c->d_sstr, c->sstr_cap + 64)); // k_reps reads whole 8-byte words
 	CTX_TRY(hipMalloc(&c->d_ctr, CTR_COUNT * sizeof(unsigned long long)));
 	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_COUNT * sizeof(unsigned long long), c->stream));
 	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
@@ -331,6 +358,14 @@ int ebd_ctx_destroy(ebd_ctx* c) {
 }
 
 void* ebd_ctx_stream(ebd_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int ebd_get_hash_key(ebd_ctx* c, uint64_t out[2]) {
+	if (!c || !out)
+		return -EINVAL;
+	out[0] = c->hkey.k0;
+	out[1] = c->hkey.k1;
+	return 0;
+}
 
 int ebd_set_interfaces(ebd_ctx* c, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6) {
 	if (!c || n4 > 64 || n6 > 32 || (n4 && !v4) || (n6 && !v6))
@@ -552,25 +587,24 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
-	if (!c->d_collect)
-		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(launch_collect(c->d_slots, c->slot_cap, c->d_collect, c->d_cnt, c->stream));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	uint64_t used = c->h_ctr[CTR_SARENA];
 	if (used > c->sarena_cap)
 		used = c->sarena_cap;
-	const uint64_t cnt = c->h_ctr[CTR_COUNT];
+	const uint64_t cnt = c->h_ctr[CTR_SERVICES];
 	*strlen = used;
 	*n = (uint32_t)cnt;
 	if (!out)
 		return 0;
 	if (cnt > cap || (used && (!strings || used > strcap)))
 		return -ENOSPC;
-	if (cnt)
+	if (cnt) {
+		if (!c->d_collect)
+			HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
+		HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_collect, c->stream, c->cus));
 		HIP_TRY(hipMemcpyAsync(out, c->d_collect, cnt * sizeof(ebd_service), hipMemcpyDeviceToHost, c->stream));
+	}
 	if (used)
 		HIP_TRY(hipMemcpyAsync(strings, c->d_sarena, used, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -582,10 +616,9 @@ int ebd_clear(ebd_ctx* c) {
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
-	HIP_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->stream, c->cus); }));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
 
@@ -809,11 +842,11 @@ struct HostMem {
 };
 
 int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags, const uint8_t* src16,
-		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, ebd_event_result* out,
-		uint64_t key[2]) {
+		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, const uint64_t hash_key[2],
+		ebd_event_result* out, uint64_t key[2]) {
 	const KeyTrie* trie;
 	const DfaTable* t = host_dfa(&trie);
-	if (!t || !out || (len && !buf) || len > EBD_BUFFER_MAX_DATA_SIZE)
+	if (!t || !out || !hash_key || (len && !buf) || len > EBD_BUFFER_MAX_DATA_SIZE)
 		return -EINVAL;
 	static Interfaces ifs;
 	fill_ifs(ifs, v4, n4, v6, n6);
@@ -823,7 +856,7 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
 	const bool post = len > 0 && buf[0] == 'P';
-	fresh_finalize(HostTab{t->next}, t->info, sr, s, post, HostMem{buf, len}, len, pid, flags, fr);
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, post, HostMem{buf, len}, len, HashKey{hash_key[0], hash_key[1]}, pid, flags, fr);
 	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
 		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
 	if (fr.cip) { // what k_agg_fast (cip_classify) does for this event
@@ -876,11 +909,11 @@ int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t
 	return classify_token(ifs, token + tb, te - tb);
 }
 
-int ebd_host_endpoint_key(uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]) {
-	if (!key || (len && !endpoint))
+int ebd_host_endpoint_key(const uint64_t hash_key[2], uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]) {
+	if (!hash_key || !key || (len && !endpoint))
 		return -EINVAL;
 	KeyHasher kh;
-	kh.init(pid);
+	kh.init(HashKey{hash_key[0], hash_key[1]}, pid);
 	kh.bytes(endpoint, len);
 	const Hash128 h = kh.finish();
 	key[0] = h.lo;

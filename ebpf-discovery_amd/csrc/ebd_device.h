@@ -92,6 +92,7 @@ struct Dev {
 	DfaInfo di;
 	const KeyTrie* trie;
 	const Interfaces* ifs;
+	HashKey hkey; // service-key PRF key (ebd_spec.h KeyHasher)
 	// batch
 	const EventRec* ev;
 	const uint32_t* len;

@@ -221,7 +221,7 @@ EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint
 // several events).  pid: the DiscoveryEvent's (Discovery.cpp:136, 157).
 template <typename Tab, typename Mem>
 EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, bool post, const Mem& mem,
-		uint32_t L, uint32_t pid, uint8_t flags, FreshResult& out) {
+		uint32_t L, const HashKey& key, uint32_t pid, uint8_t flags, FreshResult& out) {
 	FinLoads f;
 	fresh_loads(di, sr, mem, f);
 	fresh_spans(T, di, sr, s_final, post, f, L, flags, out);
@@ -231,7 +231,7 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 		out.key.lo = sp.host_len * 31 + sp.url_len;
 		out.key.hi = 1;
 #else
-		out.key = endpoint_key(pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
+		out.key = endpoint_key(key, pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
 #endif
 	}
 }

@@ -60,7 +60,9 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 			t = atomicCAS(&s->tag, 0ull, h.lo);
 			if (t == 0) {
 				atomicExch(&s->hi, h.hi);
-				const unsigned long long k = atomicAdd(&d.ctr[CTR_NEW], 1ull);
+				// the claimed-slot list is cumulative over batches (k_reps, ebd_clear and
+				// ebd_collect_services walk it); CTR_SERVICES moves only in k_verify
+				const unsigned long long k = atomicAdd(&d.ctr[CTR_NEW], 1ull) + ld_relaxed(&d.ctr[CTR_SERVICES]);
 				if (k < d.new_cap)
 					d.new_slots[k] = idx;
 				else
@@ -454,7 +456,7 @@ __device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, co
 		ul[n] = k ? fr[n].r.u.span.url_len : 0;
 		en[n] = hl[n] + ul[n];
 		nmax = max(nmax, en[n]);
-		kh[n].init(q[n].pid);
+		kh[n].init(d.hkey, q[n].pid);
 	}
 	for (uint32_t g = 0; g < nmax; g += 8 * kGroup) {
 		uint64_t A[N][kGroup], B[N][kGroup];
@@ -469,11 +471,10 @@ __device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, co
 #pragma unroll
 		for (int n = 0; n < N; n++)
 #pragma unroll
-			for (uint32_t k = 0; k < kGroup; k += 2) {
+			for (uint32_t k = 0; k < kGroup; k++) {
 				const uint32_t oo = g + 8 * k;
 				if (oo < en[n])
-					kh[n].block(endpoint_piece(hl[n], en[n], oo, A[n][k], B[n][k]),
-							endpoint_piece(hl[n], en[n], oo + 8, A[n][k + 1], B[n][k + 1]));
+					kh[n].word(endpoint_piece(hl[n], en[n], oo, A[n][k], B[n][k]));
 			}
 	}
 #pragma unroll
@@ -485,7 +486,7 @@ __device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, co
 #ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
 			d.keys[i] = Hash128{en[n], 1};
 #else
-			d.keys[i] = kh[n].finish_blocks(en[n]);
+			d.keys[i] = kh[n].finish_words(en[n]);
 #endif
 		} else if (fr[n].r.status == EBD_STATUS_UNFINISHED) {
 			// the session may be saved (Discovery.cpp:148-150): sequential path
@@ -532,6 +533,7 @@ struct StagedMem {
 template <typename Mem>
 __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q, const Mem& mem) {
 	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
+	(void)p; // used by the debug builds below
 	const uint32_t L = (uint32_t)(q.pl >> 48);
 	const uint32_t i = q.idx;
 #ifdef EBD_DBG_CHECK2 // debug build: a record that cannot be real raises bit 60 and is dropped
@@ -572,7 +574,7 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 		}
 	}
 #endif
-	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, mem, L, q.pid, (uint8_t)(q.sf >> 8), fr);
+	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, mem, L, d.hkey, q.pid, (uint8_t)(q.sf >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
@@ -1003,7 +1005,7 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	uint8_t info = (uint8_t)((g.mcand == 'P' ? EBD_INFO_POST : 0) | ((g.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0) | EBD_INFO_SESSION);
 	uint8_t cls;
 	KeyHasher kh;
-	kh.init(ev.pid);
+	kh.init(d.hkey, ev.pid);
 	uint32_t tb = 0, te = 0;
 	if (at + total > d.sstr_cap) {
 		set_error(d, EBD_ERR_ARENA_FULL);
@@ -1266,13 +1268,14 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 }
 
 // First-arrival representative of every service created in this batch (Aggregator.cpp:
-// 112-130, 160-167): endpoint string, domain, scheme, pid.
+// 112-130, 160-167): endpoint string, domain, scheme, pid.  The endpoint E = host + url is
+// copied as 8-byte words (unaligned loads from the buffer, aligned stores to an 8-byte
+// aligned arena offset), and the domain (A:117-125) is found on the words in registers.
 __global__ void k_reps(Dev d) {
 	const unsigned long long nn = d.ctr[CTR_NEW];
-	const uint32_t n_new = (uint32_t)(nn < d.new_cap ? nn : d.new_cap);
-	if (blockIdx.x == 0 && threadIdx.x == 0 && nn)
-		atomicAdd(&d.ctr[CTR_SERVICES], nn);
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n_new; k += gridDim.x * blockDim.x) {
+	const unsigned long long base = d.ctr[CTR_SERVICES];
+	const unsigned long long end = min(base + nn, (unsigned long long)d.new_cap);
+	for (unsigned long long k = base + blockIdx.x * blockDim.x + threadIdx.x; k < end; k += gridDim.x * blockDim.x) {
 		Slot* s = d.slots + d.new_slots[k];
 		const unsigned long long seq = s->min_seq;
 		const uint32_t e = (uint32_t)(seq - d.seq_base);
@@ -1292,24 +1295,48 @@ __global__ void k_reps(Dev d) {
 			url = p + r.u.span.url_off;
 			ul = r.u.span.url_len;
 		}
-		const unsigned long long at = atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)(hl + ul));
-		uint32_t doff = 0, dlen = 0;
-		host_domain(host, hl, &doff, &dlen);
+		const uint32_t n = hl + ul;
+		const unsigned long long at = atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((n + 7u) & ~7u));
 		s->pid = d.ev[e].pid;
-		s->ep_len = hl + ul;
-		s->dom = doff | (dlen << 16);
+		s->ep_len = n;
 		s->info = ((r.info & EBD_INFO_HTTPS) ? 1u : 0u) | 2u;
-		if (at + hl + ul > d.sarena_cap) {
+		const bool fits = at + n <= d.sarena_cap;
+		if (!fits) {
 			set_error(d, EBD_ERR_ARENA_FULL);
 			s->ep_off = ~0ull;
-			continue;
+		} else {
+			s->ep_off = at;
 		}
-		s->ep_off = at;
-		uint8_t* dst = d.sarena + at;
-		for (uint32_t b = 0; b < hl; b++)
-			dst[b] = host[b];
-		for (uint32_t b = 0; b < ul; b++)
-			dst[hl + b] = url[b];
+		unsigned long long* dst = (unsigned long long*)(d.sarena + at);
+		uint32_t lb = kNone, rb = kNone, colon = kNone;
+		for (uint32_t oo = 0; oo < n; oo += 8) {
+			const unsigned long long A = gload8u(host + (oo < hl ? oo : 0));
+			const unsigned long long B = gload8u(url + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
+			const unsigned long long w = endpoint_piece(hl, n, oo, A, B);
+			if (fits)
+				dst[oo >> 3] = w;
+			if (oo < hl && (lb == kNone || rb == kNone || colon == kNone)) { // host bytes of this word
+				const uint32_t m = min(8u, hl - oo);
+				for (uint32_t b = 0; b < m; b++) {
+					const uint32_t c = (uint32_t)(w >> (8 * b)) & 0xffu;
+					if (c == '[' && lb == kNone)
+						lb = oo + b;
+					else if (c == ']' && lb != kNone && rb == kNone)
+						rb = oo + b;
+					if (c == ':' && colon == kNone)
+						colon = oo + b;
+				}
+			}
+		}
+		uint32_t doff, dlen;
+		if (lb != kNone) {
+			doff = rb != kNone ? lb : 0;
+			dlen = rb != kNone ? rb - lb + 1 : 0;
+		} else {
+			doff = 0;
+			dlen = colon != kNone ? colon : hl;
+		}
+		s->dom = doff | (dlen << 16);
 	}
 }
 
@@ -1319,6 +1346,30 @@ __global__ void k_verify(Dev d) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
 		if (d.slots[d.verify[k].slot].hi != d.verify[k].hi)
 			set_error(d, EBD_ERR_COLLISION);
+	if (blockIdx.x == 0 && threadIdx.x == 0) { // this batch's claims join the service count (after k_reps)
+		const unsigned long long nn = d.ctr[CTR_NEW], base = d.ctr[CTR_SERVICES];
+		d.ctr[CTR_SERVICES] = min(base + nn, (unsigned long long)d.new_cap);
+	}
+}
+
+// Aggregator::clear (Aggregator.cpp:136-153): every claimed slot back to empty.
+__global__ void k_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots) {
+	const unsigned long long n = ctr[CTR_SERVICES];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		Slot s;
+		s.tag = 0;
+		s.hi = 0;
+		s.min_seq = ~0ull;
+		s.ep_off = 0;
+		s.pid = 0;
+		s.internal_clients = 0;
+		s.external_clients = 0;
+		s.ep_len = 0;
+		s.dom = 0;
+		s.info = 0;
+		s.pad[0] = s.pad[1] = 0;
+		slots[used[k]] = s;
+	}
 }
 
 __global__ void k_sset_clear(Dev d) {
@@ -1352,12 +1403,11 @@ __global__ void k_slots_init(Slot* slots, uint32_t n) {
 	}
 }
 
-__global__ void k_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt) {
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		const Slot& s = slots[k];
-		if (s.tag == 0)
-			continue;
-		const unsigned long long at = atomicAdd(cnt, 1ull);
+// Aggregator::collectServices (Aggregator.cpp:170-181) over the claimed-slot list.
+__global__ void k_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out) {
+	const unsigned long long n = ctr[CTR_SERVICES];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const Slot& s = slots[used[k]];
 		ebd_service v;
 		v.pid = s.pid;
 		v.internal_clients = s.internal_clients;
@@ -1372,7 +1422,7 @@ __global__ void k_collect(const Slot* slots, uint32_t n, ebd_service* out, unsig
 		v.first_seq = s.min_seq;
 		v.key_lo = s.tag;
 		v.key_hi = s.hi;
-		out[at] = v;
+		out[k] = v;
 	}
 }
 
@@ -1433,7 +1483,7 @@ hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
 	return hipGetLastError();
 }
 hipError_t launch_reps(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_reps, dim3(cus * 4), dim3(64), 0, st, d);
+	hipLaunchKernelGGL(k_reps, dim3(cus * 16), dim3(256), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus) {
@@ -1448,8 +1498,13 @@ hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(k_slots_init, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n);
 	return hipGetLastError();
 }
-hipError_t launch_collect(const Slot* slots, uint32_t n, ebd_service* out, unsigned long long* cnt, hipStream_t st) {
-	hipLaunchKernelGGL(k_collect, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n, out, cnt);
+hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out,
+		hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, slots, used, ctr, out);
+	return hipGetLastError();
+}
+hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_clear_used, dim3(cus * 8), dim3(256), 0, st, used, ctr, slots);
 	return hipGetLastError();
 }
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,

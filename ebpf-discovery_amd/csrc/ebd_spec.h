@@ -660,49 +660,57 @@ EBD_HD uint64_t fmix64(uint64_t k) {
 	return k;
 }
 
-// 64 x 64 -> 128-bit multiply folded to 64 bits (the "mum" step of wyhash).
-EBD_HD uint64_t wymix(uint64_t a, uint64_t b) {
-	const unsigned __int128 r = (unsigned __int128)a * b;
-	return (uint64_t)r ^ (uint64_t)(r >> 64);
-}
-
-// The endpoint E = host + url is hashed in 16-byte blocks (two little-endian 64-bit
-// pieces, the last block zero-padded) by two independent wymix chains, then finished
-// with the length.  A block depends only on E's bytes, so every host/url split of the
-// same endpoint hashes alike.  The data-side constants have bytes >= 0x80, which no
-// host/url byte can have (HttpRequestParser.cpp:53-76 character classes), so no
-// block can zero a multiplier.
-constexpr uint64_t kEpP0 = 0xa0761d6478bd642full, kEpP1 = 0xe7037ed1a0b428dbull;
-constexpr uint64_t kEpP2 = 0x8ebc6af09c88c6e3ull, kEpP3 = 0x589965cc75374cc3ull;
+// The service key is a keyed pseudo-random function of the exact bytes the reference keys
+// on (pid, endpoint = host + url; Aggregator.h:29-37): SipHash-1-3 with the 128-bit output
+// (Aumasson & Bernstein; the HashDoS-resistant PRF), keyed by a secret 128-bit HashKey
+// drawn per context (ebd_config.hash_key, or getrandom).  The message is the 8-byte pid,
+// then E = host + url as little-endian 8-byte words (the last one zero-padded), then a word
+// holding |E|; so every host/url split of the same endpoint hashes alike, and the encoding
+// is injective.  Without the key an adversary cannot construct two endpoints with one key;
+// two distinct (pid, endpoint) pairs share a key with probability 2^-128 each.
+struct HashKey {
+	uint64_t k0, k1;
+};
 
 struct KeyHasher {
-	uint64_t h1, h2, a, acc;
-	uint32_t total, has_a;
-	EBD_HD void init(uint32_t pid) {
-		h1 = fmix64(0x9368e53c2f6af274ull ^ pid);
-		h2 = fmix64(0x586dcd208f7cd3fdull ^ ((uint64_t)pid << 32));
-		a = acc = 0;
-		total = has_a = 0;
+	uint64_t v0, v1, v2, v3, acc;
+	uint32_t total;
+	EBD_HD static void round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& e) {
+		a += b;
+		b = rotl64(b, 13);
+		b ^= a;
+		a = rotl64(a, 32);
+		c += e;
+		e = rotl64(e, 16);
+		e ^= c;
+		a += e;
+		e = rotl64(e, 21);
+		e ^= a;
+		c += b;
+		b = rotl64(b, 17);
+		b ^= c;
+		c = rotl64(c, 32);
 	}
-	EBD_HD void block(uint64_t x, uint64_t y) {
-		h1 = wymix(x ^ kEpP0, y ^ h1);
-		h2 = wymix(y ^ kEpP1, x ^ h2);
+	EBD_HD void word(uint64_t m) { // one message word, c = 1 round
+		v3 ^= m;
+		round(v0, v1, v2, v3);
+		v0 ^= m;
+	}
+	EBD_HD void init(const HashKey& k, uint32_t pid) {
+		v0 = k.k0 ^ 0x736f6d6570736575ull;
+		v1 = k.k1 ^ 0x646f72616e646f6dull ^ 0xee; // 128-bit output variant
+		v2 = k.k0 ^ 0x6c7967656e657261ull;
+		v3 = k.k1 ^ 0x7465646279746573ull;
+		acc = 0;
+		total = 0;
+		word(pid);
 	}
 	// streaming form (session path, host code)
-	EBD_HD void piece(uint64_t v) {
-		if (has_a) {
-			block(a, v);
-			has_a = 0;
-		} else {
-			a = v;
-			has_a = 1;
-		}
-	}
 	EBD_HD void byte(uint32_t b) {
 		acc |= (uint64_t)(b & 0xff) << (8 * (total & 7));
 		total++;
 		if ((total & 7) == 0) {
-			piece(acc);
+			word(acc);
 			acc = 0;
 		}
 	}
@@ -710,21 +718,26 @@ struct KeyHasher {
 		for (uint32_t i = 0; i < n; i++)
 			byte(p[i]);
 	}
-	// after blocks fed directly (block form): n = endpoint length
-	EBD_HD Hash128 finish_blocks(uint32_t n) const {
-		uint64_t x = wymix(h1 ^ kEpP2, (uint64_t)n ^ kEpP3);
-		uint64_t y = wymix(h2 ^ kEpP3, ((uint64_t)n << 32) ^ kEpP2);
+	// after the words were fed directly (block form): n = endpoint length; d = 3 rounds
+	EBD_HD Hash128 finish_words(uint32_t n) {
+		word(((uint64_t)0xe5 << 56) | n);
+		v2 ^= 0xee;
+		round(v0, v1, v2, v3);
+		round(v0, v1, v2, v3);
+		round(v0, v1, v2, v3);
 		Hash128 r;
-		r.lo = fmix64(x + y) | 1ull; // 0 marks an empty slot
-		r.hi = fmix64(y ^ rotl64(x, 29)) | 1ull;
+		r.lo = (v0 ^ v1 ^ v2 ^ v3) | 1ull; // 0 marks an empty slot
+		v1 ^= 0xdd;
+		round(v0, v1, v2, v3);
+		round(v0, v1, v2, v3);
+		round(v0, v1, v2, v3);
+		r.hi = (v0 ^ v1 ^ v2 ^ v3) | 1ull;
 		return r;
 	}
 	EBD_HD Hash128 finish() {
 		if (total & 7)
-			piece(acc);
-		if (has_a)
-			block(a, 0);
-		return finish_blocks(total);
+			word(acc);
+		return finish_words(total);
 	}
 };
 
@@ -744,10 +757,10 @@ EBD_HD uint64_t endpoint_piece(uint32_t hl, uint32_t n, uint32_t oo, uint64_t A,
 // a group of 8 pieces (64 bytes of E) are all issued before any is used, so an endpoint of
 // up to 64 bytes costs one memory round trip.
 template <typename Ld8>
-EBD_HD Hash128 endpoint_key(uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us, uint32_t ul, Ld8 ld8) {
+EBD_HD Hash128 endpoint_key(const HashKey& key, uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us, uint32_t ul, Ld8 ld8) {
 	constexpr uint32_t kGroup = 8;
 	KeyHasher kh;
-	kh.init(pid);
+	kh.init(key, pid);
 	const uint32_t n = hl + ul;
 	for (uint32_t g = 0; g < n; g += 8 * kGroup) {
 		uint64_t A[kGroup], B[kGroup];
@@ -759,13 +772,13 @@ EBD_HD Hash128 endpoint_key(uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us,
 			B[k] = ld8(us + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
 		}
 #pragma unroll
-		for (uint32_t k = 0; k < kGroup; k += 2) {
+		for (uint32_t k = 0; k < kGroup; k++) {
 			const uint32_t oo = g + 8 * k;
 			if (oo < n)
-				kh.block(endpoint_piece(hl, n, oo, A[k], B[k]), endpoint_piece(hl, n, oo + 8, A[k + 1], B[k + 1]));
+				kh.word(endpoint_piece(hl, n, oo, A[k], B[k]));
 		}
 	}
-	return kh.finish_blocks(n);
+	return kh.finish_words(n);
 }
 
 } // namespace ebd

@@ -40,12 +40,15 @@ SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
 assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 64
 CFG_TIMING = 2
+# A fixed service-key PRF key for tests that compare keys across contexts or with the host
+# hooks; products leave the key to the library (a fresh random key per context).
+TEST_HASH_KEY = (0x0706050403020100, 0x0F0E0D0C0B0A0908)
 
 
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("max_events", C.c_uint32), ("max_payload", C.c_uint64),
                 ("service_capacity", C.c_uint32), ("string_arena", C.c_uint64), ("lru_capacity", C.c_uint32),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("hash_key", C.c_uint64 * 2)]
 
 
 class DeviceBatch(C.Structure):
@@ -81,6 +84,7 @@ _SIGS = {
     "ebd_ctx_create": (C.c_int, [C.POINTER(Config), C.POINTER(C.c_void_p)]),
     "ebd_ctx_destroy": (C.c_int, [C.c_void_p]),
     "ebd_ctx_stream": (C.c_void_p, [C.c_void_p]),
+    "ebd_get_hash_key": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ebd_set_interfaces": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     "ebd_submit_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                    C.c_uint32]),
@@ -98,6 +102,7 @@ _SIGS = {
     "ebd_clear": (C.c_int, [C.c_void_p]),
     "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ebd_strerror": (C.c_char_p, [C.c_int]),
+    "ebd_build_id": (C.c_char_p, []),
     "ebd_trace_size": (C.c_int, [C.POINTER(TraceConfig), C.POINTER(C.c_uint64)]),
     "ebd_trace_generate_host": (C.c_int, [C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_uint64]),
@@ -107,12 +112,12 @@ _SIGS = {
     # testing header
     "ebd_host_dfa_info": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
-                                 C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+                                 C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ebd_host_gp_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
     "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_uint32]),
     "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
-    "ebd_host_endpoint_key": (C.c_int, [C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "ebd_host_endpoint_key": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
 }
 
 _lib = None
@@ -135,6 +140,10 @@ def lib():
             f.argtypes = args
         _lib = L
     return _lib
+
+
+def build_id():
+    return lib().ebd_build_id().decode()
 
 
 class EbdError(RuntimeError):
@@ -174,10 +183,12 @@ class Context:
     """One GPU context: the Discovery consumer state (session LRU) + the Aggregator."""
 
     def __init__(self, max_events, device=0, max_payload=0, service_capacity=0, string_arena=0, lru_capacity=0,
-                 timing=False):
+                 timing=False, hash_key=None):
         cfg = Config(device=device, max_events=max_events, max_payload=max_payload,
                      service_capacity=service_capacity, string_arena=string_arena, lru_capacity=lru_capacity,
                      flags=CFG_TIMING if timing else 0)
+        if hash_key is not None:
+            cfg.hash_key[0], cfg.hash_key[1] = int(hash_key[0]), int(hash_key[1])
         h = C.c_void_p()
         _check(lib().ebd_ctx_create(C.byref(cfg), C.byref(h)), "ebd_ctx_create")
         self.h = h
@@ -194,6 +205,12 @@ class Context:
     @property
     def stream(self):
         return lib().ebd_ctx_stream(self.h)
+
+    @property
+    def hash_key(self):
+        k = np.zeros(2, np.uint64)
+        _check(lib().ebd_get_hash_key(self.h, _p(k)), "ebd_get_hash_key")
+        return int(k[0]), int(k[1])
 
     def set_interfaces(self, v4=(), v6=()):
         v4, v6 = list(v4), list(v6)
@@ -339,14 +356,20 @@ def dfa_info():
     return dict(zip(keys, (int(x) for x in a)))
 
 
-def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_DATA, src16=bytes(16), v4=(), v6=()):
+def _hkey(hash_key):
+    return np.array(hash_key if hash_key is not None else TEST_HASH_KEY, np.uint64)
+
+
+def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_DATA, src16=bytes(16), v4=(), v6=(),
+               hash_key=None):
     out = np.zeros(1, RESULT_DTYPE)
+    hk = _hkey(hash_key)
     key = np.zeros(2, np.uint64)
     b = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
     s = np.frombuffer(src16, np.uint8)
     v4, v6 = list(v4), list(v6)
     _check(lib().ebd_host_fresh(_p(b), len(buf), pid, flags, _p(s), _nets4(v4), len(v4), _nets6(v6), len(v6),
-                                _p(out), _p(key)), "ebd_host_fresh")
+                                _p(hk), _p(out), _p(key)), "ebd_host_fresh")
     return out[0], (int(key[0]), int(key[1]))
 
 
@@ -375,10 +398,11 @@ def host_classify_source(src16: bytes, flags, v4=(), v6=()):
     return lib().ebd_host_classify(_p(b), 16, 1, flags, _nets4(v4), len(v4), _nets6(v6), len(v6))
 
 
-def host_endpoint_key(pid: int, endpoint: bytes):
+def host_endpoint_key(pid: int, endpoint: bytes, hash_key=None):
     b = np.frombuffer(endpoint, np.uint8) if endpoint else np.zeros(1, np.uint8)
     key = np.zeros(2, np.uint64)
-    _check(lib().ebd_host_endpoint_key(pid, _p(b), len(endpoint), _p(key)), "ebd_host_endpoint_key")
+    hk = _hkey(hash_key)
+    _check(lib().ebd_host_endpoint_key(_p(hk), pid, _p(b), len(endpoint), _p(key)), "ebd_host_endpoint_key")
     return int(key[0]), int(key[1])
 
 

@@ -170,6 +170,10 @@ typedef struct ebd_config {
 	uint64_t string_arena;     /* bytes for service endpoint strings (0 = default 256 MiB) */
 	uint32_t lru_capacity;     /* 0 = EBD_MAX_SESSIONS (Discovery.cpp:39) */
 	uint32_t flags;            /* EBD_CFG_* */
+	/* Secret key of the 128-bit service-key PRF (SipHash-1-3-128 over pid + endpoint bytes).
+	 * {0, 0} = draw one from getrandom().  Contexts whose tables are merged (shards of one
+	 * trace on several GPUs) must share it: read it back with ebd_get_hash_key. */
+	uint64_t hash_key[2];
 } ebd_config;
 
 #define EBD_CFG_TIMING 2u /* time every kernel launch with HIP events (ebd_kernel_times) */
@@ -193,6 +197,8 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out);
 int ebd_ctx_destroy(ebd_ctx* ctx);
 /* The context's HIP stream (hipStream_t), for callers that time or order work. */
 void* ebd_ctx_stream(ebd_ctx* ctx);
+/* The context's service-key PRF key (ebd_config.hash_key as used). */
+int ebd_get_hash_key(ebd_ctx* ctx, uint64_t out[2]);
 
 /* IpAddressCheckerImpl's interface list (InterfacesReader::collectAllIpInterfaces,
  * InterfacesReader.cpp:50-78) — injected, because it is host dependent. */
@@ -237,6 +243,8 @@ int ebd_collect_services(ebd_ctx* ctx, ebd_service* out, uint32_t cap, uint32_t*
 int ebd_clear(ebd_ctx* ctx);
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
+/* Hash of the sources this library was built from (profiles/ name the build they measured). */
+const char* ebd_build_id(void);
 
 /* --- synthetic traces, identical on host and device ---------- */
 typedef struct ebd_trace_config {

@@ -18,10 +18,11 @@ extern "C" {
 /* DFA layout: nstates, url_id, g2, g3, g4, hvc0, hvh, fin0, fin1, inv, init. */
 int ebd_host_dfa_info(uint32_t* info, uint32_t n);
 
-/* The fast path (k_fresh's per-event logic) for one buffer. */
+/* The fast path (k_fresh's per-event logic) for one buffer; key = its service key under
+ * hash_key (ebd_config.hash_key). */
 int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags, const uint8_t* src16,
-		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, ebd_event_result* out,
-		uint64_t key[2]);
+		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, const uint64_t hash_key[2],
+		ebd_event_result* out, uint64_t key[2]);
 
 /* The generic parser (k_walk's parser) over consecutive chunks of one stream
  * (HttpRequestParser::parse per chunk).  out8[12] = state, url_start, url_len,
@@ -34,9 +35,9 @@ int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t n
 int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t flags, const ebd_ipv4_network* v4,
 		uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6);
 
-/* Service key of (pid, endpoint) in its streaming form (the session path's): key[0] = lo,
- * key[1] = hi.  The fast path computes the same key in 16-byte blocks. */
-int ebd_host_endpoint_key(uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]);
+/* Service key of (pid, endpoint) under hash_key in its streaming form (the session path's):
+ * key[0] = lo, key[1] = hi.  The fast path computes the same key word by word from spans. */
+int ebd_host_endpoint_key(const uint64_t hash_key[2], uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]);
 
 /* inet_pton restatement used on the device: 1 = parsed. */
 int ebd_host_pton(int af6, const uint8_t* text, uint32_t len, uint8_t* out);

@@ -79,10 +79,36 @@ def test_reference_parser_vectors_as_sessions(vectors):
 
 
 def test_reference_parser_vectors_interleaved_and_closed(vectors):
-    cases = vectors["parser_valid"] + vectors["parser_invalid"] + vectors["probe_parser"][:9]
-    chunk_lists = [[b(c) for c in case["chunks"]] for case in cases]
+    cases = vectors["parser_valid"] + vectors["parser_invalid"] + vectors["probe_parser"]
+    chunk_lists = [T.probe_chunks(case) for case in cases]
     ev, lens, offs, payload = T.session_trace(chunk_lists, interleave=True, close=True)
     assert_parity(ev, lens, offs, payload)
+
+
+def test_request_length_cap_on_gpu(vectors):
+    """HttpRequestParser.cpp:88-91: before each byte, length > 8192 makes the parser INVALID
+    without consuming it, so an 8193-byte request finishes and an 8194-byte one is INVALID
+    after 8193 bytes.  The probes run through the session path (k_walk), in one batch and
+    split across batches (the request's bytes carried between polls)."""
+    probes = [c for c in vectors["probe_parser"] if "lengths" in c]
+    assert len(probes) == 2
+    chunk_lists = [T.probe_chunks(c) for c in probes]
+    expect = [(c["state"], c["total"]) for c in probes]
+    for lengths in ([4096, 4097], [1, 8192], [8000, 150, 43], [8192, 2], [4000, 4000, 195], [8192, 808],
+                    [3000, 3000, 3000], [8192, 1, 1]):
+        chunk_lists.append(T.length_request_chunks(lengths))
+        total = sum(lengths)
+        expect.append(("FINISHED" if total <= 8193 else "INVALID", min(total, 8193)))
+    ev, lens, offs, payload = T.session_trace(chunk_lists)
+    for batches in (1, 2, 5):
+        gv, _ = assert_parity(ev, lens, offs, payload, batches=batches)
+        k = 0
+        for chunks, (state, total) in zip(chunk_lists, expect):
+            views = gv[k:k + len(chunks)]
+            k += len(chunks)
+            assert sum(v[1] for v in views) == total, (chunks and len(chunks), total)
+            last = [v for v in views if v[0] in (ebd.STATUS_FINISHED, ebd.STATUS_INVALID)]
+            assert last and last[-1][0] == (ebd.STATUS_FINISHED if state == "FINISHED" else ebd.STATUS_INVALID)
 
 
 def test_aggregator_vectors_real_checker(vectors):
@@ -189,7 +215,7 @@ def test_sharded_contexts_merge_to_whole_trace():
     for ev, lens, offs, payload in (ebd.generate_host(3, 21, 0, 30000), T.fragmented_trace(400, seed=23, window=64)):
         tables = []
         for idx in shard.shard_indices(ev, 3):
-            ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size)
+            ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size, hash_key=ebd.TEST_HASH_KEY)
             ctx.submit(ev[idx], lens[idx], offs[idx], payload)
             assert ctx.stats()["errors"] == 0
             tables.append(shard.ServiceTable.from_context(ctx, global_index=idx))

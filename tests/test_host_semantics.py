@@ -169,6 +169,80 @@ def test_fresh_key_is_streaming_key_of_endpoint():
     assert ebd.host_endpoint_key(7, b"") != ebd.host_endpoint_key(7, b"\0")
 
 
+M64 = (1 << 64) - 1
+
+
+def _rotl(x, r):
+    return ((x << r) | (x >> (64 - r))) & M64
+
+
+def _sipround(v):
+    v0, v1, v2, v3 = v
+    v0 = (v0 + v1) & M64; v1 = _rotl(v1, 13); v1 ^= v0; v0 = _rotl(v0, 32)
+    v2 = (v2 + v3) & M64; v3 = _rotl(v3, 16); v3 ^= v2
+    v0 = (v0 + v3) & M64; v3 = _rotl(v3, 21); v3 ^= v0
+    v2 = (v2 + v1) & M64; v1 = _rotl(v1, 17); v1 ^= v2; v2 = _rotl(v2, 32)
+    return [v0, v1, v2, v3]
+
+
+def _siphash(k0, k1, words, c, d, out128):
+    """SipHash-c-d (Aumasson & Bernstein 2012) over 64-bit message words; the 128-bit output
+    variant when out128 (v1 ^= 0xee at init, v2 ^= 0xee, then v1 ^= 0xdd for the 2nd half)."""
+    v = [k0 ^ 0x736F6D6570736575, k1 ^ 0x646F72616E646F6D, k0 ^ 0x6C7967656E657261, k1 ^ 0x7465646279746573]
+    if out128:
+        v[1] ^= 0xEE
+    for m in words:
+        v[3] ^= m
+        for _ in range(c):
+            v = _sipround(v)
+        v[0] ^= m
+    v[2] ^= 0xEE if out128 else 0xFF
+    for _ in range(d):
+        v = _sipround(v)
+    lo = v[0] ^ v[1] ^ v[2] ^ v[3]
+    if not out128:
+        return lo
+    v[1] ^= 0xDD
+    for _ in range(d):
+        v = _sipround(v)
+    return lo, v[0] ^ v[1] ^ v[2] ^ v[3]
+
+
+def test_siphash_rounds_pinned_by_published_vector():
+    """The round function above is pinned by the SipHash paper's test vector (SipHash-2-4,
+    key 00..0f, message 00..0e -> a129ca6149be45e5)."""
+    msg = bytes(range(15))
+    words = [int.from_bytes(msg[0:8], "little"), int.from_bytes(msg[8:15], "little") | (15 << 56)]
+    k0, k1 = int.from_bytes(bytes(range(8)), "little"), int.from_bytes(bytes(range(8, 16)), "little")
+    assert _siphash(k0, k1, words, 2, 4, False) == 0xA129CA6149BE45E5
+
+
+def test_service_key_is_siphash13_128_of_pid_and_endpoint():
+    """ebd_spec.h KeyHasher = SipHash-1-3-128 over [pid, E as zero-padded LE words, 0xe5<<56|len],
+    with the low bit of each half forced to 1 (0 marks an empty table slot)."""
+    rng = random.Random(5)
+    for t in range(300):
+        hk = (rng.getrandbits(64), rng.getrandbits(64)) if t % 3 else ebd.TEST_HASH_KEY
+        pid = rng.getrandbits(32)
+        ep = bytes(rng.randrange(0x21, 0x7F) for _ in range(rng.randrange(0, 90)))
+        words = [pid] + [int.from_bytes(ep[o:o + 8], "little") for o in range(0, len(ep), 8)]
+        words.append((0xE5 << 56) | len(ep))
+        lo, hi = _siphash(hk[0], hk[1], words, 1, 3, True)
+        assert ebd.host_endpoint_key(pid, ep, hash_key=hk) == (lo | 1, hi | 1)
+
+
+def test_unkeyed_hash_collision_pair_is_separated():
+    """two (pid, endpoint) pairs that collided under the round-1 unkeyed wymix
+    hash.  Under the keyed PRF they get different keys (under any key we try)."""
+    a = (1234, b"/3;9mw7wYuiP611jT,M,4AWTVmL_U37J/api/v1/users")
+    b = (99999, b"/[~pQ5)Faj9%d2.%rIb]]?-iOPR2'u%9/api/v1/users")
+    rng = random.Random(9)
+    for hk in [ebd.TEST_HASH_KEY] + [(rng.getrandbits(64), rng.getrandbits(64)) for _ in range(20)]:
+        assert ebd.host_endpoint_key(*a, hash_key=hk) != ebd.host_endpoint_key(*b, hash_key=hk)
+    # keys depend on the secret
+    assert ebd.host_endpoint_key(*a, hash_key=(1, 2)) != ebd.host_endpoint_key(*a, hash_key=(1, 3))
+
+
 def test_fresh_random_mutations():
     rng = random.Random(11)
     base = [b"GET /p/q?x=1 HTTP/1.1\r\nHost: svc.example.com:80\r\nX-Forwarded-For: 8.8.8.8:9, 10.0.0.1\r\n"

@@ -130,6 +130,27 @@ def fragmented_trace(n_conn, seed=4, window=512, max_req=8, kmin=2, kmax=4):
     return events(rows), lens, offs, payload
 
 
+def probe_chunks(case):
+    """Chunks of a parser probe vector: the literal chunks, or for the length-cap probes
+    ("lengths") a GET request of sum(lengths) bytes cut at those lengths."""
+    if "lengths" in case:
+        return length_request_chunks(case["lengths"])
+    return [c.encode("latin-1") for c in case["chunks"]]
+
+
+def length_request_chunks(lengths):
+    """A GET request of exactly sum(lengths) bytes (a long URL), cut into recv() pieces of
+    the given lengths (each <= 8192, the saved-buffer limit)."""
+    total = sum(lengths)
+    req = b"GET /" + b"a" * (total - 5 - 13) + b" HTTP/1.1\r\n\r\n"
+    assert len(req) == total
+    out, at = [], 0
+    for n in lengths:
+        out.append(req[at:at + n])
+        at += n
+    return out
+
+
 def oracle_view(out, blob):
     """Per-event comparable tuples from the oracle."""
     res = []

@@ -36,9 +36,10 @@ def main():
     ap.add_argument("--kernel", default="k_fresh")
     ap.add_argument("--out", required=True)
     ap.add_argument("--fetch-scale", type=float, default=1.0)
+    ap.add_argument("--build-id", required=True, help="ebd.build_id() of the library the passes measured")
     a = ap.parse_args()
     fkib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
-    out = {"kernel": a.kernel, "events": a.events, "config": a.config, "dispatches": nf,
+    out = {"kernel": a.kernel, "events": a.events, "config": a.config, "build_id": a.build_id, "dispatches": nf,
            "fetch_size_kib_per_launch": fkib, "fetch_scale": a.fetch_scale,
            "hbm_read_bytes_per_launch": fkib * 1024 * a.fetch_scale}
     total = out["hbm_read_bytes_per_launch"]
