@@ -21,12 +21,11 @@ hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
-hipError_t launch_reps(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
-hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out,
-		hipStream_t st, int cus);
+hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
+		ebd_service* out, hipStream_t st, int cus);
 hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
 		unsigned long long* alen, hipStream_t st);
@@ -429,7 +428,6 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 			HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
 	}
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
-	HIP_TRY(timed(c, KT_REPS, [&] { return launch_reps(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
 	if (c->h_ctr[CTR_DIRTY])
 		HIP_TRY(timed(c, KT_SSET_CLEAR, [&] { return launch_sset_clear(d, c->stream, c->cus); }));
@@ -602,7 +600,7 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 	if (cnt) {
 		if (!c->d_collect)
 			HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-		HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_collect, c->stream, c->cus));
+		HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_sarena, c->d_collect, c->stream, c->cus));
 		HIP_TRY(hipMemcpyAsync(out, c->d_collect, cnt * sizeof(ebd_service), hipMemcpyDeviceToHost, c->stream));
 	}
 	if (used)

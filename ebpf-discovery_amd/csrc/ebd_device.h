@@ -11,17 +11,15 @@ namespace ebd {
 // Service table slot (64 B, one cache line half): the Aggregator's
 // unordered_map<pair<pid, endpoint>, Service> (Aggregator.h:29-37, Service.h:43-66).
 struct Slot {
-	unsigned long long tag;     // Hash128.lo of (pid, endpoint); 0 = empty; claimed by CAS
-	unsigned long long hi;      // Hash128.hi, published by the claimer
-	unsigned long long min_seq; // first-arrival request (global event order), atomicMin
-	unsigned long long ep_off;  // endpoint bytes in the string arena (set by the representative)
-	unsigned int pid;
+	unsigned long long tag;    // Hash128.lo of (pid, endpoint); 0 = empty; claimed by CAS
+	unsigned long long hi;     // Hash128.hi, published by the claimer
+	unsigned long long first;  // min over requests of seq << 16 | isHttps << 15 | host length (atomicMin)
+	unsigned long long ep_off; // endpoint bytes in the string arena (claimer)
+	unsigned int pid;          // (claimer, one 8-byte store with ep_len)
+	unsigned int ep_len;
 	unsigned int internal_clients; // uint32, wraps like Service.h:53-54
 	unsigned int external_clients;
-	unsigned int ep_len;
-	unsigned int dom;  // domain offset | length << 16, within the endpoint
-	unsigned int info; // bit0 https, bit1 representative written
-	unsigned int pad[2];
+	unsigned int pad[4];
 };
 static_assert(sizeof(Slot) == 64, "slot is 64 bytes");
 

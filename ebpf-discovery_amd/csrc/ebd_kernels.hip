@@ -31,6 +31,15 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
 __device__ __forceinline__ unsigned long long rmw_read(unsigned long long* p) { return atomicCAS(p, ~0ull, ~0ull); }
 __device__ __forceinline__ unsigned int rmw_read(unsigned int* p) { return atomicCAS(p, 0xffffffffu, 0xffffffffu); }
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef v4u v4u_a1 __attribute__((aligned(1)));
+typedef unsigned long long u64a1 __attribute__((aligned(1)));
+typedef unsigned int u32a1 __attribute__((aligned(1)));
+// 8 bytes at any alignment: global_load_dwordx2 (gfx950 runs in unaligned-access mode)
+__device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
+	return *(const __attribute__((address_space(1))) u64a1*)a;
+}
+
 // ---------------------------------------------------------------------------------
 // Service table: open addressing on the 64-bit tag, 128-bit key verified.
 //
@@ -39,41 +48,43 @@ __device__ __forceinline__ unsigned int rmw_read(unsigned int* p) { return atomi
 // A claimer CASes the tag and stores the second half; a finder compares the second half
 // when it is already visible and otherwise queues (slot, hi) for k_verify, which runs
 // after the inserting kernel.  A mismatch there is reported as EBD_ERR_COLLISION.
+//
+// First arrival (Aggregator.cpp:155-168: the request that creates a key fixes its domain
+// and scheme): every request offers first = seq << 16 | isHttps << 15 | host length, and
+// the slot keeps the minimum (atomicMin), so the earliest request's scheme and host/url
+// split win.  The endpoint bytes are the same for every request of a key, so the claimer
+// stores them (claim_publish) whoever arrives first.
 // ---------------------------------------------------------------------------------
-__device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, uint32_t cls) {
+EBD_HD unsigned long long first_word(unsigned long long seq, bool https, uint32_t hl) {
+	return (seq << 16) | ((unsigned long long)(https ? 1u : 0u) << 15) | (hl & 0x7fffu);
+}
+
+// Returns the slot (kNone when the table is full); *claimed: this call created the service.
+__device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first, uint32_t cls, bool* claimed) {
 	uint32_t idx = (uint32_t)h.lo & d.slot_mask;
 	bool found = false;
-	unsigned long long seen_min = 0;
+	*claimed = false;
+	unsigned long long seen_first = 0;
 	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
 		Slot* s = d.slots + idx;
 		// One plain load pass over the slot's first 32 bytes.  tag and hi are written once
-		// (0 -> value), min_seq only decreases: a stale copy at worst shows 0 (resolved by
-		// the CAS below, or the coherent re-read of hi) or a larger min_seq (a redundant
+		// (0 -> value), first only decreases: a stale copy at worst shows 0 (resolved by
+		// the CAS below, or the coherent re-read of hi) or a larger first (a redundant
 		// atomicMin).  Slot words are only ever written by atomics here, so no dirty line
 		// sits in L2 when the next kernel starts.
 		const ulonglong2 th = *(const ulonglong2*)&s->tag;
-		const ulonglong2 mo = *(const ulonglong2*)&s->min_seq;
-		seen_min = mo.x;
+		const ulonglong2 mo = *(const ulonglong2*)&s->first;
+		seen_first = mo.x;
 		unsigned long long t = th.x;
-		bool claimed = false;
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, h.lo);
 			if (t == 0) {
 				atomicExch(&s->hi, h.hi);
-				// the claimed-slot list is cumulative over batches (k_reps, ebd_clear and
-				// ebd_collect_services walk it); CTR_SERVICES moves only in k_verify
-				const unsigned long long k = atomicAdd(&d.ctr[CTR_NEW], 1ull) + ld_relaxed(&d.ctr[CTR_SERVICES]);
-				if (k < d.new_cap)
-					d.new_slots[k] = idx;
-				else
-					set_error(d, EBD_ERR_TABLE_FULL);
-				claimed = true;
-				seen_min = ~0ull;
+				*claimed = true;
+				seen_first = ~0ull;
+				found = true;
+				break;
 			}
-		}
-		if (claimed) {
-			found = true;
-			break;
 		}
 		if (t == h.lo) {
 			unsigned long long hi = th.y;
@@ -100,18 +111,50 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long seq, 
 	}
 	if (!found) {
 		set_error(d, EBD_ERR_TABLE_FULL);
-		return 0xffffffffu;
+		return kNone;
 	}
 	Slot* s = d.slots + idx;
-#ifndef EBD_EXP_AGG_NOATOMIC // experiment: no counter atomics (counts are wrong)
 	if (cls == CLS_INTERNAL)
 		atomicAdd(&s->internal_clients, 1u);
 	else if (cls == CLS_EXTERNAL)
 		atomicAdd(&s->external_clients, 1u);
-#endif
-	if (seq < seen_min)
-		atomicMin(&s->min_seq, seq);
+	if (first < seen_first)
+		atomicMin(&s->first, first);
 	return idx;
+}
+
+// Endpoint E = host + url as 8-byte words (ebd_spec.h endpoint_piece) to an 8-byte aligned
+// destination: unaligned 8-byte loads (gfx950 runs in unaligned mode; sources are readable
+// 8 bytes past their end), aligned stores.
+__device__ __forceinline__ void copy_endpoint(unsigned long long* dst, const uint8_t* host, uint32_t hl, const uint8_t* url,
+		uint32_t ul) {
+	const uint32_t n = hl + ul;
+	for (uint32_t oo = 0; oo < n; oo += 8) {
+		const unsigned long long A = gload8u(host + (oo < hl ? oo : 0));
+		const unsigned long long B = gload8u(url + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
+		dst[oo >> 3] = endpoint_piece(hl, n, oo, A, B);
+	}
+}
+
+// The claimer of slot idx publishes the service's list entry, pid and endpoint bytes.
+// list_at: its position in the claimed-slot list; ep_at: its (8-aligned) arena offset.
+__device__ void claim_publish(const Dev& d, uint32_t idx, unsigned long long list_at, unsigned long long ep_at, uint32_t pid,
+		const uint8_t* host, uint32_t hl, const uint8_t* url, uint32_t ul) {
+	Slot* s = d.slots + idx;
+	if (list_at < d.new_cap)
+		d.new_slots[list_at] = idx;
+	else
+		set_error(d, EBD_ERR_TABLE_FULL);
+	const uint32_t n = hl + ul;
+	unsigned long long off = ~0ull;
+	if (ep_at + n <= d.sarena_cap) {
+		copy_endpoint((unsigned long long*)(d.sarena + ep_at), host, hl, url, ul);
+		off = ep_at;
+	} else {
+		set_error(d, EBD_ERR_ARENA_FULL);
+	}
+	atomicExch(&s->ep_off, off);
+	atomicExch((unsigned long long*)&s->pid, (unsigned long long)pid | ((unsigned long long)n << 32)); // pid, ep_len
 }
 
 // ---------------------------------------------------------------------------------
@@ -210,10 +253,6 @@ struct Chunk {
 	uint32_t w[4];
 };
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-typedef v4u v4u_a1 __attribute__((aligned(1)));
-typedef unsigned long long u64a1 __attribute__((aligned(1)));
-typedef unsigned int u32a1 __attribute__((aligned(1)));
 // 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
 __device__ __forceinline__ Chunk gload16(uintptr_t a) {
 	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
@@ -223,10 +262,6 @@ __device__ __forceinline__ Chunk gload16(uintptr_t a) {
 	c.w[2] = v.z;
 	c.w[3] = v.w;
 	return c;
-}
-// 8 bytes at any alignment: global_load_dwordx2 (gfx950 runs in unaligned-access mode)
-__device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
-	return *(const __attribute__((address_space(1))) u64a1*)a;
 }
 
 // Buffer access for fresh_finalize on the device: 4 and 8 bytes at any buffer offset.  Every
@@ -1035,7 +1070,11 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	}
 	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
 	kh.bytes(dst, hl + ul);
-	agg_insert(d, kh.finish(), d.seq_base + i, cls);
+	bool claimed;
+	const uint32_t slot = agg_insert(d, kh.finish(), first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl), cls, &claimed);
+	if (claimed) // a rare path: one reservation per claim
+		claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
+				atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
 	atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
 	const unsigned long long q = atomicAdd(&d.ctr[CTR_SREQ], 1ull);
 	SessReq sr;
@@ -1190,33 +1229,64 @@ __global__ void k_carry_pass(Dev d) {
 // with a client-IP header (~30 % in config 3) are queued in LDS and parsed kAggThreads at a
 // time, so the token parse, the longest code path, runs on full waves instead of on the
 // few lanes of each wave that have one.  Aggregation is order-free (counters, atomicMin of
-// the first-arrival sequence), so queueing does not change the result.  Requests are counted
-// per block: one global atomic each.
+// the first-arrival word), so queueing does not change the result.  Services created in a
+// step reserve their list entries and arena bytes with one global atomic per block and step
+// (a single hot counter serialises at ~12 ns per atomic); requests are counted per block.
 constexpr uint32_t kCipQueue = 2 * kAggThreads;
 
-__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row) {
+// A service this thread created in the current step, waiting for its reservations.
+struct PendingClaim {
+	uint32_t slot, pid, hl, ul, li;
+	unsigned long long ab;
+	const uint8_t *host, *url;
+};
+
+struct AggShared {
+	uint32_t q[kCipQueue]; // queued client-IP requests
+	uint32_t qn;
+	uint32_t cn;           // claims of this step (list entries)
+	unsigned long long cb; // their arena bytes
+	unsigned long long list_base, arena_base;
+	unsigned long long nreq;
+};
+
+__device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
+		PendingClaim& pc, bool& has) {
+	bool claimed;
+	const Hash128 key = d.keys[i];
+	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len), cls,
+			&claimed);
+	if (claimed) {
+		const uint8_t* p = d.payload + d.off[i];
+		pc.slot = slot;
+		pc.pid = d.ev[i].pid;
+		pc.host = p + r.u.span.host_off;
+		pc.hl = r.u.span.host_len;
+		pc.url = p + r.u.span.url_off;
+		pc.ul = r.u.span.url_len;
+		pc.li = atomicAdd(&sh.cn, 1u);
+		pc.ab = atomicAdd(&sh.cb, (unsigned long long)((pc.hl + pc.ul + 7u) & ~7u));
+		has = true;
+	}
+}
+
+__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh, PendingClaim& pc, bool& has) {
 	ebd_event_result r = d.res[i];
-#ifdef EBD_EXP_NOCIP // experiment: no client-IP token parse (classes are wrong)
-	const uint32_t cls = CLS_NONE;
-#else
 	const uint32_t cls = cip_classify(d, i, r, row);
-#endif
 	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 	d.res[i] = r;
-#ifndef EBD_EXP_AGG_NOPROBE // experiment: no service table access (results are wrong)
-	agg_insert(d, d.keys[i], d.seq_base + i, cls);
-#endif
+	agg_request(d, i, r, cls, sh, pc, has);
 }
 
 __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
-	__shared__ uint32_t q[kCipQueue]; // queued client-IP requests
-	__shared__ uint32_t qn;
-	__shared__ unsigned long long nreq;
+	__shared__ AggShared sh;
 	uint8_t* row = rows + threadIdx.x * kCipStride;
 	if (threadIdx.x == 0) {
-		nreq = 0;
-		qn = 0;
+		sh.nreq = 0;
+		sh.qn = 0;
+		sh.cn = 0;
+		sh.cb = 0;
 	}
 	__syncthreads();
 	uint32_t cnt = 0;
@@ -1224,13 +1294,15 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 	const uint32_t per = (steps + gridDim.x - 1) / gridDim.x;
 	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
 	for (uint32_t st = s0; st < s1; st++) { // uniform trip count: the barriers below are safe
+		PendingClaim pc[2];
+		bool has[2] = {false, false};
 		const uint32_t i = st * kAggThreads + threadIdx.x;
 		if (i < d.n) {
 			ebd_event_result r = d.res[i];
 			if (r.status == EBD_STATUS_FINISHED && !(r.info & EBD_INFO_SESSION)) {
 				cnt++;
 				if (r.info & EBD_INFO_CIP) {
-					q[atomicAdd(&qn, 1u)] = i;
+					sh.q[atomicAdd(&sh.qn, 1u)] = i;
 				} else {
 					const uint8_t* evb = (const uint8_t*)(d.ev + i);
 					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
@@ -1239,105 +1311,46 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 					const uint32_t cls = classify_source(*d.ifs, evb[32], src);
 					r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 					d.res[i] = r;
-#ifndef EBD_EXP_AGG_NOPROBE
-					agg_insert(d, d.keys[i], d.seq_base + i, cls);
-#endif
+					agg_request(d, i, r, cls, sh, pc[0], has[0]);
 				}
 			}
 		}
 		__syncthreads();
-		const uint32_t m = qn; // < kCipQueue: below kAggThreads before this step, + at most kAggThreads
-		__syncthreads();       // every thread has read qn before a push or the drain changes it
-		if (m >= kAggThreads) {
-			agg_cip_one(d, q[threadIdx.x], row);
+		const uint32_t m = sh.qn; // < kCipQueue: below kAggThreads before this step, + at most kAggThreads
+		__syncthreads();          // every thread has read qn before a push or the drain changes it
+		const bool last = st + 1 == s1;
+		if (m >= kAggThreads || (last && m > 0)) { // full waves; the block's last step drains the rest
+			if (threadIdx.x < min(m, (uint32_t)kAggThreads))
+				agg_cip_one(d, sh.q[threadIdx.x], row, sh, pc[1], has[1]);
 			__syncthreads();
-			if (threadIdx.x < m - kAggThreads) // [kAggThreads, m) -> [0, m - kAggThreads): disjoint
-				q[threadIdx.x] = q[kAggThreads + threadIdx.x];
+			if (m >= kAggThreads && threadIdx.x < m - kAggThreads) // [kAggThreads, m) -> [0, m - kAggThreads)
+				sh.q[threadIdx.x] = sh.q[kAggThreads + threadIdx.x];
 			if (threadIdx.x == 0)
-				qn = m - kAggThreads;
-			__syncthreads();
+				sh.qn = m >= kAggThreads ? m - kAggThreads : 0;
 		}
-	}
-	__syncthreads();
-	if (threadIdx.x < qn)
-		agg_cip_one(d, q[threadIdx.x], row);
-	atomicAdd(&nreq, (unsigned long long)cnt);
-	__syncthreads();
-	if (threadIdx.x == 0 && nreq)
-		atomicAdd(&d.ctr[CTR_REQUESTS], nreq);
-}
-
-// First-arrival representative of every service created in this batch (Aggregator.cpp:
-// 112-130, 160-167): endpoint string, domain, scheme, pid.  The endpoint E = host + url is
-// copied as 8-byte words (unaligned loads from the buffer, aligned stores to an 8-byte
-// aligned arena offset), and the domain (A:117-125) is found on the words in registers.
-__global__ void k_reps(Dev d) {
-	const unsigned long long nn = d.ctr[CTR_NEW];
-	const unsigned long long base = d.ctr[CTR_SERVICES];
-	const unsigned long long end = min(base + nn, (unsigned long long)d.new_cap);
-	for (unsigned long long k = base + blockIdx.x * blockDim.x + threadIdx.x; k < end; k += gridDim.x * blockDim.x) {
-		Slot* s = d.slots + d.new_slots[k];
-		const unsigned long long seq = s->min_seq;
-		const uint32_t e = (uint32_t)(seq - d.seq_base);
-		const ebd_event_result r = d.res[e];
-		const uint8_t *host, *url;
-		uint32_t hl, ul;
-		if (r.info & EBD_INFO_SESSION) {
-			const SessReq& q = d.sreq[r.u.session.index];
-			host = d.sstr + q.str_off;
-			hl = q.host_len;
-			url = host + hl;
-			ul = q.url_len;
-		} else {
-			const uint8_t* p = d.payload + d.off[e];
-			host = p + r.u.span.host_off;
-			hl = r.u.span.host_len;
-			url = p + r.u.span.url_off;
-			ul = r.u.span.url_len;
-		}
-		const uint32_t n = hl + ul;
-		const unsigned long long at = atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((n + 7u) & ~7u));
-		s->pid = d.ev[e].pid;
-		s->ep_len = n;
-		s->info = ((r.info & EBD_INFO_HTTPS) ? 1u : 0u) | 2u;
-		const bool fits = at + n <= d.sarena_cap;
-		if (!fits) {
-			set_error(d, EBD_ERR_ARENA_FULL);
-			s->ep_off = ~0ull;
-		} else {
-			s->ep_off = at;
-		}
-		unsigned long long* dst = (unsigned long long*)(d.sarena + at);
-		uint32_t lb = kNone, rb = kNone, colon = kNone;
-		for (uint32_t oo = 0; oo < n; oo += 8) {
-			const unsigned long long A = gload8u(host + (oo < hl ? oo : 0));
-			const unsigned long long B = gload8u(url + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
-			const unsigned long long w = endpoint_piece(hl, n, oo, A, B);
-			if (fits)
-				dst[oo >> 3] = w;
-			if (oo < hl && (lb == kNone || rb == kNone || colon == kNone)) { // host bytes of this word
-				const uint32_t m = min(8u, hl - oo);
-				for (uint32_t b = 0; b < m; b++) {
-					const uint32_t c = (uint32_t)(w >> (8 * b)) & 0xffu;
-					if (c == '[' && lb == kNone)
-						lb = oo + b;
-					else if (c == ']' && lb != kNone && rb == kNone)
-						rb = oo + b;
-					if (c == ':' && colon == kNone)
-						colon = oo + b;
-				}
+		__syncthreads();
+		// this step's claims: one reservation of list entries and arena bytes for the block
+		if (threadIdx.x == 0) {
+			const uint32_t cn = sh.cn;
+			if (cn) {
+				sh.list_base = atomicAdd(&d.ctr[CTR_SERVICES], (unsigned long long)cn);
+				sh.arena_base = atomicAdd(&d.ctr[CTR_SARENA], sh.cb);
 			}
+			sh.cn = 0;
+			sh.cb = 0;
 		}
-		uint32_t doff, dlen;
-		if (lb != kNone) {
-			doff = rb != kNone ? lb : 0;
-			dlen = rb != kNone ? rb - lb + 1 : 0;
-		} else {
-			doff = 0;
-			dlen = colon != kNone ? colon : hl;
-		}
-		s->dom = doff | (dlen << 16);
+		__syncthreads();
+#pragma unroll
+		for (int k = 0; k < 2; k++)
+			if (has[k])
+				claim_publish(d, pc[k].slot, sh.list_base + pc[k].li, sh.arena_base + pc[k].ab, pc[k].pid, pc[k].host, pc[k].hl,
+						pc[k].url, pc[k].ul);
+		__syncthreads(); // list_base / arena_base are read before the next step's reservation
 	}
+	atomicAdd(&sh.nreq, (unsigned long long)cnt);
+	__syncthreads();
+	if (threadIdx.x == 0 && sh.nreq)
+		atomicAdd(&d.ctr[CTR_REQUESTS], sh.nreq);
 }
 
 __global__ void k_verify(Dev d) {
@@ -1346,30 +1359,27 @@ __global__ void k_verify(Dev d) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
 		if (d.slots[d.verify[k].slot].hi != d.verify[k].hi)
 			set_error(d, EBD_ERR_COLLISION);
-	if (blockIdx.x == 0 && threadIdx.x == 0) { // this batch's claims join the service count (after k_reps)
-		const unsigned long long nn = d.ctr[CTR_NEW], base = d.ctr[CTR_SERVICES];
-		d.ctr[CTR_SERVICES] = min(base + nn, (unsigned long long)d.new_cap);
-	}
+}
+
+__device__ __forceinline__ Slot empty_slot() {
+	Slot s;
+	s.tag = 0;
+	s.hi = 0;
+	s.first = ~0ull;
+	s.ep_off = 0;
+	s.pid = 0;
+	s.ep_len = 0;
+	s.internal_clients = 0;
+	s.external_clients = 0;
+	s.pad[0] = s.pad[1] = s.pad[2] = s.pad[3] = 0;
+	return s;
 }
 
 // Aggregator::clear (Aggregator.cpp:136-153): every claimed slot back to empty.
 __global__ void k_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots) {
 	const unsigned long long n = ctr[CTR_SERVICES];
-	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		Slot s;
-		s.tag = 0;
-		s.hi = 0;
-		s.min_seq = ~0ull;
-		s.ep_off = 0;
-		s.pid = 0;
-		s.internal_clients = 0;
-		s.external_clients = 0;
-		s.ep_len = 0;
-		s.dom = 0;
-		s.info = 0;
-		s.pad[0] = s.pad[1] = 0;
-		slots[used[k]] = s;
-	}
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+		slots[used[k]] = empty_slot();
 }
 
 __global__ void k_sset_clear(Dev d) {
@@ -1386,40 +1396,35 @@ __global__ void k_sset_clear(Dev d) {
 }
 
 __global__ void k_slots_init(Slot* slots, uint32_t n) {
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		Slot s;
-		s.tag = 0;
-		s.hi = 0;
-		s.min_seq = ~0ull;
-		s.ep_off = 0;
-		s.pid = 0;
-		s.internal_clients = 0;
-		s.external_clients = 0;
-		s.ep_len = 0;
-		s.dom = 0;
-		s.info = 0;
-		s.pad[0] = s.pad[1] = 0;
-		slots[k] = s;
-	}
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+		slots[k] = empty_slot();
 }
 
-// Aggregator::collectServices (Aggregator.cpp:170-181) over the claimed-slot list.
-__global__ void k_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out) {
+// Aggregator::collectServices (Aggregator.cpp:170-181) over the claimed-slot list.  Domain
+// and scheme come from the first-arrival word (the earliest request's host length and
+// isHttps, Aggregator.cpp:112-130): the domain is "[...]" through the first ']' after the
+// host's first '[' (empty without one), else the host up to its first ':'.
+__global__ void k_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
+		ebd_service* out) {
 	const unsigned long long n = ctr[CTR_SERVICES];
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
 		const Slot& s = slots[used[k]];
+		const uint32_t hl = (uint32_t)(s.first & 0x7fffu);
+		uint32_t doff = 0, dlen = 0;
+		if (s.ep_off != ~0ull)
+			host_domain(arena + s.ep_off, hl, &doff, &dlen);
 		ebd_service v;
 		v.pid = s.pid;
 		v.internal_clients = s.internal_clients;
 		v.external_clients = s.external_clients;
-		v.https = (uint8_t)(s.info & 1u);
+		v.https = (uint8_t)((s.first >> 15) & 1u);
 		v.pad_[0] = v.pad_[1] = v.pad_[2] = 0;
 		v.endpoint_off = s.ep_off;
 		v.endpoint_len = s.ep_len;
-		v.domain_off = s.dom & 0xffffu;
-		v.domain_len = s.dom >> 16;
+		v.domain_off = doff;
+		v.domain_len = dlen;
 		v.pad2_ = 0;
-		v.first_seq = s.min_seq;
+		v.first_seq = s.first >> 16;
 		v.key_lo = s.tag;
 		v.key_hi = s.hi;
 		out[k] = v;
@@ -1482,10 +1487,6 @@ hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_agg_fast, dim3(grid_for(d.n, kAggThreads, cus * 8)), dim3(kAggThreads), 0, st, d);
 	return hipGetLastError();
 }
-hipError_t launch_reps(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_reps, dim3(cus * 16), dim3(256), 0, st, d);
-	return hipGetLastError();
-}
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_verify, dim3(cus), dim3(256), 0, st, d);
 	return hipGetLastError();
@@ -1498,9 +1499,9 @@ hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(k_slots_init, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n);
 	return hipGetLastError();
 }
-hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, ebd_service* out,
-		hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, slots, used, ctr, out);
+hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
+		ebd_service* out, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, slots, used, ctr, arena, out);
 	return hipGetLastError();
 }
 hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus) {

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--events", type=int, default=20_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--cold", action="store_true", help="ebd_clear before every submit (services created each time)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -41,6 +42,8 @@ def main():
     ctx.reset_kernel_times()
     t = time.perf_counter()
     for k in range(args.reps):
+        if args.cold:
+            ctx.clear()
         ctx.set_seq_base((k + 1) * E)
         ctx.submit_device(ev, ln, of, pay, E)
     ctx.sync()
@@ -49,7 +52,7 @@ def main():
     res = ctx.results()
     alg = int(res["consumed"].astype(np.uint64).sum()) + 40 * int((res["status"] != 0).sum())
     fr = kt["k_fresh"][1] / max(kt["k_fresh"][0], 1)
-    print(json.dumps({"events": E, "step_ms": dt * 1e3, "events_per_s": E / dt,
+    print(json.dumps({"lib": os.path.basename(ebd.LIB_PATH), "cold": args.cold, "events": E, "step_ms": dt * 1e3, "events_per_s": E / dt,
                       "k_fresh_ms": fr, "k_fresh_alg_gbps": alg / fr / 1e6,
                       "kernel_ms": {k: v[1] / v[0] for k, v in kt.items() if v[0]},
                       "errors": ctx.stats()["error_names"]}))
