@@ -3,28 +3,38 @@
 
 A step = one poll cycle of the hot path (Discovery::fetchAndHandleEvents -> per-buffer
 HttpRequestParser::parse -> Aggregator::newRequest) over one batch of captured events
-already resident in HBM.  Default workload: SURVEY.md 8(d) config 3 — 100 M mixed
-32-1024 B GET/POST requests (mean ~252 B), Zipf endpoints, client-IP headers, ~1 %
-invalid bytes, generated in HBM from Philox (identical to the host generator).
+already resident in HBM.  Workloads, generated in HBM from Philox
+(bit-identical to the host generator):
+  N = 1: config 3 - 100 M mixed 32-1024 B GET/POST requests, Zipf endpoints, client-IP
+         headers, ~1 % invalid bytes;
+  N > 1: config 5 - the config-3 distribution (seed 5), N x 125 M requests sharded by
+         hash(pid, fd, sessionID) across the GPUs (8 GPUs: the 1 B-request trace), one shard
+         per GPU, then the owner-partitioned service merge over RCCL (timed as merge_ms).
 
-  python bench.py                      # N=1, config 3, 5 timed steps
-  torchrun --nproc-per-node N bench.py --gpus N   # weak scaling, one shard per GPU
+  python bench.py                          # N=1, config 3
+  python bench.py --gpus 8                 # spawns 8 ranks (one process per GPU)
+  torchrun --nproc-per-node 8 bench.py --gpus 8
+  python bench.py --gpus 2 --dry-run-cpu   # the multi-rank flow on CPU (gloo, no GPU)
+
+Step modes: cold (default) = every step is one report interval: the service table is
+cleared (Aggregator::clear) before the batch, so every service of the batch is created
+inside the timed step; warm = the table keeps the services of earlier steps.  The other
+mode is measured and reported beside.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ebpf-discovery_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-import ebd  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 WORKLOADS = {
@@ -32,8 +42,11 @@ WORKLOADS = {
     2: "config2: fixed 64-B GET, single endpoint 10.0.0.1:8080/index.html",
     3: "config3: mixed 32-1024 B GET/POST (mean ~252 B), Zipf(1.1) URLs x 1e5 and hosts x 1e3, 64 pids, "
        "30% client-IP headers, ~1% invalid",
+    5: "config5: N x 125 M mixed-length requests (config-3 distribution, seed 5; 8 GPUs = the 1 B-request trace) "
+       "sharded by hash(pid, fd, sessionID) across N GPUs, owner-partitioned RCCL service merge",
 }
-DEFAULT_EVENTS = {1: 1_000_000, 2: 10_000_000, 3: 100_000_000}
+DEFAULT_EVENTS = {1: 1_000_000, 2: 10_000_000, 3: 100_000_000, 5: 125_000_000}
+GEN_CHUNK = 1 << 28  # candidate events per device generation call
 
 
 def parse_args():
@@ -41,18 +54,21 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--config", type=int, default=0, help="default: 3 at one GPU, 5 at several")
     ap.add_argument("--events", type=int, default=0, help="events per GPU (default: the config's size)")
     ap.add_argument("--seed", type=int, default=0, help="trace seed (default: the config number)")
     ap.add_argument("--service-capacity", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline budget (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per thread count (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("cold", "warm"), default="cold",
                     help="cold: every step is one report interval, the service table cleared before the batch "
                          "(every service of the batch is created inside the timed step); warm: the table keeps "
                          "the services of earlier steps (all hits after the first batch)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fetch_config3.json"),
-                    help="rocprofv3 FETCH_SIZE summary giving HBM traffic per k_fresh launch")
+                    help="rocprofv3 FETCH/WRITE_SIZE summary giving HBM traffic per k_fresh launch (matched by build id)")
+    ap.add_argument("--dry-run-cpu", action="store_true",
+                    help="no GPU: spawn the ranks over gloo, shard a small config-5 trace, replay each shard with the "
+                         "oracle (in place of a GPU context) and run the owner-partitioned merge")
     return ap.parse_args()
 
 
@@ -60,79 +76,173 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def stream_read_peak(dev):
-    """Measured HBM read bandwidth of a plain 4 GiB reduction (for context, not the roofline)."""
-    x = torch.ones(1 << 30, dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
-    best = 0.0
-    for _ in range(5):
-        t = time.perf_counter()
-        x.sum()
-        torch.cuda.synchronize()
-        best = max(best, x.numel() * 4 / (time.perf_counter() - t) / 1e9)
-    del x
+def spawn_ranks(n):
+    """One process per GPU, started before anything touches a GPU; exits with the worst code."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max((abs(c) for c in rcs), default=0)
+
+
+def copy_peak(dev):
+    """Measured HBM read+write rate of a 2 x 2 GiB device copy (HIP-event timed): context for
+    the 8 TB/s spec peak the roofline uses."""
+    import torch
+    x = torch.ones(1 << 29, dtype=torch.float32, device=dev)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        y.copy_(x)
+    b.record()
+    b.synchronize()
+    gbps = 10 * 2 * x.numel() * 4 / (a.elapsed_time(b) / 1e3) / 1e9
+    del x, y
     torch.cuda.empty_cache()
-    return best
+    return gbps
 
 
 def cpu_baseline(config, seed, budget_s):
-    """The oracle (C restatement of the reference path, 1 thread) on a bounded sample of
-    the same workload, regenerated on the host."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    """The oracle (C restatement of the reference path) on a bounded sample of the same
+    workload regenerated on the host, 1 thread (the reference's single consumer thread,
+    ServiceDetectionTask.cpp:43) and all host threads (connection-sharded)."""
     import oracle_py as O
-
+    import ebd
     o = O.Oracle()
-    chunk = 250_000 if config == 3 else 1_000_000
+    chunk = 250_000 if config in (3, 5) else 1_000_000
     done, spent, first = 0, 0.0, 0
+    gen = 3 if config == 5 else config
     while spent < budget_s:
-        ev, lens, offs, payload = ebd.generate_host(config, seed, first, chunk)
+        ev, lens, offs, payload = ebd.generate_host(gen, seed, first, chunk)
         t = time.perf_counter()
         o.process(ev, lens, offs, payload)
         spent += time.perf_counter() - t
         done += chunk
         first += chunk
-    return dict(value=done / spent, unit="events/s", cores=1, kind="port",
-                sample=f"first {done} events of the same config-{config} trace (seed {seed}) regenerated on the host, "
-                       f"oracle/ C restatement (Discovery+HttpRequestParser+Aggregator semantics), 1 thread, "
-                       f"{spent:.1f} s")
+    one = done / spent
+    out = dict(value=one, unit="events/s", cores=1, kind="port",
+               sample=f"first {done} events of the same config-{config} trace (seed {seed}) regenerated on the host, "
+                      f"oracle/ C restatement (Discovery+HttpRequestParser+Aggregator semantics), 1 thread, "
+                      f"{spent:.1f} s")
+    mt = O.parallel_throughput(gen, seed, budget_s)
+    if mt:
+        out["all_threads"] = mt
+    return out
+
+
+def dry_run_cpu(args):
+    """The multi-rank flow without a GPU (gloo): each rank generates its config-5 shard on
+    the host, replays it with the oracle (stand-in for its GPU context), keys its services
+    with the product's endpoint key and runs the owner-partitioned exchange + merge."""
+    import torch.distributed as dist
+    import ebd
+    import oracle_py as O
+    from ebd import shard
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    dist.init_process_group("gloo")
+    E = args.events or 20_000
+    ev, lens, offs, payload, gidx = ebd.generate_host(5, 5, 0, E * world, shard=(world, rank), with_gidx=True)
+    t = time.perf_counter()
+    o = O.Oracle()
+    o.process(ev, lens, offs, payload)
+    rows = [(p, ep, dom, sch, i, e, int(gidx[f])) for (p, ep, dom, sch, i, e, f) in o.services_first()]
+    table = shard.ServiceTable.from_rows(rows, [ebd.host_endpoint_key(r[0], r[1]) for r in rows])
+    el = time.perf_counter() - t
+    tm = time.perf_counter()
+    mine = shard.exchange_merge(table, device="cpu")
+    merge_ms = (time.perf_counter() - tm) * 1e3
+    counts = [None] * world
+    dist.all_gather_object(counts, (len(ev), mine.rec.size, el))
+    dist.destroy_process_group()
+    if rank == 0:
+        n_ev = sum(c[0] for c in counts)
+        print(json.dumps({"metric": "HTTP events parsed/s (CPU dry run: oracle stand-in, no GPU)", "dry_run": True,
+                          "value": n_ev / max(c[2] for c in counts), "unit": "events/s", "n_gpus": world,
+                          "steps": 1, "warmup": 0, "higher_is_better": True, "scaling": "weak",
+                          "events_per_rank": [c[0] for c in counts], "services_merged": sum(c[1] for c in counts),
+                          "merge_ms": merge_ms, "config": {"workload": WORKLOADS[5], "config": 5}}), flush=True)
+
+
+def generate_shard(ctx, cfg, seed, E, world, rank, dev):
+    """This rank's batch in HBM: config 5 = the events of candidates [0, world * E) whose
+    connection hashes to this rank (generated in chunks); otherwise candidates [0, E).
+    Returns (events, len, off, payload, gidx, n)."""
+    import torch
+    import ebd
+    shard_ = (world, rank) if cfg == 5 else (1, 0)
+    cand = E * world if cfg == 5 else E
+    plan, n_tot, b_tot = [], 0, 0
+    for c0 in range(0, cand, GEN_CHUNK):
+        cn = min(GEN_CHUNK, cand - c0)
+        k, b = ebd.trace_size_device(ctx, cfg, seed, c0, cn, align=16, shard=shard_, with_events=True)
+        plan.append((c0, cn, k, b, n_tot, b_tot))
+        n_tot += k
+        b_tot += b
+    ev_t = torch.empty(n_tot * 36, dtype=torch.uint8, device=dev)
+    len_t = torch.empty(n_tot, dtype=torch.int32, device=dev)
+    off_t = torch.empty(n_tot, dtype=torch.int64, device=dev)
+    gidx_t = torch.empty(n_tot, dtype=torch.int64, device=dev)
+    pay_t = torch.empty(b_tot + 64, dtype=torch.uint8, device=dev)
+    for c0, cn, k, b, n0, b0 in plan:
+        if k == 0:
+            continue
+        ebd.generate_device(ctx, cfg, seed, c0, cn, ev_t[n0 * 36:], len_t[n0:], off_t[n0:], pay_t[b0:], b + 64,
+                            align=16, shard=shard_, gidx=gidx_t[n0:])
+        if b0:
+            off_t[n0:n0 + k] += b0
+    torch.cuda.synchronize()
+    return ev_t, len_t, off_t, pay_t, gidx_t, n_tot, b_tot
 
 
 def main():
     args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.dry_run_cpu:
+        return dry_run_cpu(args)
+    import torch
+    import ebd
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    cfg = args.config
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = args.config or (5 if world > 1 else 3)
     seed = args.seed or cfg
     E = args.events or DEFAULT_EVENTS[cfg]
-    first = rank * E  # shard = a contiguous range of connections (one event per connection here)
 
-    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(E, 1) * 0.8)))))
-    ctx = ebd.Context(max_events=E, device=local, service_capacity=svc_cap, string_arena=max(256 << 20, E * 48),
-                      timing=True)
-    # the batch, generated straight into HBM
+    # every rank keys services with the same secret (the merge matches keys across GPUs)
+    key = np.frombuffer(os.urandom(16), np.uint64).copy()
+    if world > 1:
+        kt_ = torch.tensor(key.view(np.int64), device=dev)
+        torch.distributed.broadcast(kt_, 0)
+        key = kt_.cpu().numpy().view(np.uint64)
+    cap = int(E * 1.15) if cfg == 5 else E
+    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(cap, 1) * 0.8)))))
+    ctx = ebd.Context(max_events=cap, device=local, service_capacity=svc_cap, string_arena=max(256 << 20, cap * 48),
+                      timing=True, hash_key=(int(key[0]), int(key[1])))
     t0 = time.perf_counter()
-    size = ebd.trace_size_device(ctx, cfg, seed, first, E, align=16)
-    ev_t = torch.empty(E * 36, dtype=torch.uint8, device=dev)
-    len_t = torch.empty(E, dtype=torch.int32, device=dev)
-    off_t = torch.empty(E, dtype=torch.int64, device=dev)
-    pay_t = torch.empty(size + 64, dtype=torch.uint8, device=dev)
-    ebd.generate_device(ctx, cfg, seed, first, E, ev_t, len_t, off_t, pay_t, pay_t.numel(), align=16)
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] generated {E} events, {size / 1e9:.2f} GB payload in {time.perf_counter() - t0:.1f} s")
+    ev_t, len_t, off_t, pay_t, gidx_t, n, size = generate_shard(ctx, cfg, seed, E, world, rank, dev)
+    log(f"[rank {rank}] generated {n} events, {size / 1e9:.2f} GB payload in {time.perf_counter() - t0:.1f} s")
+    G = E * world if cfg == 5 else E  # trace positions per step (candidates)
 
     def step(k, cold):
         if cold:
             ctx.clear()  # Aggregator::clear after the previous interval's report (Aggregator.cpp:136-153)
-        ctx.set_seq_base(k * world * E + first)  # global trace order of this shard's events
-        ctx.submit_device(ev_t, len_t, off_t, pay_t, E)
+        # global trace order: step k's event i is at k * G + its position in the trace
+        ctx.set_seq_base(k * G if cfg == 5 else k * world * G + rank * G)
+        ctx.submit_device(ev_t, len_t, off_t, pay_t, n)
 
     def timed_steps(k0, cold):
         if world > 1:
@@ -160,51 +270,66 @@ def main():
     elapsed = timed_steps(args.warmup, cold)
     kt = ctx.kernel_times()
     st = ctx.stats()
+    res = ctx.results()  # of the last timed batch
     # the other mode, reported beside (same batch, same number of steps)
     other_mode = "warm" if cold else "cold"
     ctx.reset_kernel_times()
-    other_elapsed = timed_steps(args.warmup + args.steps, not cold)
+    k_other = args.warmup + args.steps
+    other_elapsed = timed_steps(k_other, not cold)
     other_kt = ctx.kernel_times()
 
     # algorithmic bytes of one batch: sum(consumed + 40) per data event
-    res = ctx.results()
     data_events = int((res["status"] != ebd.STATUS_NONE).sum())
     alg_bytes = int(res["consumed"].astype(np.uint64).sum()) + 40 * data_events
     fresh_launches, fresh_ms = kt["k_fresh"]
     fresh_avg_ms = fresh_ms / max(fresh_launches, 1)
     achieved = alg_bytes / (fresh_avg_ms / 1e3) / 1e9
     traffic = None
-    if os.path.exists(args.pmc):
+    if world == 1 and os.path.exists(args.pmc):
         try:
             with open(args.pmc) as f:
                 pm = json.load(f)
-            if pm.get("events") == E and pm.get("config") == cfg and pm.get("build_id") == ebd.build_id():
+            if pm.get("events") == n and pm.get("config") == cfg and pm.get("build_id") == ebd.build_id():
                 traffic = pm["hbm_bytes_per_launch"]
             else:
                 log(f"[bench] {args.pmc} is for build {pm.get('build_id')} / {pm.get('events')} events: traffic null")
         except (OSError, ValueError, KeyError):
             traffic = None
 
-    # the final per-(pid, endpoint) merge across GPUs, once, after the timed steps: owner-
-    # partitioned all_to_all over RCCL (ebd.shard); seq numbers are already global
-    merge_ms = None
+    # the final per-(pid, endpoint) merge across GPUs, once, after the timed steps:
+    # owner-partitioned all_to_all over RCCL and a device merge on each owner (ebd.shard)
+    merge = None
+    n_all = n
     if world > 1:
         from ebd import shard
-        tm = time.perf_counter()
-        merged = shard.exchange_merge(shard.ServiceTable.from_context(ctx), device=dev)
-        n_services = merged.rec.size if merged is not None else None
-        merge_ms = (time.perf_counter() - tm) * 1e3
-    else:
-        n_services = st["services"]
+        def map_first(f):  # local first_seq (k * G + local index) -> trace position (k * G + gidx)
+            k = torch.div(f, G, rounding_mode="floor")
+            return k * G + gidx_t[f - k * G]
 
-    if rank != 0:
-        torch.distributed.destroy_process_group()
-        return
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
+        tm = time.perf_counter()
+        sent, got = shard.device_exchange_merge(ctx, dev, map_first=map_first)
+        ctx.sync()
+        torch.distributed.barrier()
+        merge_ms = (time.perf_counter() - tm) * 1e3
+        owned = ctx.stats()["services"]
+        tot = torch.tensor([n, owned, sent, got], dtype=torch.int64, device=dev)
+        torch.distributed.all_reduce(tot)
+        mt = torch.tensor([merge_ms], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(mt, op=torch.distributed.ReduceOp.MAX)
+        n_all = int(tot[0])
+        merge = {"merge_ms": float(mt.item()), "services_merged": int(tot[1]), "records_exchanged": int(tot[2]),
+                 "table_state": "the last timed step's interval (cold) or all steps (warm)"}
+        if rank != 0:
+            torch.distributed.destroy_process_group()
+            return
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, seed, args.cpu_seconds)
-    peak_read = stream_read_peak(dev)
-    total_events = E * world * args.steps
+    peak_copy = copy_peak(dev)
+    total_events = n_all * args.steps
     out = {
         "metric": "HTTP events parsed/s (device-resident)",
         "value": total_events / elapsed,
@@ -218,24 +343,29 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: Philox-seeded trace generated in HBM (bit-identical to the host generator)",
-        "config": {"workload": WORKLOADS[cfg], "config": cfg, "events_per_gpu": E, "seed": seed,
-                   "payload_bytes_per_gpu": size, "parallelism": f"{world} shard(s) by connection id, RCCL merge"},
+        "config": {"workload": WORKLOADS[cfg], "config": cfg, "events_per_gpu": n, "seed": seed,
+                   "payload_bytes_per_gpu": size, "step_mode": args.mode,
+                   "parallelism": (f"{world} shards by hash(pid, fd, sessionID), RCCL owner merge" if world > 1
+                                   else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_fresh", "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "k_fresh", "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_def": "sum(consumed) + 40 B per data event (36-B DiscoveryEvent + 4-B length)"},
         "cpu_baseline": cpu,
         "step_gbps_alg": alg_bytes * world * args.steps / elapsed / 1e9,
-        "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items()},
-        "measured_stream_read_gbps": peak_read,
-        "services": n_services,
+        "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items() if v[0]},
+        "measured_copy_gbps": peak_copy,
+        "services": st["services"],
         "errors": st["error_names"],
-        "merge_ms": merge_ms,
+        "merge": merge,
         "mode": args.mode,
         other_mode: {"value": total_events / other_elapsed, "ms_per_step": other_elapsed / args.steps * 1e3,
-                     "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in other_kt.items()}},
+                     "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in other_kt.items() if v[0]}},
         "build_id": ebd.build_id(),
     }
     print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

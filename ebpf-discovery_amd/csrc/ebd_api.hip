@@ -28,10 +28,17 @@ hipError_t launch_collect(const Slot* slots, const unsigned int* used, const uns
 		ebd_service* out, hipStream_t st, int cus);
 hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
-		unsigned long long* alen, hipStream_t st);
-hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, EventRec* ev,
-		uint32_t* len, const unsigned long long* off, uint8_t* payload, hipStream_t st);
+		uint32_t count, uint32_t index, unsigned long long* alen, uint32_t* keep, hipStream_t st);
+hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n,
+		const uint32_t* keep, const uint32_t* pos, const unsigned long long* boff, EventRec* ev, uint32_t* len,
+		unsigned long long* off, uint8_t* payload, unsigned long long* gidx, hipStream_t st);
 void build_gen_tables(GenTables* T);
+hipError_t launch_owner_count(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cnt,
+		unsigned long long* bytes, hipStream_t st, int cus);
+hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
+		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
+		hipStream_t st, int cus);
+hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
 } // namespace ebd
 
 using namespace ebd;
@@ -620,6 +627,63 @@ int ebd_clear(ebd_ctx* c) {
 	return 0;
 }
 
+int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
+		uint32_t* counts, uint64_t* str_counts) {
+	if (!c || world == 0 || world > 64 || !counts || !str_counts)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_collect)
+		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
+	unsigned long long* own = nullptr; // cnt, bytes, cur, scur, sbase: world each
+	HIP_TRY(hipMallocAsync((void**)&own, 5 * 64 * sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(own, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_sarena, c->d_collect, c->stream, c->cus));
+	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, own, own + 64, c->stream, c->cus));
+	unsigned long long h[5 * 64];
+	HIP_TRY(hipMemcpyAsync(h, own, 2 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	uint64_t total = 0, stotal = 0;
+	for (uint32_t w = 0; w < world; w++) {
+		counts[w] = (uint32_t)h[w];
+		str_counts[w] = h[64 + w];
+		h[128 + w] = total;  // cur
+		h[192 + w] = stotal; // scur
+		h[256 + w] = stotal; // sbase
+		total += h[w];
+		stotal += h[64 + w];
+	}
+	int rc = 0;
+	if (recs) {
+		if (total > cap || stotal > strcap || !strings) {
+			rc = -ENOSPC;
+		} else {
+			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 3 * 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
+			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, c->d_sarena, own + 128, own + 192, own + 256, recs, strings,
+					c->stream, c->cus));
+		}
+	}
+	HIP_TRY(hipFreeAsync(own, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return rc;
+}
+
+int ebd_merge_services_device(ebd_ctx* c, const ebd_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen) {
+	if (!c || (n && (!recs || (!strings && strlen))))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (n == 0)
+		return 0;
+	Dev d = make_dev(c);
+	d.n = 0;
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_merge(d, recs, n, strings, c->stream, c->cus));
+	HIP_TRY(launch_verify(d, c->stream, c->cus));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
 int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 	if (!c || !s)
 		return -EINVAL;
@@ -654,106 +718,145 @@ static const GenTables* host_tables() {
 	return g_tables;
 }
 
-static bool single_config(uint32_t cfg) { return cfg == 1 || cfg == 11 || cfg == 2 || cfg == 3; }
+static bool single_config(uint32_t cfg) { return cfg == 1 || cfg == 11 || cfg == 2 || cfg == 3 || cfg == 5; }
+static bool trace_ok(const ebd_trace_config* t) {
+	return t && single_config(t->config) && !(t->align & (t->align - 1)) && (t->shard_count <= 1 || t->shard_index < t->shard_count);
+}
+// config 5 is config 3's distribution, sharded by connection
+static uint32_t gen_config(uint32_t c) { return c == 5 ? 3 : c; }
 
-int ebd_trace_size(const ebd_trace_config* t, uint64_t* payload_bytes) {
-	if (!t || !payload_bytes || !single_config(t->config) || (t->align & (t->align - 1)))
+int ebd_trace_size(const ebd_trace_config* t, uint32_t* n_events, uint64_t* payload_bytes) {
+	if (!trace_ok(t) || !payload_bytes)
 		return -EINVAL;
 	const GenTables* T = host_tables();
 	const uint32_t a = t->align ? t->align : 1;
 	uint64_t total = 0;
-	for (uint32_t i = 0; i < t->n; i++)
-		total += align_up(gen_single(T, t->config, t->seed, t->first + i, nullptr, nullptr), a);
+	uint32_t kept = 0;
+	for (uint32_t i = 0; i < t->n; i++) {
+		const uint32_t L = gen_single_shard(T, gen_config(t->config), t->seed, t->first + i, t->shard_count, t->shard_index,
+				nullptr, nullptr);
+		if (L || t->shard_count <= 1) {
+			total += align_up(L, a);
+			kept++;
+		}
+	}
 	*payload_bytes = total;
+	if (n_events)
+		*n_events = kept;
 	return 0;
 }
 
 int ebd_trace_generate_host(const ebd_trace_config* t, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
-		uint8_t* payload, uint64_t payload_cap) {
-	if (!t || !single_config(t->config) || (t->align & (t->align - 1)) || (t->n && (!events || !len || !off || !payload)))
+		uint8_t* payload, uint64_t payload_cap, uint64_t* gidx) {
+	if (!trace_ok(t) || (t->n && (!events || !len || !off || !payload)))
 		return -EINVAL;
 	const GenTables* T = host_tables();
 	const uint32_t a = t->align ? t->align : 1;
 	uint64_t at = 0;
+	uint32_t k = 0;
 	for (uint32_t i = 0; i < t->n; i++) {
-		const uint32_t L = gen_single(T, t->config, t->seed, t->first + i, nullptr, nullptr);
+		const uint32_t L = gen_single_shard(T, gen_config(t->config), t->seed, t->first + i, t->shard_count, t->shard_index,
+				nullptr, nullptr);
+		if (!L && t->shard_count > 1)
+			continue;
 		if (at + L > payload_cap)
 			return -ENOSPC;
 		EventRec e;
-		gen_single(T, t->config, t->seed, t->first + i, &e, payload + at);
-		std::memcpy(&events[i], &e, sizeof(e));
-		len[i] = L;
-		off[i] = at;
+		gen_single(T, gen_config(t->config), t->seed, t->first + i, &e, payload + at);
+		std::memcpy(&events[k], &e, sizeof(e));
+		len[k] = L;
+		off[k] = at;
+		if (gidx)
+			gidx[k] = t->first + i;
+		k++;
 		at = align_up(at + L, a);
 	}
 	return 0;
 }
 
-int ebd_trace_size_device(ebd_ctx* c, const ebd_trace_config* t, uint64_t* payload_bytes) {
-	if (!c || !t || !payload_bytes || !single_config(t->config) || (t->align & (t->align - 1)) || t->n == 0)
-		return -EINVAL;
-	std::lock_guard<std::mutex> lk(c->mu);
-	HIP_TRY(hipSetDevice(c->device));
+static int ensure_gen_tables(ebd_ctx* c) {
 	if (!c->d_gen) {
 		HIP_TRY(hipMalloc(&c->d_gen, sizeof(GenTables)));
 		HIP_TRY(hipMemcpy(c->d_gen, host_tables(), sizeof(GenTables), hipMemcpyHostToDevice));
 	}
-	unsigned long long *alen = nullptr, *sum = nullptr;
-	void* tmp = nullptr;
-	size_t tmp_bytes = 0;
-	HIP_TRY(hipMallocAsync((void**)&alen, (size_t)t->n * 8, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&sum, 8, c->stream));
-	HIP_TRY(launch_gen_len(c->d_gen, t->config, t->seed, t->first, t->n, t->align ? t->align : 1, alen, c->stream));
-	HIP_TRY(hipcub::DeviceReduce::Sum(nullptr, tmp_bytes, alen, sum, (int)t->n, c->stream));
-	HIP_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 16, c->stream));
-	HIP_TRY(hipcub::DeviceReduce::Sum(tmp, tmp_bytes, alen, sum, (int)t->n, c->stream));
-	unsigned long long v = 0;
-	HIP_TRY(hipMemcpyAsync(&v, sum, 8, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
-	HIP_TRY(hipFreeAsync(sum, c->stream));
-	HIP_TRY(hipFreeAsync(alen, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
-	*payload_bytes = v;
 	return 0;
 }
 
-int ebd_trace_generate_device(ebd_ctx* c, const ebd_trace_config* t, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
-		uint8_t* payload, uint64_t payload_cap) {
-	if (!c || !t || !single_config(t->config) || (t->align & (t->align - 1)) || t->n == 0)
+// Both device passes share the length pass and its scans; `out` == nullptr: sizes only.
+struct GenOut {
+	EventRec* ev;
+	uint32_t* len;
+	uint64_t* off;
+	uint8_t* payload;
+	uint64_t cap;
+	uint64_t* gidx;
+};
+
+static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out, uint32_t* n_events, uint64_t* bytes) {
+	HIP_TRY(hipSetDevice(c->device));
+	int rc = ensure_gen_tables(c);
+	if (rc)
+		return rc;
+	const uint32_t n = t->n, a = t->align ? t->align : 1, cfg = gen_config(t->config);
+	unsigned long long *alen = nullptr, *boff = nullptr;
+	uint32_t *keep = nullptr, *pos = nullptr;
+	HIP_TRY(hipMallocAsync((void**)&alen, (size_t)n * 8 + 8, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&boff, (size_t)n * 8 + 8, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&keep, (size_t)n * 4 + 4, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&pos, (size_t)n * 4 + 4, c->stream));
+	HIP_TRY(launch_gen_len(c->d_gen, cfg, t->seed, t->first, n, a, t->shard_count, t->shard_index, alen, keep, c->stream));
+	if (t->shard_count <= 1) // every candidate is kept (a kept event may be empty only here)
+		HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)keep, 1, n, c->stream));
+	size_t b1 = 0, b2 = 0;
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, alen, boff, (int)n + 1, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, keep, pos, (int)n + 1, c->stream));
+	void* tmp = nullptr;
+	HIP_TRY(hipMallocAsync(&tmp, (b1 > b2 ? b1 : b2) + 16, c->stream));
+	// the (n+1)-th entries become the totals
+	HIP_TRY(hipMemsetAsync(alen + n, 0, 8, c->stream));
+	HIP_TRY(hipMemsetAsync(keep + n, 0, 4, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, alen, boff, (int)n + 1, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, keep, pos, (int)n + 1, c->stream));
+	unsigned long long total = 0;
+	uint32_t kept = 0;
+	HIP_TRY(hipMemcpyAsync(&total, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(&kept, pos + n, 4, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	rc = 0;
+	if (out) {
+		if (total > out->cap)
+			rc = -ENOSPC;
+		else
+			HIP_TRY(launch_gen_write(c->d_gen, cfg, t->seed, t->first, n, keep, pos, boff, out->ev, out->len,
+					(unsigned long long*)out->off, out->payload, (unsigned long long*)out->gidx, c->stream));
+	}
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipFreeAsync(alen, c->stream));
+	HIP_TRY(hipFreeAsync(boff, c->stream));
+	HIP_TRY(hipFreeAsync(keep, c->stream));
+	HIP_TRY(hipFreeAsync(pos, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	if (n_events)
+		*n_events = kept;
+	if (bytes)
+		*bytes = total;
+	return rc;
+}
+
+int ebd_trace_size_device(ebd_ctx* c, const ebd_trace_config* t, uint32_t* n_events, uint64_t* payload_bytes) {
+	if (!c || !trace_ok(t) || !payload_bytes || t->n == 0)
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
-	HIP_TRY(hipSetDevice(c->device));
-	if (!c->d_gen) {
-		HIP_TRY(hipMalloc(&c->d_gen, sizeof(GenTables)));
-		HIP_TRY(hipMemcpy(c->d_gen, host_tables(), sizeof(GenTables), hipMemcpyHostToDevice));
-	}
-	const uint32_t a = t->align ? t->align : 1;
-	unsigned long long* alen = (unsigned long long*)off;
-	HIP_TRY(launch_gen_len(c->d_gen, t->config, t->seed, t->first, t->n, a, alen, c->stream));
-	size_t tmp_bytes = 0;
-	unsigned long long* tmp_out = nullptr;
-	HIP_TRY(hipMallocAsync((void**)&tmp_out, (size_t)t->n * sizeof(unsigned long long), c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, alen, tmp_out, (int)t->n, c->stream));
-	void* tmp = nullptr;
-	HIP_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 16, c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, alen, tmp_out, (int)t->n, c->stream));
-	unsigned long long last_off = 0, last_len = 0;
-	HIP_TRY(hipMemcpyAsync(&last_off, tmp_out + t->n - 1, 8, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipMemcpyAsync(&last_len, alen + t->n - 1, 8, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
-	if (last_off + last_len > payload_cap) {
-		HIP_TRY(hipFreeAsync(tmp, c->stream));
-		HIP_TRY(hipFreeAsync(tmp_out, c->stream));
-		HIP_TRY(hipStreamSynchronize(c->stream));
-		return -ENOSPC;
-	}
-	HIP_TRY(hipMemcpyAsync(off, tmp_out, (size_t)t->n * 8, hipMemcpyDeviceToDevice, c->stream));
-	HIP_TRY(launch_gen_write(c->d_gen, t->config, t->seed, t->first, t->n, (EventRec*)events, len,
-			(const unsigned long long*)off, payload, c->stream));
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
-	HIP_TRY(hipFreeAsync(tmp_out, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
-	return 0;
+	return trace_device(c, t, nullptr, n_events, payload_bytes);
+}
+
+int ebd_trace_generate_device(ebd_ctx* c, const ebd_trace_config* t, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
+		uint8_t* payload, uint64_t payload_cap, uint64_t* gidx) {
+	if (!c || !trace_ok(t) || t->n == 0 || !events || !len || !off || !payload)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	const GenOut o{(EventRec*)events, len, off, payload, payload_cap, gidx};
+	return trace_device(c, t, &o, nullptr, nullptr);
 }
 
 // --------------------------------------------------------------------------------------

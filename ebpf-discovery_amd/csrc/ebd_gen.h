@@ -387,4 +387,27 @@ EBD_HD uint32_t gen_single(const GenTables* T, uint32_t config, uint64_t seed, u
 
 EBD_HD uint64_t align_up(uint64_t x, uint32_t a) { return (x + a - 1) & ~(uint64_t)(a - 1); }
 
+// Shard of a connection (pid, fd, sessionID) among `count` GPUs: every
+// event of a connection lands on one GPU, so parser sessions never cross GPUs.  Same
+// function as ebd/shard.py connection_hash.
+EBD_HD uint32_t conn_shard(uint32_t pid, uint32_t fd, uint32_t sid, uint32_t count) {
+	const uint64_t kv = (uint64_t)pid | ((uint64_t)fd << 32);
+	return count <= 1 ? 0u : (uint32_t)(fmix64(kv ^ ((uint64_t)sid * 0x9E3779B97F4A7C15ull)) % count);
+}
+
+// Event `idx` of a single-buffer config kept by shard `index` of `count`?  Its length when
+// kept (0 when not: a kept event is never empty).
+EBD_HD uint32_t gen_single_shard(const GenTables* T, uint32_t config, uint64_t seed, uint64_t idx, uint32_t count,
+		uint32_t index, EventRec* ev, uint8_t* out) {
+	if (count <= 1)
+		return gen_single(T, config, seed, idx, ev, out);
+	EventRec e;
+	const uint32_t L = gen_single(T, config, seed, idx, &e, nullptr);
+	if (conn_shard(e.pid, e.fd, e.sessionID, count) != index)
+		return 0;
+	if (ev || out)
+		gen_single(T, config, seed, idx, ev, out);
+	return L;
+}
+
 } // namespace ebd

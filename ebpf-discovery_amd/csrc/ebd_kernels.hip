@@ -60,7 +60,9 @@ EBD_HD unsigned long long first_word(unsigned long long seq, bool https, uint32_
 }
 
 // Returns the slot (kNone when the table is full); *claimed: this call created the service.
-__device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first, uint32_t cls, bool* claimed) {
+// inc_int / inc_ext: the counter increments (one request: its class; a merged record: its counts).
+__device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first, uint32_t inc_int, uint32_t inc_ext,
+		bool* claimed) {
 	uint32_t idx = (uint32_t)h.lo & d.slot_mask;
 	bool found = false;
 	*claimed = false;
@@ -114,10 +116,10 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 		return kNone;
 	}
 	Slot* s = d.slots + idx;
-	if (cls == CLS_INTERNAL)
-		atomicAdd(&s->internal_clients, 1u);
-	else if (cls == CLS_EXTERNAL)
-		atomicAdd(&s->external_clients, 1u);
+	if (inc_int)
+		atomicAdd(&s->internal_clients, inc_int);
+	if (inc_ext)
+		atomicAdd(&s->external_clients, inc_ext);
 	if (first < seen_first)
 		atomicMin(&s->first, first);
 	return idx;
@@ -1071,7 +1073,8 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
 	kh.bytes(dst, hl + ul);
 	bool claimed;
-	const uint32_t slot = agg_insert(d, kh.finish(), first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl), cls, &claimed);
+	const uint32_t slot = agg_insert(d, kh.finish(), first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl),
+			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (claimed) // a rare path: one reservation per claim
 		claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
 				atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
@@ -1254,8 +1257,8 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 		PendingClaim& pc, bool& has) {
 	bool claimed;
 	const Hash128 key = d.keys[i];
-	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len), cls,
-			&claimed);
+	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
+			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (claimed) {
 		const uint8_t* p = d.payload + d.off[i];
 		pc.slot = slot;
@@ -1423,7 +1426,7 @@ __global__ void k_collect(const Slot* slots, const unsigned int* used, const uns
 		v.endpoint_len = s.ep_len;
 		v.domain_off = doff;
 		v.domain_len = dlen;
-		v.pad2_ = 0;
+		v.host_len = hl;
 		v.first_seq = s.first >> 16;
 		v.key_lo = s.tag;
 		v.key_hi = s.hi;
@@ -1432,21 +1435,101 @@ __global__ void k_collect(const Slot* slots, const unsigned int* used, const uns
 }
 
 // ---------------------------------------------------------------------------------
-// Synthetic trace generation in HBM (ebd_gen.h).
+// Cross-GPU merge.  Export: the collected services grouped by owner GPU
+// (key_lo % world) with their endpoint bytes; merge: received records inserted into the
+// owner's table with agg_insert (counters add, the smallest first word wins).
 // ---------------------------------------------------------------------------------
-__global__ void k_gen_len(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
-		uint32_t align, unsigned long long* alen) {
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-		alen[i] = align_up(gen_single(T, config, seed, first + i, nullptr, nullptr), align);
+constexpr int kOwnerMax = 64;
+
+// Per owner: records and (8-aligned) string bytes, block histograms in LDS.
+__global__ void k_owner_count(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cnt,
+		unsigned long long* bytes) {
+	__shared__ unsigned long long hc[kOwnerMax], hb[kOwnerMax];
+	for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
+		hc[w] = hb[w] = 0;
+	__syncthreads();
+	const unsigned long long n = ctr[CTR_SERVICES];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const uint32_t w = (uint32_t)(rec[k].key_lo % world);
+		atomicAdd(&hc[w], 1ull);
+		atomicAdd(&hb[w], (unsigned long long)((rec[k].endpoint_len + 7u) & ~7u));
+	}
+	__syncthreads();
+	for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) {
+		if (hc[w])
+			atomicAdd(&cnt[w], hc[w]);
+		if (hb[w])
+			atomicAdd(&bytes[w], hb[w]);
+	}
 }
 
-__global__ void k_gen_write(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
-		EventRec* ev, uint32_t* len, const unsigned long long* off, uint8_t* payload) {
+// cur[w] / scur[w]: the next record / string byte of owner w (initialised to the owners'
+// segment starts); records land in arbitrary order inside their owner's segment.
+__global__ void k_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
+		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings) {
+	const unsigned long long n = ctr[CTR_SERVICES];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		ebd_service v = rec[k];
+		const uint32_t w = (uint32_t)(v.key_lo % world);
+		const uint32_t nb = (v.endpoint_len + 7u) & ~7u;
+		const unsigned long long at = atomicAdd(&cur[w], 1ull);
+		const unsigned long long sat = atomicAdd(&scur[w], (unsigned long long)nb);
+		if (v.endpoint_off != ~0ull) {
+			const unsigned long long* src = (const unsigned long long*)(arena + v.endpoint_off);
+			unsigned long long* dst = (unsigned long long*)(strings + sat);
+			for (uint32_t b = 0; b < nb / 8; b++)
+				dst[b] = src[b];
+			v.endpoint_off = sat - sbase[w];
+		}
+		out[at] = v;
+	}
+}
+
+__global__ void k_merge(Dev d, const ebd_service* rec, uint32_t n, const uint8_t* strings) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const ebd_service v = rec[k];
+		bool claimed;
+		const unsigned long long first = (v.first_seq << 16) | ((unsigned long long)(v.https & 1u) << 15) | (v.host_len & 0x7fffu);
+		const uint32_t slot = agg_insert(d, Hash128{v.key_lo, v.key_hi}, first, v.internal_clients, v.external_clients, &claimed);
+		if (claimed) {
+			const uint8_t* ep = strings + (v.endpoint_off == ~0ull ? 0 : v.endpoint_off);
+			const uint32_t hl = min(v.host_len, v.endpoint_len);
+			claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
+					atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((v.endpoint_len + 7u) & ~7u)), v.pid, ep, hl, ep + hl,
+					v.endpoint_len - hl);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// Synthetic trace generation in HBM (ebd_gen.h).
+// ---------------------------------------------------------------------------------
+// Pass 1: aligned length of every candidate event (0: another shard's), and whether it is kept.
+__global__ void k_gen_len(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
+		uint32_t align, uint32_t count, uint32_t index, unsigned long long* alen, uint32_t* keep) {
 	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		const uint32_t L = gen_single_shard(T, config, seed, first + i, count, index, nullptr, nullptr);
+		alen[i] = L ? align_up(L, align) : 0;
+		keep[i] = L ? 1u : 0u;
+	}
+}
+
+// Pass 2: kept candidates written at their scanned positions; gidx (optional) = the trace
+// index of each written event.
+__global__ void k_gen_write(const GenTables* T, uint32_t config, unsigned long long seed, unsigned long long first, uint32_t n,
+		const uint32_t* keep, const uint32_t* pos, const unsigned long long* boff, EventRec* ev, uint32_t* len,
+		unsigned long long* off, uint8_t* payload, unsigned long long* gidx) {
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+		if (!keep[i])
+			continue;
 		EventRec e;
-		const uint32_t L = gen_single(T, config, seed, first + i, &e, payload + off[i]);
-		ev[i] = e;
-		len[i] = L;
+		const uint32_t k = pos[i];
+		const uint32_t L = gen_single(T, config, seed, first + i, &e, payload + boff[i]);
+		ev[k] = e;
+		len[k] = L;
+		off[k] = boff[i];
+		if (gidx)
+			gidx[k] = first + i;
 	}
 }
 
@@ -1509,15 +1592,32 @@ hipError_t launch_clear_used(const unsigned int* used, const unsigned long long*
 	return hipGetLastError();
 }
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
-		unsigned long long* alen, hipStream_t st) {
+		uint32_t count, uint32_t index, unsigned long long* alen, uint32_t* keep, hipStream_t st) {
 	hipLaunchKernelGGL(k_gen_len, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, T, config, (unsigned long long)seed,
-			(unsigned long long)first, n, align, alen);
+			(unsigned long long)first, n, align, count, index, alen, keep);
 	return hipGetLastError();
 }
-hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, EventRec* ev,
-		uint32_t* len, const unsigned long long* off, uint8_t* payload, hipStream_t st) {
+hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n,
+		const uint32_t* keep, const uint32_t* pos, const unsigned long long* boff, EventRec* ev, uint32_t* len,
+		unsigned long long* off, uint8_t* payload, unsigned long long* gidx, hipStream_t st) {
 	hipLaunchKernelGGL(k_gen_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, T, config, (unsigned long long)seed,
-			(unsigned long long)first, n, ev, len, off, payload);
+			(unsigned long long)first, n, keep, pos, boff, ev, len, off, payload, gidx);
+	return hipGetLastError();
+}
+
+hipError_t launch_owner_count(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cnt,
+		unsigned long long* bytes, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_owner_count, dim3(cus * 4), dim3(256), 0, st, rec, ctr, world, cnt, bytes);
+	return hipGetLastError();
+}
+hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
+		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
+		hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_owner_scatter, dim3(cus * 8), dim3(256), 0, st, rec, ctr, world, arena, cur, scur, sbase, out, strings);
+	return hipGetLastError();
+}
+hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_merge, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n, strings);
 	return hipGetLastError();
 }
 

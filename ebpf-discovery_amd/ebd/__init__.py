@@ -35,7 +35,7 @@ SESSION_REQ_DTYPE = np.dtype([("seq", "<u8"), ("pid", "<u4"), ("str_off", "<u4")
                               ("status", "u1"), ("pad", "<u2"), ("pad2", "<u4")])
 SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4"), ("https", "u1"),
                           ("pad", "u1", (3,)), ("endpoint_off", "<u8"), ("endpoint_len", "<u4"),
-                          ("domain_off", "<u4"), ("domain_len", "<u4"), ("pad2", "<u4"), ("first_seq", "<u8"),
+                          ("domain_off", "<u4"), ("domain_len", "<u4"), ("host_len", "<u4"), ("first_seq", "<u8"),
                           ("key_lo", "<u8"), ("key_hi", "<u8")])
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
 assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 64
@@ -68,7 +68,7 @@ class KernelTime(C.Structure):
 
 class TraceConfig(C.Structure):
     _fields_ = [("config", C.c_uint32), ("seed", C.c_uint64), ("first", C.c_uint64), ("n", C.c_uint32),
-                ("align", C.c_uint32), ("pad", C.c_uint32)]
+                ("align", C.c_uint32), ("shard_count", C.c_uint32), ("shard_index", C.c_uint32)]
 
 
 class Ipv4Network(C.Structure):
@@ -100,15 +100,19 @@ _SIGS = {
     "ebd_collect_services": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
                                        C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_clear": (C.c_int, [C.c_void_p]),
+    "ebd_export_services_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
+                                             C.c_void_p, C.c_void_p]),
+    "ebd_merge_services_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ebd_strerror": (C.c_char_p, [C.c_int]),
     "ebd_build_id": (C.c_char_p, []),
-    "ebd_trace_size": (C.c_int, [C.POINTER(TraceConfig), C.POINTER(C.c_uint64)]),
+    "ebd_trace_size": (C.c_int, [C.POINTER(TraceConfig), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "ebd_trace_generate_host": (C.c_int, [C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                          C.c_uint64]),
-    "ebd_trace_size_device": (C.c_int, [C.c_void_p, C.POINTER(TraceConfig), C.POINTER(C.c_uint64)]),
+                                          C.c_uint64, C.c_void_p]),
+    "ebd_trace_size_device": (C.c_int, [C.c_void_p, C.POINTER(TraceConfig), C.POINTER(C.c_uint32),
+                                        C.POINTER(C.c_uint64)]),
     "ebd_trace_generate_device": (C.c_int, [C.c_void_p, C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p,
-                                            C.c_void_p, C.c_uint64]),
+                                            C.c_void_p, C.c_uint64, C.c_void_p]),
     # testing header
     "ebd_host_dfa_info": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
@@ -295,6 +299,28 @@ class Context:
     def clear(self):
         _check(lib().ebd_clear(self.h), "ebd_clear")
 
+    def export_services_device(self, world, device):
+        """The services grouped by owner (key_lo % world) in device tensors:
+        (records as uint8 [n * 64], strings uint8, counts[world], str_counts[world])."""
+        import torch
+        counts = np.zeros(world, np.uint32)
+        scounts = np.zeros(world, np.uint64)
+        _check(lib().ebd_export_services_device(self.h, world, None, 0, None, 0, _p(counts), _p(scounts)), "export")
+        n, sb = int(counts.sum()), int(scounts.sum())
+        recs = torch.empty(max(n, 1) * SERVICE_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        strs = torch.empty(max(sb, 8), dtype=torch.uint8, device=device)
+        _check(lib().ebd_export_services_device(self.h, world, C.c_void_p(recs.data_ptr()), max(n, 1),
+                                                C.c_void_p(strs.data_ptr()), strs.numel(), _p(counts), _p(scounts)),
+               "ebd_export_services_device")
+        return recs[:n * SERVICE_DTYPE.itemsize], strs[:sb], counts, scounts
+
+    def merge_services_device(self, recs, strings):
+        """Inserts exported service records (device uint8 tensors) into this table."""
+        n = recs.numel() // SERVICE_DTYPE.itemsize
+        _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
+                                               C.c_void_p(strings.data_ptr()) if strings.numel() else None,
+                                               strings.numel()), "ebd_merge_services_device")
+
     def stats(self):
         s = Stats()
         _check(lib().ebd_get_stats(self.h, C.byref(s)), "ebd_get_stats")
@@ -311,41 +337,46 @@ def _ptrval(x):
     return int(x)
 
 
-def trace_config(config, seed, first, n, align=1):
-    return TraceConfig(config=config, seed=seed, first=first, n=n, align=align)
+def trace_config(config, seed, first, n, align=1, shard=(1, 0)):
+    return TraceConfig(config=config, seed=seed, first=first, n=n, align=align, shard_count=shard[0],
+                       shard_index=shard[1])
 
 
-def trace_size(config, seed, first, n, align=1):
-    t = trace_config(config, seed, first, n, align)
-    v = C.c_uint64()
-    _check(lib().ebd_trace_size(C.byref(t), C.byref(v)), "ebd_trace_size")
-    return v.value
+def trace_size(config, seed, first, n, align=1, shard=(1, 0), with_events=False):
+    """Payload bytes (and with_events: kept events) of candidates [first, first + n)."""
+    t = trace_config(config, seed, first, n, align, shard)
+    v, k = C.c_uint64(), C.c_uint32()
+    _check(lib().ebd_trace_size(C.byref(t), C.byref(k), C.byref(v)), "ebd_trace_size")
+    return (k.value, v.value) if with_events else v.value
 
 
-def generate_host(config, seed, first, n, align=1):
-    """Synthetic trace on the host: (events, lens, offs, payload)."""
-    size = trace_size(config, seed, first, n, align)
-    ev = np.zeros(n, EVENT_DTYPE)
-    lens = np.zeros(n, np.uint32)
-    offs = np.zeros(n, np.uint64)
+def generate_host(config, seed, first, n, align=1, shard=(1, 0), with_gidx=False):
+    """Synthetic trace on the host: (events, lens, offs, payload[, gidx]).
+    shard=(count, index) keeps the events of connections hashing to index (config 5)."""
+    k, size = trace_size(config, seed, first, n, align, shard, with_events=True)
+    ev = np.zeros(k, EVENT_DTYPE)
+    lens = np.zeros(k, np.uint32)
+    offs = np.zeros(k, np.uint64)
+    gidx = np.zeros(k, np.uint64)
     payload = np.zeros(size + 16, np.uint8)
-    t = trace_config(config, seed, first, n, align)
-    _check(lib().ebd_trace_generate_host(C.byref(t), _p(ev), _p(lens), _p(offs), _p(payload), payload.size),
+    t = trace_config(config, seed, first, n, align, shard)
+    _check(lib().ebd_trace_generate_host(C.byref(t), _p(ev), _p(lens), _p(offs), _p(payload), payload.size, _p(gidx)),
            "ebd_trace_generate_host")
-    return ev, lens, offs, payload
+    return (ev, lens, offs, payload, gidx) if with_gidx else (ev, lens, offs, payload)
 
 
-def trace_size_device(ctx, config, seed, first, n, align=1):
-    t = trace_config(config, seed, first, n, align)
-    v = C.c_uint64()
-    _check(lib().ebd_trace_size_device(ctx.h, C.byref(t), C.byref(v)), "ebd_trace_size_device")
-    return v.value
+def trace_size_device(ctx, config, seed, first, n, align=1, shard=(1, 0), with_events=False):
+    t = trace_config(config, seed, first, n, align, shard)
+    v, k = C.c_uint64(), C.c_uint32()
+    _check(lib().ebd_trace_size_device(ctx.h, C.byref(t), C.byref(k), C.byref(v)), "ebd_trace_size_device")
+    return (k.value, v.value) if with_events else v.value
 
 
-def generate_device(ctx, config, seed, first, n, events, lens, offs, payload, payload_cap, align=1):
-    t = trace_config(config, seed, first, n, align)
+def generate_device(ctx, config, seed, first, n, events, lens, offs, payload, payload_cap, align=1, shard=(1, 0),
+                    gidx=None):
+    t = trace_config(config, seed, first, n, align, shard)
     _check(lib().ebd_trace_generate_device(ctx.h, C.byref(t), _ptrval(events), _ptrval(lens), _ptrval(offs),
-                                           _ptrval(payload), payload_cap), "ebd_trace_generate_device")
+                                           _ptrval(payload), payload_cap, _ptrval(gidx)), "ebd_trace_generate_device")
 
 
 # ---- host hooks (product semantics on the CPU, for tests) -------------------------------

@@ -136,7 +136,7 @@ typedef struct ebd_service {
 	uint32_t endpoint_len;
 	uint32_t domain_off; /* relative to endpoint_off */
 	uint32_t domain_len;
-	uint32_t pad2_;
+	uint32_t host_len;   /* the first request's host length (its host/url split of the endpoint) */
 	uint64_t first_seq; /* global order of the request that created it (first arrival) */
 	uint64_t key_lo, key_hi; /* 128-bit hash of (pid, endpoint): identical on every GPU, so
 	                            shards merge and pick owners by it without comparing strings */
@@ -241,6 +241,19 @@ int ebd_collect_services(ebd_ctx* ctx, ebd_service* out, uint32_t cap, uint32_t*
 		uint64_t* strlen);
 /* Aggregator::clear (Aggregator.cpp:136-153, network counters off). */
 int ebd_clear(ebd_ctx* ctx);
+
+/* --- cross-GPU merge of per-GPU service tables ------------------------ */
+/* The context's services grouped by owner GPU, owner = key_lo % world, into DEVICE arrays:
+ * recs[] ordered by owner (counts[w] records for owner w), strings[] the owners' endpoint
+ * bytes in owner order (str_counts[w] bytes for owner w, 8-byte aligned pieces), and each
+ * record's endpoint_off relative to its owner's string segment.  counts / str_counts are
+ * host arrays of `world` entries.  recs == NULL: sizes only. */
+int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_service* recs, uint32_t cap, uint8_t* strings,
+		uint64_t strcap, uint32_t* counts, uint64_t* str_counts);
+/* Merges n service records (DEVICE arrays, endpoint_off into strings) into the context's
+ * table: counters add (uint32), the record with the smallest first_seq fixes scheme and
+ * host/url split (Aggregator.cpp:155-168 across GPUs), the endpoint bytes are copied in. */
+int ebd_merge_services_device(ebd_ctx* ctx, const ebd_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen);
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
 /* Hash of the sources this library was built from (profiles/ name the build they measured). */
@@ -248,24 +261,26 @@ const char* ebd_build_id(void);
 
 /* --- synthetic traces, identical on host and device ---------- */
 typedef struct ebd_trace_config {
-	uint32_t config; /* 1, 2, 3 (single-buffer); 4 (fragmented, keep-alive) */
+	uint32_t config; /* 1, 11, 2, 3: single-buffer configs; 5: config 3's distribution, sharded */
 	uint64_t seed;
-	uint64_t first;  /* first event index (shards / samples regenerate identically) */
-	uint32_t n;      /* events */
+	uint64_t first;  /* first candidate event index of the trace */
+	uint32_t n;      /* candidate events [first, first + n) */
 	uint32_t align;  /* payload offset alignment (power of two, >= 1) */
-	uint32_t pad_;
+	uint32_t shard_count; /* > 1: keep only the events whose connection (pid, fd, sessionID) hashes */
+	uint32_t shard_index; /*     to shard_index mod shard_count (ebd/shard.py connection_hash) */
 } ebd_trace_config;
 
-/* Payload bytes needed for events [first, first + n) of a single-buffer config. */
-int ebd_trace_size(const ebd_trace_config* cfg, uint64_t* payload_bytes);
-/* Host generation into caller arrays (events[n], len[n], off[n], payload). */
+/* Events kept and payload bytes of a trace slice. */
+int ebd_trace_size(const ebd_trace_config* cfg, uint32_t* n_events, uint64_t* payload_bytes);
+/* Host generation into caller arrays (events, len, off, payload; gidx = trace index of each
+ * kept event, may be NULL). */
 int ebd_trace_generate_host(const ebd_trace_config* cfg, ebd_discovery_event* events, uint32_t* len, uint64_t* off,
-		uint8_t* payload, uint64_t payload_cap);
-/* Payload bytes for a single-buffer config, computed on the context's GPU. */
-int ebd_trace_size_device(ebd_ctx* ctx, const ebd_trace_config* cfg, uint64_t* payload_bytes);
-/* Device generation straight into HBM (pointers are device pointers). */
+		uint8_t* payload, uint64_t payload_cap, uint64_t* gidx);
+/* The same sizes, computed on the context's GPU. */
+int ebd_trace_size_device(ebd_ctx* ctx, const ebd_trace_config* cfg, uint32_t* n_events, uint64_t* payload_bytes);
+/* Device generation straight into HBM (pointers are device pointers; gidx may be NULL). */
 int ebd_trace_generate_device(ebd_ctx* ctx, const ebd_trace_config* cfg, ebd_discovery_event* events, uint32_t* len,
-		uint64_t* off, uint8_t* payload, uint64_t payload_cap);
+		uint64_t* off, uint8_t* payload, uint64_t payload_cap, uint64_t* gidx);
 
 #ifdef __cplusplus
 }

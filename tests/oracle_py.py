@@ -6,6 +6,7 @@ cpu_baseline leg, always as the checker, never as the thing measured or shipped.
 import ctypes as C
 import os
 import subprocess
+import time
 
 import numpy as np
 
@@ -261,3 +262,44 @@ class Oracle:
 
     def is_v6_external(self, b16):
         return bool(lib().orc_is_v6_external(self.h, C.c_char_p(b16)))
+
+
+def _throughput_worker(args):
+    config, seed, first, n, budget_s = args
+    import ebd
+    o = Oracle()
+    done, spent, at = 0, 0.0, first
+    chunk = 100_000
+    while spent < budget_s:
+        ev, lens, offs, payload = ebd.generate_host(config, seed, at, chunk)
+        t = time.perf_counter()
+        o.process(ev, lens, offs, payload)
+        spent += time.perf_counter() - t
+        done += chunk
+        at += chunk
+    return done, spent
+
+
+def parallel_throughput(config, seed, budget_s, threads=None):
+    """The oracle on `threads` host processes (default: the host's CPU share, at most 16 —
+    the GPU box gives one GPU's job 16 cores), each on its own connection slice of the
+    trace (one event per connection in configs 2/3/5, so index slices are connection
+    shards) with its own Discovery/Aggregator state; aggregate events/s = total events /
+    the slowest worker's busy time.  The per-worker tables would be merged as the GPUs'
+    are; the merge is not timed here."""
+    import multiprocessing as mp
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    threads = threads or min(16, share)
+    if threads < 2:
+        return None
+    slice_ = 50_000_000
+    with mp.get_context("fork").Pool(threads) as pool:
+        res = pool.map(_throughput_worker, [(config, seed, k * slice_, slice_, budget_s) for k in range(threads)])
+    done = sum(r[0] for r in res)
+    busy = max(r[1] for r in res)
+    return dict(value=done / busy, unit="events/s", cores=threads, kind="port",
+                sample=f"{threads} processes x ~{budget_s:.0f} s, each on its own connection slice of the config-{config} "
+                       f"trace (seed {seed}), {done} events in all")

@@ -222,3 +222,101 @@ def test_sharded_contexts_merge_to_whole_trace():
         got = shard.merge_tables(tables).packed().rows()
         _, want, _ = run_oracle(ev, lens, offs, payload)
         assert got == want
+
+
+def _owner_segments(recs, strs, counts, scounts):
+    ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    so = np.concatenate([[0], np.cumsum(scounts.astype(np.int64))])
+    n = ebd.SERVICE_DTYPE.itemsize
+    return [(recs[ro[w] * n:ro[w + 1] * n], strs[so[w]:so[w + 1]]) for w in range(len(counts))]
+
+
+def test_device_export_by_owner_and_merge_equals_whole_trace():
+    """The cross-GPU merge's device half on one GPU: each connection shard runs in its own
+    context (as one GPU would), groups its services by owner on the device
+    (ebd_export_services_device), first arrival mapped to trace positions; each owner's
+    segments from every shard are merged on the device (ebd_merge_services_device).  The
+    owners' tables together equal the oracle over the whole trace."""
+    import torch
+    from ebd import shard
+    dev = torch.device("cuda:0")
+    W = 3
+    for ev, lens, offs, payload in (ebd.generate_host(3, 21, 0, 30000), T.fragmented_trace(400, seed=23, window=64)):
+        segs = [[] for _ in range(W)]
+        for idx in shard.shard_indices(ev, W):
+            ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size, hash_key=ebd.TEST_HASH_KEY)
+            ctx.submit(ev[idx], lens[idx], offs[idx], payload)
+            recs, strs, counts, scounts = ctx.export_services_device(W, dev)
+            if recs.numel():
+                words = recs.view(torch.int64).view(-1, 8)
+                words[:, 5] = torch.tensor(idx.astype(np.int64), device=dev)[words[:, 5]]
+                owner = (words[:, 6].cpu().numpy().view(np.uint64) % np.uint64(W)).astype(np.int64)
+                assert np.all(np.diff(owner) >= 0)  # grouped by owner
+            for w, seg in enumerate(_owner_segments(recs, strs, counts, scounts)):
+                segs[w].append(seg)
+        rows = []
+        for w in range(W):
+            base, rparts, sparts = 0, [], []
+            for r, s in segs[w]:
+                r = r.clone()
+                if r.numel():
+                    r.view(torch.int64).view(-1, 8)[:, 2] += base
+                rparts.append(r)
+                sparts.append(s)
+                base += s.numel()
+            m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY)
+            m.merge_services_device(torch.cat(rparts), torch.cat(sparts))
+            assert m.stats()["errors"] == 0
+            rows += m.services()
+        rows.sort(key=lambda t: (t[0], t[1]))
+        _, want, _ = run_oracle(ev, lens, offs, payload)
+        assert rows == want
+
+
+def test_device_exchange_merge_over_rccl_world1():
+    """shard.device_exchange_merge end to end through RCCL (a world-1 nccl group): export,
+    all_to_all_single on GPU tensors, device merge; the table is unchanged."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from ebd import shard
+    ev, lens, offs, payload = ebd.generate_host(3, 31, 0, 20000)
+    ctx = ebd.Context(max_events=len(ev), max_payload=payload.size)
+    ctx.submit(ev, lens, offs, payload)
+    before = ctx.services()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        sent, got = shard.device_exchange_merge(ctx, torch.device("cuda", 0), map_first=lambda f: f)
+    finally:
+        dist.destroy_process_group()
+    assert sent == got == len(before)
+    assert ctx.services() == before
+
+
+def test_device_sharded_generator_matches_host():
+    """Config 5 on the device (bench.py's per-rank shard, chunked): the events of a
+    connection shard, with their trace positions, equal the host generator's."""
+    import torch
+    dev = torch.device("cuda:0")
+    ctx = ebd.Context(max_events=16)
+    for world, rank in ((4, 1), (3, 2), (1, 0)):
+        hev, hl, ho, hp, hg = ebd.generate_host(5, 5, 1000, 30000, align=16, shard=(world, rank), with_gidx=True)
+        k, size = ebd.trace_size_device(ctx, 5, 5, 1000, 30000, align=16, shard=(world, rank), with_events=True)
+        assert k == len(hev) and size <= hp.size
+        e = torch.empty(k * 36, dtype=torch.uint8, device=dev)
+        l_ = torch.empty(k, dtype=torch.int32, device=dev)
+        o_ = torch.empty(k, dtype=torch.int64, device=dev)
+        g_ = torch.empty(k, dtype=torch.int64, device=dev)
+        p_ = torch.zeros(size + 64, dtype=torch.uint8, device=dev)
+        ebd.generate_device(ctx, 5, 5, 1000, 30000, e, l_, o_, p_, p_.numel(), align=16, shard=(world, rank), gidx=g_)
+        torch.cuda.synchronize()
+        assert np.array_equal(e.cpu().numpy().view(ebd.EVENT_DTYPE), hev)
+        assert np.array_equal(l_.cpu().numpy().view(np.uint32), hl)
+        assert np.array_equal(o_.cpu().numpy().view(np.uint64), ho)
+        assert np.array_equal(g_.cpu().numpy().view(np.uint64), hg)
+        pd = p_.cpu().numpy()
+        for i in range(0, k, 37):
+            a = int(ho[i])
+            assert pd[a:a + int(hl[i])].tobytes() == hp[a:a + int(hl[i])].tobytes()

@@ -1,11 +1,14 @@
 """Multi-GPU path on CPU: connection sharding + the owner-partitioned service merge
 (ebd.shard) over a world_size-2 gloo group.
 
-Each rank takes its connection shard of a trace (ebd.shard.shard_indices), replays it with
-the oracle (the stand-in for that rank's GPU context: this test has no GPU), keys its
-services with the product's 128-bit endpoint key, and merges through
-ebd.shard.exchange_merge.  Rank 0's merged table must equal the oracle over the whole trace:
-(pid, endpoint, domain, scheme, internal, external), bit-exact.
+Each rank takes its connection shard of a trace (generated sharded, as bench.py does for
+config 5: ebd.generate_host(..., shard=(world, rank)), the same events as
+ebd.shard.shard_indices), replays it with the oracle (the stand-in for that rank's GPU
+context: this test has no GPU), keys its services with the product's 128-bit endpoint key,
+and merges through ebd.shard.exchange_merge: the device path's owner grouping and
+all_to_all exchange, with the merge rule in numpy in place of k_merge.  The owners' tables
+gathered on rank 0 must equal the oracle over the whole trace: (pid, endpoint, domain,
+scheme, internal, external), bit-exact.
 """
 import datetime
 import json
@@ -27,6 +30,8 @@ import traces
 def _trace(kind):
     if kind == "config3":
         return ebd.generate_host(3, 7, 0, 6000)
+    if kind == "config5":
+        return ebd.generate_host(5, 5, 0, 6000)
     return traces.fragmented_trace(300, seed=9, window=64)
 
 
@@ -48,12 +53,18 @@ def _worker(rank, world, port, kind, out_path):
     try:
         ev, lens, offs, payload = _trace(kind)
         idx = shard.shard_indices(ev, world)[rank]
+        if kind == "config5":  # the shard generated directly, as on the GPU
+            sev, sl, so, sp, gidx = ebd.generate_host(5, 5, 0, 6000, shard=(world, rank), with_gidx=True)
+            assert np.array_equal(gidx, idx) and np.array_equal(sev, ev[idx])
         table = _shard_table(ev, lens, offs, payload, idx)
-        merged = shard.exchange_merge(table, device="cpu")
+        mine = shard.exchange_merge(table, device="cpu")
+        owner = (mine.rec["key_lo"] % np.uint64(world)).astype(np.int64)
+        assert np.all(owner == rank)  # every merged service is on its owner
+        rows = shard.gather_rows(mine)
         if rank == 0:
             with open(out_path, "w") as f:
                 json.dump([[p, ep.decode("latin-1"), dom.decode("latin-1"), sch.decode(), i, e]
-                           for (p, ep, dom, sch, i, e) in merged.rows()], f)
+                           for (p, ep, dom, sch, i, e) in rows], f)
     finally:
         dist.destroy_process_group()
 
@@ -64,7 +75,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("kind", ["config3", "fragmented"])
+@pytest.mark.parametrize("kind", ["config3", "config5", "fragmented"])
 def test_two_rank_merge_equals_whole_trace(kind, tmp_path):
     out_path = str(tmp_path / "merged.json")
     mp.start_processes(_worker, args=(2, _free_port(), kind, out_path), nprocs=2, join=True, start_method="spawn")
@@ -102,3 +113,23 @@ def test_local_merge_rules():
                             shard.ServiceTable.from_rows(rows[1:], keys[1:])])
     got = t.packed().rows()
     assert got == [(7, b"h:1/a", b"h", b"https", 1, 4), (8, b"h:1/a", b"h", b"http", 1, 1)]
+
+
+def test_bench_dry_run_spawns_two_gloo_ranks():
+    """bench.py --gpus 2 --dry-run-cpu: the launcher spawns two ranks (no torchrun), each
+    generates its config-5 connection shard, and the owner-partitioned merge over gloo
+    yields every service of the whole trace exactly once."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run-cpu", "--events",
+                          "3000"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["dry_run"] and line["n_gpus"] == 2
+    assert sum(line["events_per_rank"]) == 6000 and min(line["events_per_rank"]) > 0
+    ev, lens, offs, payload = ebd.generate_host(5, 5, 0, 6000)
+    o = O.Oracle()
+    o.process(ev, lens, offs, payload)
+    assert line["services_merged"] == len(o.services())
