@@ -543,6 +543,10 @@ int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32
 		if (payload_bytes)
 			HIP_TRY(hipMemcpyAsync(c->d_payload, payload, payload_bytes, hipMemcpyHostToDevice, c->stream));
 	}
+	if (std::getenv("EBD_DEBUG_PTRS")) // fault triage: the device ranges a batch uses
+		std::fprintf(stderr, "ebd: batch n=%u payload=[%p, +%llu) ev=%p len=%p off=%p res=%p keys=%p sset=%p carry=%p/%p\n", n,
+				(void*)c->d_payload, (unsigned long long)c->payload_cap, (void*)c->d_ev, (void*)c->d_len, (void*)c->d_off,
+				(void*)c->d_res, (void*)c->d_keys, (void*)c->d_sset, (void*)c->d_carry[0], (void*)c->d_carry[1]);
 	int rc = run_batch(c, c->d_ev, c->d_len, c->d_off, c->d_payload, n);
 	if (rc)
 		return rc;
@@ -871,12 +875,23 @@ int ebd_host_dfa_info(uint32_t* info, uint32_t n) {
 		if (build_dfa(&trie, t) != 0)
 			return -EIO;
 	}
-	const uint32_t v[11] = {t->info.nstates, t->info.url_id, t->info.g2, t->info.g3, t->info.g4, t->info.hvc0, t->info.hvh,
-			t->info.fin0, t->info.fin1, t->info.inv, t->info.init};
+	const uint32_t v[13] = {t->info.nstates, t->info.url_id, t->info.g2, t->info.g3, t->info.g4, t->info.hvc0, t->info.hvh,
+			t->info.fin0, t->info.fin1, t->info.inv, t->info.init, t->info.vl0, t->info.vl1};
 	(void)t->info.hvc1;
-	for (uint32_t k = 0; k < n && k < 11; k++)
+	for (uint32_t k = 0; k < n && k < 13; k++)
 		info[k] = v[k];
 	return 0;
+}
+
+static const DfaTable* host_dfa(const KeyTrie** trie_out);
+
+int ebd_host_dfa_next(uint8_t* out, uint32_t cap) {
+	const KeyTrie* trie;
+	const DfaTable* t = host_dfa(&trie);
+	if (!t || !out || cap < 256u * 256u)
+		return -EINVAL;
+	std::memcpy(out, t->next, 256u * 256u);
+	return (int)t->info.nstates;
 }
 
 static const DfaTable* host_dfa(const KeyTrie** trie_out) {

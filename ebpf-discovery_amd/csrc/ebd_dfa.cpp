@@ -285,6 +285,26 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 			out->next[newid[i] * 256 + b] = (uint8_t)newid[j];
 		}
 	}
+	// the (at most two) non-terminal states that step to themselves on every byte of
+	// [0x20, 0x7e]: the kernel skips such 4-byte words without table reads (k_fresh scan_chunk)
+	in.vl0 = in.vl1 = 0xffffffffu;
+	int nvl = 0;
+	for (uint32_t st = 0; st < in.nstates; st++) {
+		if (st - in.g4 < 3u)
+			continue;
+		bool loop = true;
+		for (int b = 0x20; b <= 0x7e; b++)
+			loop &= out->next[st * 256 + b] == st;
+		if (!loop)
+			continue;
+		if (nvl == 0)
+			in.vl0 = st;
+		else if (nvl == 1)
+			in.vl1 = st;
+		nvl++;
+	}
+	if (nvl > 2)
+		return -6;
 	return 0;
 }
 

@@ -29,6 +29,7 @@ struct DfaInfo {
 	uint32_t hvc1;                 // HV(client, host seen) = hvc0 + 1 = nstates - 1
 	uint32_t fin0, fin1, inv;
 	uint32_t init;                 // reset state (METHOD, empty)
+	uint32_t vl0, vl1;             // generic header-value states: self-loops on [0x20, 0x7e] (or ~0)
 };
 
 struct DfaTable {
@@ -42,16 +43,8 @@ struct DfaTable {
 // Lanes in the same state never conflict (the 4 ASCII bytes that share b[4:0] share one
 // dword), and different states spread over the banks.  The plain (s << 8) | b layout puts
 // all lower-case letters on 7 banks (tools/ubench_lds.hip measures both).
-#if defined(EBD_LDS_PLAIN) // experiment: the plain layout
-constexpr uint32_t kLdsRow = 256;
-EBD_HD constexpr uint32_t lds_col(uint32_t b) { return b; }
-#elif defined(EBD_LDS_COLPERM) // experiment: 256-B rows, byte bits rotated (bank = b[4:0])
-constexpr uint32_t kLdsRow = 256;
-EBD_HD constexpr uint32_t lds_col(uint32_t b) { return ((b & 0x1fu) << 2) | ((b >> 5) & 3u) | (b & 0x80u); }
-#else
 constexpr uint32_t kLdsRow = 260;
 EBD_HD constexpr uint32_t lds_col(uint32_t b) { return ((b & 0x1fu) << 2) | ((b >> 5) & 3u) | (b & 0x80u); }
-#endif
 constexpr uint32_t kLdsRows = 200; // >= nstates (ebd_build_dfa checks)
 constexpr uint32_t kLdsTableBytes = kLdsRows * kLdsRow;
 void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes

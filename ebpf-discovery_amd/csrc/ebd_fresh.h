@@ -227,12 +227,7 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	fresh_spans(T, di, sr, s_final, post, f, L, flags, out);
 	if (out.keyed) {
 		const auto& sp = out.r.u.span;
-#ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
-		out.key.lo = sp.host_len * 31 + sp.url_len;
-		out.key.hi = 1;
-#else
 		out.key = endpoint_key(key, pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
-#endif
 	}
 }
 

@@ -281,60 +281,62 @@ constexpr int kFreshWaves = kFreshThreads / 64;
 #define EBD_SCAN_WAVES 12
 #endif
 constexpr int kScanWaves = EBD_SCAN_WAVES; // waves [0, kScanWaves) scan; the others finalize
+constexpr int kFinWaves = kFreshWaves - kScanWaves;
+constexpr uint32_t kScanLanes = kScanWaves * 64, kFinLanes = kFinWaves * 64;
 #ifndef EBD_RING
 #define EBD_RING 128
 #endif
-constexpr uint32_t kRing = EBD_RING; // finalize records in flight per workgroup (power of two)
-#ifndef EBD_FINPER
-#define EBD_FINPER 0
-#endif
-// records per finalize lane at a time (0: one record, finalized only by the lanes that hold one)
-constexpr int kFinPer = EBD_FINPER > 0 ? EBD_FINPER : 1;
+constexpr uint32_t kRing = EBD_RING; // finalize records in flight per workgroup
+// A push covers up to 64 consecutive positions and a finalize wave frees its 64 only when
+// all are ready: a ring of fewer than 2 x 64 slots can leave a push waiting on a slot whose
+// finalize wave waits on that same push.  Slots are pos & (kRing - 1).
+static_assert(kRing >= 128 && (kRing & (kRing - 1)) == 0, "ring: a power of two of at least 128 slots");
 
 // A chunk word with every byte b replaced by lds_col(b) (5 VALU per 4 bytes).
 __device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
-#ifndef EBD_LDS_PLAIN
 	return ((w << 2) & 0x7c7c7c7cu) | ((w >> 5) & 0x03030303u) | (w & 0x80808080u);
-#else
-	return w;
-#endif
 }
 
-// LDS address of entry (s, byte k of the column-mapped word wc).
+// LDS address of entry (s, byte k of the column-mapped word wc): v_bfe + v_mad_u32_u24.
 __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
-#if !defined(EBD_LDS_PLAIN) && !defined(EBD_LDS_COLPERM)
-	return s * kLdsRow + __builtin_amdgcn_ubfe(wc, 8 * (k & 3), 8); // v_bfe + v_mad_u32_u24
-#else
-	return __builtin_amdgcn_perm(s, wc, 0x0c0c0400u | (uint32_t)(k & 3)); // (s << 8) | byte
-#endif
+	return s * kLdsRow + __builtin_amdgcn_ubfe(wc, 8 * (k & 3), 8);
+}
+
+// Every byte of w in [0x20, 0x7e] (SWAR: no byte < 0x20, none >= 0x7f; exact tests).
+__device__ __forceinline__ bool printable4(uint32_t w) {
+	const uint32_t lt = (w - 0x20202020u) & ~w & 0x80808080u;
+	const uint32_t ge = ((w + 0x01010101u) | w) & 0x80808080u;
+	return (lt | ge) == 0;
 }
 
 // 16 DFA steps over one chunk: s advances, m = the maximum next state, qs = the states at
 // the quarter starts (s0 | s4 << 8 | s8 << 16 | s12 << 24), qm = running maxima after 4, 8
-// and 12 steps (ebd_fresh.h chunk_update).
-__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t& qs,
-		uint32_t& qm) {
+// and 12 steps (ebd_fresh.h chunk_update).  A quarter (one 4-byte word) whose start state
+// is a generic header-value state (di.vl0 / di.vl1: they step to themselves on every byte
+// in [0x20, 0x7e], checked when the table is built) and whose bytes are all in that range
+// leaves the state as it is: the lane skips its 4 table reads (exec-masked), which takes
+// the User-Agent-style padding that dominates request bytes off the LDS.
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t vl0, uint32_t vl1, uint32_t& s,
+		uint32_t& m, uint32_t& qs, uint32_t& qm) {
 	qs = s;
-#ifdef EBD_EXP_MEMONLY // experiment: the loads without the DFA (results are wrong)
-	m = w.w[0] ^ w.w[1] ^ w.w[2] ^ w.w[3];
-	qm = 0;
-	return;
-#endif
-	const uint32_t wc[4] = {lds_cols(w.w[0]), lds_cols(w.w[1]), lds_cols(w.w[2]), lds_cols(w.w[3])};
 	m = 0;
 #pragma unroll
-	for (int k = 0; k < 16; k++) {
-		s = T[tab_index(s, wc[k >> 2], k)];
-		m = max(m, s); // pairs fold into v_max3
-		if (k == 3) {
-			qs |= s << 8;
-			qm = m;
-		} else if (k == 7) {
-			qs |= s << 16;
-			qm |= m << 8;
-		} else if (k == 11) {
-			qs |= s << 24;
-			qm |= m << 16;
+	for (int q = 0; q < 4; q++) {
+		const uint32_t x = w.w[q];
+		const bool skip = (s == vl0 || s == vl1) && printable4(x);
+		if (!skip) {
+			const uint32_t wc = lds_cols(x);
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				s = T[tab_index(s, wc, k)];
+				m = max(m, s);
+			}
+		} else {
+			m = max(m, s);
+		}
+		if (q < 3) {
+			qs |= s << (8 * (q + 1));
+			qm = q == 0 ? m : (qm | (m << (8 * q)));
 		}
 	}
 }
@@ -400,32 +402,13 @@ __device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end
 	const uint32_t flags = evb[32];
 	e.pf = *(const uint32_t*)evb;
 	e.flags = flags;
-#ifdef EBD_EXP_L2ONLY // experiment: every event parses one of the first 4096 buffers (L2-resident)
-	const uint32_t L = d.len[i & 4095];
-	const uint64_t off = d.off[i & 4095];
-#else
 	const uint32_t L = d.len[i];
 	const uint64_t off = d.off[i];
-#endif
-	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 48) ? EK_BAD : EK_PARSE;
+	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 40) ? EK_BAD : EK_PARSE;
 	e.L = e.kind == EK_PARSE ? L : 0;
 	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
 	return e;
 }
-
-// A finished scan waiting for fresh_finalize (64 B).
-struct FinRec {
-	unsigned long long pl; // buffer address (bits 0..47) | L << 48
-	uint32_t idx, pid;
-	uint32_t sf;  // final state | flags << 8 | cseen << 16 | post << 17
-	uint32_t cqm;
-	uint32_t c01; // url.c | host.c << 16
-	uint32_t c23; // hend.c | cip.c << 16
-	uint32_t c4;  // term.c
-	uint32_t qs[5];
-	uint32_t pad[2];
-};
-static_assert(sizeof(FinRec) == 64, "finalize record is 64 bytes");
 
 __device__ __forceinline__ void write_none(const Dev& d, uint32_t i) {
 	ebd_event_result r;
@@ -451,107 +434,41 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
 }
 
-// fresh_finalize for N records per lane, its steps interleaved so that the records' memory
-// round trips overlap: the quarter bytes of every record, then spans, then the endpoint
-// pieces of every record, 64 bytes of each per round trip.  have[n]: record n is real.
-template <int N>
-__device__ __forceinline__ void finalize_recs(const Dev& d, const uint8_t* T, const FinRec (&q)[N], const bool (&have)[N]) {
-	const DfaInfo& di = d.di;
-	ScanRec sr[N];
-	FinLoads f[N];
-	const uint8_t* p[N];
-	uint32_t L[N];
-#pragma unroll
-	for (int n = 0; n < N; n++) {
-		p[n] = have[n] ? (const uint8_t*)(uintptr_t)(q[n].pl & 0xffffffffffffull) : d.payload;
-		L[n] = have[n] ? (uint32_t)(q[n].pl >> 48) : 0;
-		sr[n].url = Trk{q[n].c01 & 0xffffu, q[n].qs[0]};
-		sr[n].host = Trk{q[n].c01 >> 16, q[n].qs[1]};
-		sr[n].hend = Trk{q[n].c23 & 0xffffu, q[n].qs[2]};
-		sr[n].cip = Trk{q[n].c23 >> 16, q[n].qs[3]};
-		sr[n].term = Trk{q[n].c4, q[n].qs[4]};
-		sr[n].cqm = q[n].cqm;
-		sr[n].cseen = (q[n].sf >> 16) & 1u;
-		if (!have[n])
-			rec_init(di, sr[n]); // loads at offset 0 of a valid address
-		fresh_loads(di, sr[n], DevMem{p[n]}, f[n]);
-	}
-	FreshResult fr[N];
-#pragma unroll
-	for (int n = 0; n < N; n++)
-		fresh_spans(LdsTable{T}, di, sr[n], q[n].sf & 0xffu, ((q[n].sf >> 17) & 1u) != 0, f[n], L[n], (uint8_t)(q[n].sf >> 8), fr[n]);
-	// keys (ebd_spec.h endpoint_key, groups of 8 pieces, all records' loads issued together)
-	constexpr uint32_t kGroup = 8;
-	KeyHasher kh[N];
-	uint32_t hs[N], hl[N], us[N], ul[N], en[N], nmax = 0;
-#pragma unroll
-	for (int n = 0; n < N; n++) {
-		const bool k = have[n] && fr[n].keyed;
-		hs[n] = k ? fr[n].r.u.span.host_off : 0;
-		hl[n] = k ? fr[n].r.u.span.host_len : 0;
-		us[n] = k ? fr[n].r.u.span.url_off : 0;
-		ul[n] = k ? fr[n].r.u.span.url_len : 0;
-		en[n] = hl[n] + ul[n];
-		nmax = max(nmax, en[n]);
-		kh[n].init(d.hkey, q[n].pid);
-	}
-	for (uint32_t g = 0; g < nmax; g += 8 * kGroup) {
-		uint64_t A[N][kGroup], B[N][kGroup];
-#pragma unroll
-		for (int n = 0; n < N; n++)
-#pragma unroll
-			for (uint32_t k = 0; k < kGroup; k++) {
-				const uint32_t oo = g + 8 * k;
-				A[n][k] = gload8u(p[n] + hs[n] + (oo < hl[n] ? oo : 0));
-				B[n][k] = gload8u(p[n] + us[n] + ((oo > hl[n] && oo - hl[n] < ul[n]) ? oo - hl[n] : 0));
-			}
-#pragma unroll
-		for (int n = 0; n < N; n++)
-#pragma unroll
-			for (uint32_t k = 0; k < kGroup; k++) {
-				const uint32_t oo = g + 8 * k;
-				if (oo < en[n])
-					kh[n].word(endpoint_piece(hl[n], en[n], oo, A[n][k], B[n][k]));
-			}
-	}
-#pragma unroll
-	for (int n = 0; n < N; n++) {
-		if (!have[n])
-			continue;
-		const uint32_t i = q[n].idx;
-		if (fr[n].r.status == EBD_STATUS_FINISHED) {
-#ifdef EBD_EXP_NOHASH // experiment: finalize without the key (results are wrong)
-			d.keys[i] = Hash128{en[n], 1};
-#else
-			d.keys[i] = kh[n].finish_words(en[n]);
-#endif
-		} else if (fr[n].r.status == EBD_STATUS_UNFINISHED) {
-			// the session may be saved (Discovery.cpp:148-150): sequential path
-			const EventRec& ev = d.ev[i];
-			atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-			sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
-		}
-		d.res[i] = fr[n].r;
-	}
-}
+// A finished scan waiting for fresh_finalize: 16 words, kept in the ring as 16 arrays of
+// kRing words (structure of arrays), so the 64 lanes of a push or of a finalize wave, which
+// hold consecutive ring positions, touch consecutive words: no LDS bank conflicts (a 64-B
+// record per lane made every access 16-way conflicted).
+enum : uint32_t {
+	R_PLO,  // buffer address bits 0..31
+	R_PHI,  // buffer address bits 32..47 | L << 16
+	R_IDX,  // event index
+	R_PID,
+	R_SF,   // final state | flags << 8 | cseen << 16 | post << 17
+	R_CQM,
+	R_C01,  // url.c | host.c << 16
+	R_C23,  // hend.c | cip.c << 16
+	R_C4,   // term.c
+	R_QS,   // qs[0..4] (url, host, hend, cip, term)
+	R_LIM = R_QS + 5, // staged leading bytes that are valid
+	R_POS,  // ring position + 1 (checked by finalize)
+	R_WORDS
+};
+static_assert(R_WORDS == 16, "finalize record is 16 words");
 
-// Leading buffer bytes a scan record carries in LDS (window 0 and half of window 1), so that
-// finalize reads the request line and usually the Host header from LDS instead of reloading
-// lines that left L2 while the lane scanned the rest of the buffer.
-#ifndef EBD_STAGE
-#define EBD_STAGE 64
-#endif
-constexpr uint32_t kStage = EBD_STAGE;
-static_assert(kStage == 0 || kStage == 64 || kStage == 96 || kStage == 128, "whole or half windows");
+// Leading buffer bytes a scan lane stages (window 0), carried to finalize in LDS so that it
+// reads the request line and usually the Host header from LDS instead of reloading lines
+// that left L2 while the lane scanned the rest of the buffer.  Rows are structure of
+// arrays too: word j of the row of lane (or slot) l at [j * stride + l], one row of slack.
+constexpr uint32_t kStage = 64, kStageWords = kStage / 4;
 
-// Buffer bytes for fresh_finalize: offsets [0, lim) from the staged LDS copy `s` (4-B aligned,
-// readable 4 bytes past lim), the rest from the buffer in global memory.
+// Buffer bytes for fresh_finalize: offsets [0, lim) from the staged copy (word j at
+// s[j * kFinLanes]), the rest from the buffer in global memory.
 struct StagedMem {
 	const uint8_t* p;
 	const uint32_t* s;
 	uint32_t lim;
 	__device__ __forceinline__ uint32_t lds4(uint32_t o) const {
-		return __builtin_amdgcn_alignbyte(s[(o >> 2) + 1], s[o >> 2], o & 3u);
+		return __builtin_amdgcn_alignbyte(s[((o >> 2) + 1) * kFinLanes], s[(o >> 2) * kFinLanes], o & 3u);
 	}
 	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
 		if (o + 4 <= lim)
@@ -565,53 +482,49 @@ struct StagedMem {
 	}
 };
 
-// fresh_finalize for one record (ebd_fresh.h), run only by the lanes that hold one.  `stage`:
-// the record's staged leading bytes (pad[0] of the record = how many are valid).
-template <typename Mem>
-__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const FinRec& q, const Mem& mem) {
-	const uint8_t* p = (const uint8_t*)(uintptr_t)(q.pl & 0xffffffffffffull);
-	(void)p; // used by the debug builds below
-	const uint32_t L = (uint32_t)(q.pl >> 48);
-	const uint32_t i = q.idx;
-#ifdef EBD_DBG_CHECK2 // debug build: a record that cannot be real raises bit 60 and is dropped
-	if (p < d.payload || p >= d.payload + (1ull << 36) || L > EBD_BUFFER_MAX_DATA_SIZE || i >= d.n) {
-		atomicOr(&d.ctr[CTR_ERRORS], 1ull << 60);
+__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
+	__hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Workgroup state shared by the scan and finalize waves.
+struct FreshShared {
+	uint32_t ring[R_WORDS * kRing];
+	uint32_t ready[kRing]; // position + 1 once the slot's record is written
+	uint32_t freed[kRing]; // position + 1 once the slot's record is taken
+	uint32_t rdata[(kStageWords + 1) * kRing];      // staged bytes of each slot's record
+	uint32_t stage[kStageWords * kScanLanes];       // a scan lane's current buffer, as scanned
+	uint32_t fstage[(kStageWords + 1) * kFinLanes]; // a finalize lane's record's bytes
+	uint32_t next_ev;   // next event of the workgroup's range
+	uint32_t tail;      // positions handed out to scan lanes
+	uint32_t claim;     // positions handed out to finalize waves
+	uint32_t scan_done; // scan waves that finished
+};
+static_assert(sizeof(FreshShared) + kLdsTableBytes <= 160 * 1024, "k_fresh LDS fits one CU");
+
+// fresh_finalize (ebd_fresh.h) for the record in the lane's registers; the lane's staged
+// bytes are at fs (word j at fs[j * kFinLanes]).
+__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const uint32_t (&q)[R_WORDS], const uint32_t* fs) {
+	const uint8_t* p = (const uint8_t*)(uintptr_t)((unsigned long long)q[R_PLO] | ((unsigned long long)(q[R_PHI] & 0xffffu) << 32));
+	const uint32_t L = q[R_PHI] >> 16;
+	const uint32_t i = q[R_IDX];
+	if (i >= d.n || L > EBD_BUFFER_MAX_DATA_SIZE || (unsigned long long)(p - d.payload) >> 40) {
+		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
 		return;
 	}
-#endif
-#ifdef EBD_DBG_CHECK // debug build: a record that cannot be real is reported and dropped
-	if (p < d.payload || p >= d.payload + (1ull << 36) || L > EBD_BUFFER_MAX_DATA_SIZE || i >= d.n) {
-		printf("EBD_DBG fin: block %u thread %u idx %u n %u L %u p-payload %lld c4 %u sf %x\n", blockIdx.x, threadIdx.x, i, d.n,
-				L, (long long)(p - d.payload), q.c4, q.sf);
-		return;
-	}
-#endif
 	ScanRec sr;
-	sr.url = Trk{q.c01 & 0xffffu, q.qs[0]};
-	sr.host = Trk{q.c01 >> 16, q.qs[1]};
-	sr.hend = Trk{q.c23 & 0xffffu, q.qs[2]};
-	sr.cip = Trk{q.c23 >> 16, q.qs[3]};
-	sr.term = Trk{q.c4, q.qs[4]};
-	sr.cqm = q.cqm;
-	sr.cseen = (q.sf >> 16) & 1u;
+	sr.url = Trk{q[R_C01] & 0xffffu, q[R_QS + 0]};
+	sr.host = Trk{q[R_C01] >> 16, q[R_QS + 1]};
+	sr.hend = Trk{q[R_C23] & 0xffffu, q[R_QS + 2]};
+	sr.cip = Trk{q[R_C23] >> 16, q[R_QS + 3]};
+	sr.term = Trk{q[R_C4], q[R_QS + 4]};
+	sr.cqm = q[R_CQM];
+	sr.cseen = (q[R_SF] >> 16) & 1u;
 	FreshResult fr;
-#ifdef EBD_DBG_CHECK
-	{
-		FinLoads f;
-		fresh_loads(d.di, sr, DevMem{p}, f);
-		fresh_spans(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, f, L, (uint8_t)(q.sf >> 8), fr);
-		const auto& sp = fr.r.u.span;
-		if (fr.keyed && (sp.host_off + sp.host_len > L || sp.url_off + sp.url_len > L)) {
-			printf("EBD_DBG span: idx %u L %u host %u+%u url %u+%u\n", i, L, sp.host_off, sp.host_len, sp.url_off, sp.url_len);
-			return;
-		}
-		if (16 * sr.term.c >= L + 16 || 16 * sr.url.c >= L + 16 || 16 * sr.host.c >= L + 16 || 16 * sr.cip.c >= L + 16) {
-			printf("EBD_DBG trk: idx %u L %u term %u url %u host %u cip %u\n", i, L, sr.term.c, sr.url.c, sr.host.c, sr.cip.c);
-			return;
-		}
-	}
-#endif
-	fresh_finalize(LdsTable{T}, d.di, sr, q.sf & 0xffu, ((q.sf >> 17) & 1u) != 0, mem, L, d.hkey, q.pid, (uint8_t)(q.sf >> 8), fr);
+	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM]}, L, d.hkey,
+			q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
@@ -623,33 +536,16 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	d.res[i] = fr.r;
 }
 
-__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
-	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
-	__hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Workgroup state shared by the scan and finalize waves.
-struct FreshShared {
-	FinRec ring[kRing];
-	uint32_t ready[kRing]; // position + 1 once ring[pos % kRing] is written
-	uint32_t freed[kRing]; // position + 1 once ring[pos % kRing] is finalized
-#if EBD_STAGE
-	uint32_t rdata[kRing * (kStage / 4) + 4];      // staged leading bytes of ring[slot] (+4: lds4 slack)
-	uint32_t stage[kScanWaves * 64 * (kStage / 4)]; // a scan lane's current buffer, as scanned
-	uint32_t fstage[(kFreshWaves - kScanWaves) * 64 * (kStage / 4) + 4]; // a finalize lane's record's bytes
-#endif
-	uint32_t next_ev;      // next event of the workgroup's range
-	uint32_t tail;         // positions handed out to scan lanes
-	uint32_t claim;        // positions handed out to finalize waves
-	uint32_t scan_done;    // scan waves that finished
+// The table first: LDS address = table index, so a step's read needs no base add.
+struct FreshLds {
+	uint8_t T[kLdsTableBytes];
+	FreshShared sh;
 };
 
 __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
-	// static LDS: the table sits at LDS address 0, so a step's index is its address
-	__shared__ __attribute__((aligned(16))) uint8_t T[kLdsTableBytes];
-	__shared__ FreshShared sh;
+	__shared__ __attribute__((aligned(16))) FreshLds lds;
+	uint8_t* T = lds.T;
+	FreshShared& sh = lds.sh;
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 3;
 	// this workgroup's contiguous share of the batch
 	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
@@ -659,65 +555,65 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 	for (uint32_t k = threadIdx.x; k < kRing; k += kFreshThreads)
 		sh.ready[k] = sh.freed[k] = 0;
 	if (threadIdx.x == 0) {
-		sh.next_ev = rb + kScanWaves * 64 * 2;
+		sh.next_ev = rb + kScanLanes * 2;
 		sh.tail = sh.claim = sh.scan_done = 0;
 	}
 	__syncthreads();
 	const DfaInfo& di = d.di;
 
 	if (wave >= kScanWaves) {
-		// ---- finalize waves: kFinPer x 64 records at a time, in position order ----
+		// ---- finalize waves: 64 records at a time, in position order ----
+		const uint32_t fl = (wave - kScanWaves) * 64 + lane; // finalize lane
+		uint32_t* fs = sh.fstage + fl;
 		for (;;) {
 			uint32_t c = 0;
 			if (lane == 0)
-				c = atomicAdd(&sh.claim, 64u * kFinPer);
+				c = atomicAdd(&sh.claim, 64u);
 			c = __builtin_amdgcn_readfirstlane(c);
-			FinRec q[kFinPer];
-			bool have[kFinPer];
-#pragma unroll
-			for (int j = 0; j < kFinPer; j++) {
-				const uint32_t pos = c + 64 * j + lane, slot = pos & (kRing - 1);
-				have[j] = false;
-				for (;;) {
-					if (lds_load_acq(&sh.ready[slot]) == pos + 1) {
-						have[j] = true;
-						break;
-					}
-					if (lds_load_acq(&sh.scan_done) == (uint32_t)kScanWaves && pos >= lds_load_acq(&sh.tail))
-						break;
-					__builtin_amdgcn_s_sleep(2);
+			const uint32_t pos = c + lane, slot = pos & (kRing - 1);
+			// 0: waiting, 1: the record is ready, 2: the scan ended before this position.
+			// The wave polls as a whole (a uniform loop): one conflict-free LDS read per lane
+			// and one lane reading the scan counters, then a sleep.
+			uint32_t st = 0;
+			for (;;) {
+				if (st == 0 && lds_load_acq(&sh.ready[slot]) == pos + 1)
+					st = 1;
+				if (__all(st != 0))
+					break;
+				uint32_t done = 0, tail = 0;
+				if (lane == 0) {
+					done = lds_load_acq(&sh.scan_done);
+					tail = lds_load_acq(&sh.tail);
 				}
-				if (have[j]) {
-					q[j] = sh.ring[slot];
-#if EBD_STAGE && EBD_FINPER == 0
-					{ // the staged bytes move to this lane's row, so the slot is free at once
-						const uint4* src = (const uint4*)(sh.rdata + slot * (kStage / 4));
-						uint4* dst = (uint4*)(sh.fstage + ((wave - kScanWaves) * 64 + lane) * (kStage / 4));
-#pragma unroll
-						for (uint32_t k = 0; k < kStage / 16; k++)
-							dst[k] = src[k];
-					}
-#endif
-					lds_store_rel(&sh.freed[slot], pos + 1);
-				} else {
-					q[j] = FinRec{};
+				done = __builtin_amdgcn_readfirstlane(done);
+				tail = __builtin_amdgcn_readfirstlane(tail);
+				if (done == (uint32_t)kScanWaves) { // every position below tail was pushed
+					if (st == 0 && pos >= tail)
+						st = 2;
+					if (__all(st != 0))
+						break;
 				}
+				__builtin_amdgcn_s_sleep(4);
 			}
-			if (!__any(have[0]))
+			if (!__any(st == 1))
 				break;
-#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
-#if EBD_FINPER == 0
-			if (have[0]) {
-#if EBD_STAGE
-				finalize_rec(d, T, q[0], StagedMem{(const uint8_t*)(uintptr_t)(q[0].pl & 0xffffffffffffull),
-						sh.fstage + ((wave - kScanWaves) * 64 + lane) * (kStage / 4), q[0].pad[0]});
-#else
-				finalize_rec(d, T, q[0], DevMem{(const uint8_t*)(uintptr_t)(q[0].pl & 0xffffffffffffull)});
-#endif
+			uint32_t q[R_WORDS];
+			if (st == 1) {
+#pragma unroll
+				for (uint32_t f = 0; f < R_WORDS; f++)
+					q[f] = sh.ring[f * kRing + slot];
+#pragma unroll
+				for (uint32_t j = 0; j < kStageWords; j++) // the staged bytes move to this lane's row
+					fs[j * kFinLanes] = sh.rdata[j * kRing + slot];
+				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
 			}
-#else
-			finalize_recs<kFinPer>(d, T, q, have);
-#endif
+#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
+			if (st == 1) {
+				if (q[R_POS] != pos + 1)
+					set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
+				else
+					finalize_rec(d, T, q, fs);
+			}
 #endif
 		}
 		return;
@@ -725,7 +621,7 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 
 	// ---- scan waves ----
 	const uint32_t sl = wave * 64 + lane; // scan lane
-	constexpr uint32_t kScanLanes = kScanWaves * 64;
+	uint32_t* stg = sh.stage + sl;        // this lane's staging row (word j at stg[j * kScanLanes])
 	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
 	// the lane's current event (e0) and the next one (e1, whose record arrives early)
 	LaneEv e0 = lane_ev(d, rb + sl, re);
@@ -750,35 +646,32 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 			if (pos >= kRing) // the slot's previous record must have been taken
 				while (lds_load_acq(&sh.freed[slot]) != pos - kRing + 1)
 					__builtin_amdgcn_s_sleep(1);
-			FinRec t;
-#if EBD_STAGE
-			{ // staged bytes equal the buffer's up to the scanned windows and the last chunk's end
-				const uint4* src = (const uint4*)(sh.stage + sl * (kStage / 4));
-				uint4* dst = (uint4*)(sh.rdata + slot * (kStage / 4));
+			// staged bytes equal the buffer's up to the scanned windows and the last chunk's end
+			const uint32_t scanned = min(64u * w0, kStage), chunks_end = (e0.L + 15u) & ~15u;
+			const unsigned long long a = (unsigned long long)(uintptr_t)e0.p;
+			uint32_t t[R_WORDS];
+			t[R_PLO] = (uint32_t)a;
+			t[R_PHI] = ((uint32_t)(a >> 32) & 0xffffu) | (e0.L << 16);
+			t[R_IDX] = e0.idx;
+			t[R_PID] = e0.pf;
+			t[R_SF] = s | (e0.flags << 8) | (sr.cseen << 16) | (post << 17);
+			t[R_CQM] = sr.cqm;
+			t[R_C01] = sr.url.c | (sr.host.c << 16);
+			t[R_C23] = sr.hend.c | (sr.cip.c << 16);
+			t[R_C4] = sr.term.c;
+			t[R_QS + 0] = sr.url.qs;
+			t[R_QS + 1] = sr.host.qs;
+			t[R_QS + 2] = sr.hend.qs;
+			t[R_QS + 3] = sr.cip.qs;
+			t[R_QS + 4] = sr.term.qs;
+			t[R_LIM] = min(scanned, chunks_end);
+			t[R_POS] = pos + 1;
 #pragma unroll
-				for (uint32_t k = 0; k < kStage / 16; k++)
-					dst[k] = src[k];
-				const uint32_t scanned = min(64u * w0, kStage), chunks_end = (e0.L + 15u) & ~15u;
-				t.pad[0] = min(scanned, chunks_end);
-			}
-#else
-			t.pad[0] = 0;
-#endif
-			t.pl = (unsigned long long)(uintptr_t)e0.p | ((unsigned long long)e0.L << 48);
-			t.idx = e0.idx;
-			t.pid = e0.pf;
-			t.sf = s | (e0.flags << 8) | (sr.cseen << 16) | (post << 17);
-			t.cqm = sr.cqm;
-			t.c01 = sr.url.c | (sr.host.c << 16);
-			t.c23 = sr.hend.c | (sr.cip.c << 16);
-			t.c4 = sr.term.c;
-			t.qs[0] = sr.url.qs;
-			t.qs[1] = sr.host.qs;
-			t.qs[2] = sr.hend.qs;
-			t.qs[3] = sr.cip.qs;
-			t.qs[4] = sr.term.qs;
-			t.pad[1] = 0;
-			sh.ring[slot] = t;
+			for (uint32_t f = 0; f < R_WORDS; f++)
+				sh.ring[f * kRing + slot] = t[f];
+#pragma unroll
+			for (uint32_t j = 0; j < kStageWords; j++)
+				sh.rdata[j * kRing + slot] = stg[j * kScanLanes];
 			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
 	};
@@ -817,39 +710,13 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		const uint32_t pc = (w << 2) | (last << 16); // window's first chunk | last chunk
 		unsigned long long ak[4];
 		uint32_t pk[4];
-#ifdef EBD_BPERM_ADDR // experiment: quad broadcast through ds_bpermute instead of DPP
-		{
-			const int qb = (int)((threadIdx.x & 63u) & ~3u) * 4;
-#pragma unroll
-			for (int k = 0; k < 4; k++) {
-				const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)(uint32_t)a);
-				const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)(uint32_t)(a >> 32));
-				ak[k] = (unsigned long long)lo | ((unsigned long long)hi << 32);
-				pk[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(qb + 4 * k, (int)pc);
-			}
-		}
-#else
 		ak[0] = qbcast64<0>(a), pk[0] = qbcast<0>(pc);
 		ak[1] = qbcast64<1>(a), pk[1] = qbcast<1>(pc);
 		ak[2] = qbcast64<2>(a), pk[2] = qbcast<2>(pc);
 		ak[3] = qbcast64<3>(a), pk[3] = qbcast<3>(pc);
-#endif
 #pragma unroll
 		for (int k = 0; k < 4; k++) {
 			const uint32_t c = min((pk[k] & 0xffffu) + r, pk[k] >> 16);
-#ifdef EBD_DBG_CHECK2
-			if (ak[k] - (uintptr_t)d.payload >= (1ull << 36)) {
-				atomicOr(&d.ctr[CTR_ERRORS], 1ull << 61);
-				ak[k] = (uintptr_t)d.payload;
-			}
-#endif
-#ifdef EBD_DBG_CHECK
-			if (ak[k] < (uintptr_t)d.payload || ak[k] >= (uintptr_t)d.payload + (1ull << 36)) {
-				printf("EBD_DBG issue: block %u thread %u k %d a-payload %lld c %u\n", blockIdx.x, threadIdx.x, k,
-						(long long)(ak[k] - (uintptr_t)d.payload), c);
-				ak[k] = (uintptr_t)d.payload;
-			}
-#endif
 			W[k] = gload16((uintptr_t)(ak[k] + 16ull * c));
 		}
 	};
@@ -879,21 +746,18 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		transpose_quad(X, r);
 		bool done = false;
 		if (valid) {
-			if (w0 == 0)
+			if (w0 == 0) {
 				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
-#if EBD_STAGE
-			if (64 * w0 < kStage) { // this window's chunks into the lane's staging row
-				uint4* st = (uint4*)(sh.stage + sl * (kStage / 4)) + 4 * w0;
 #pragma unroll
-				for (int k = 0; k < 4; k++)
-					if (64 * w0 + 16 * k < kStage)
-						st[k] = make_uint4(X[k].w[0], X[k].w[1], X[k].w[2], X[k].w[3]);
+				for (int k = 0; k < 4; k++) // window 0 into the lane's staging row
+#pragma unroll
+					for (int j = 0; j < 4; j++)
+						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
 			}
-#endif
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
-				scan_chunk(T, X[k], sx, m, qs, qm);
+				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm);
 				if (live) {
 					const uint32_t c = 4 * w0 + k;
 					chunk_update(di, sr, c, s, qs, qm, m);

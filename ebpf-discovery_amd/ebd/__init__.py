@@ -23,7 +23,7 @@ STATUS_NONE, STATUS_UNFINISHED, STATUS_FINISHED, STATUS_INVALID = 0, 1, 2, 3
 INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING = 0x01, 0x02, 0x04, 0x08, 0x40
 CLASS_NONE, CLASS_INTERNAL, CLASS_EXTERNAL = 0, 1, 2
 ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "VERIFY_FULL", 32: "BAD_INPUT",
-            64: "COLLISION"}
+            64: "COLLISION", 128: "INTERNAL"}
 
 EVENT_DTYPE = np.dtype([("pid", "<u4"), ("fd", "<u4"), ("sessionID", "<u4"), ("bufferSeq", "<u4"),
                         ("sourceIP", "u1", (16,)), ("flags", "u1"), ("pad", "u1", (3,))])
@@ -115,6 +115,7 @@ _SIGS = {
                                             C.c_void_p, C.c_uint64, C.c_void_p]),
     # testing header
     "ebd_host_dfa_info": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "ebd_host_dfa_next": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
                                  C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ebd_host_gp_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
@@ -381,14 +382,23 @@ def generate_device(ctx, config, seed, first, n, events, lens, offs, payload, pa
 
 # ---- host hooks (product semantics on the CPU, for tests) -------------------------------
 def dfa_info():
-    a = np.zeros(11, np.uint32)
-    _check(lib().ebd_host_dfa_info(_p(a), 11), "dfa_info")
-    keys = ["nstates", "url_id", "g2", "g3", "g4", "hvc0", "hvh", "fin0", "fin1", "inv", "init"]
+    a = np.zeros(13, np.uint32)
+    _check(lib().ebd_host_dfa_info(_p(a), 13), "dfa_info")
+    keys = ["nstates", "url_id", "g2", "g3", "g4", "hvc0", "hvh", "fin0", "fin1", "inv", "init", "vl0", "vl1"]
     return dict(zip(keys, (int(x) for x in a)))
 
 
 def _hkey(hash_key):
     return np.array(hash_key if hash_key is not None else TEST_HASH_KEY, np.uint64)
+
+
+def dfa_next():
+    """The fast-path DFA's transitions as an [nstates, 256] uint8 array."""
+    t = np.zeros(256 * 256, np.uint8)
+    n = lib().ebd_host_dfa_next(_p(t), t.size)
+    if n < 0:
+        raise EbdError("ebd_host_dfa_next")
+    return t.reshape(256, 256)[:n].copy()
 
 
 def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_DATA, src16=bytes(16), v4=(), v6=(),

@@ -161,6 +161,7 @@ typedef struct ebd_stats {
 #define EBD_ERR_VERIFY_FULL 16u    /* deferred key-verification list exhausted */
 #define EBD_ERR_BAD_INPUT 32u      /* len > EBD_BUFFER_MAX_DATA_SIZE, bad offsets */
 #define EBD_ERR_COLLISION 64u      /* two keys share a 64-bit tag (results not trusted) */
+#define EBD_ERR_INTERNAL 128u      /* a kernel-internal consistency check failed (results not trusted) */
 
 typedef struct ebd_config {
 	int device;                /* HIP device ordinal */

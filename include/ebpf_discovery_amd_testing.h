@@ -17,6 +17,8 @@ extern "C" {
 
 /* DFA layout: nstates, url_id, g2, g3, g4, hvc0, hvh, fin0, fin1, inv, init. */
 int ebd_host_dfa_info(uint32_t* info, uint32_t n);
+/* The DFA's transition table next[s * 256 + byte] (cap >= 65536); returns nstates. */
+int ebd_host_dfa_next(uint8_t* out, uint32_t cap);
 
 /* The fast path (k_fresh's per-event logic) for one buffer; key = its service key under
  * hash_key (ebd_config.hash_key). */

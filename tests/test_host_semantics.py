@@ -358,3 +358,17 @@ def test_generator_is_deterministic_and_shaped():
     assert (l1 == 35).all() and (ev1["pid"] == 1000).all()
     _, l16, o16, _ = ebd.generate_host(3, 3, 0, 100, align=16)
     assert (o16 % 16 == 0).all()
+
+
+def test_word_skip_states_are_printable_self_loops():
+    """k_fresh skips a 4-byte word without table reads when its start state is di.vl0 or
+    di.vl1 and every byte is in [0x20, 0x7e]: exact only if those states step to themselves
+    on each such byte (the generic header-value states, HEADER_VALUE of a non-Host,
+    non-client key, HttpRequestParser.cpp:321-352 with V-class = printable ASCII)."""
+    info = ebd.dfa_info()
+    T = ebd.dfa_next()
+    vls = [v for v in (info["vl0"], info["vl1"]) if v != 0xFFFFFFFF]
+    assert len(vls) == 2 and all(v not in (info["fin0"], info["fin1"], info["inv"]) for v in vls)
+    for v in vls:
+        assert np.all(T[v, 0x20:0x7F] == v)
+        assert T[v, ord("\r")] != v  # CR ends the value
