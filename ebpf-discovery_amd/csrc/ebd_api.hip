@@ -19,6 +19,12 @@ hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_carry_insert(const Dev& d, hipStream_t st);
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
+struct SessState;
+hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* minus, int* scan, void* tmp, size_t tmp_bytes,
+		hipStream_t st, int cus);
+hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
+		uint32_t cap, hipStream_t st, int cus);
+size_t sess_state_bytes();
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
@@ -45,7 +51,7 @@ using namespace ebd;
 
 // the layouts the Python binding (ebd/__init__.py) and tests/test_abi.py assume
 static_assert(sizeof(ebd_config) == 56, "ebd_config layout");
-static_assert(sizeof(ebd_stats) == 72, "ebd_stats layout");
+static_assert(sizeof(ebd_stats) == 88, "ebd_stats layout");
 static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 64, "result layouts");
 
 #define HIP_TRY(x)                                                                                                   \
@@ -115,6 +121,17 @@ struct ebd_ctx {
 	uint64_t* d_off = nullptr;
 	uint8_t* d_payload = nullptr;
 	uint64_t payload_cap = 0;
+	// exact LRU (allocated on first need): bound arrays, event -> position, session states
+	int* d_lru_delta = nullptr;
+	uint8_t* d_lru_minus = nullptr;
+	int* d_lru_scan = nullptr;
+	void* d_lru_tmp = nullptr;
+	size_t lru_tmp_bytes = 0;
+	uint32_t* d_lru_jpos = nullptr;
+	uint32_t* d_lru_head = nullptr;
+	void* d_lru_sess = nullptr;
+	uint32_t* d_lru_live = nullptr;
+	uint64_t lru_batches_exact = 0;
 	// bookkeeping
 	unsigned long long seq_base = 0;
 	uint32_t last_n = 0;
@@ -211,7 +228,8 @@ static Dev make_dev(ebd_ctx* c) {
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
-			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload};
+			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload, c->d_lru_delta, c->d_lru_minus,
+			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live};
 	for (void* p : ptrs)
 		if (p)
 			(void)hipFree(p);
@@ -430,9 +448,48 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 					end_bit, c->stream);
 		}));
 		d.slow_keys = c->d_slow[1];
-		HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk(d, (uint32_t)nslow, c->stream, c->cus); }));
-		if (c->n_carry)
-			HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
+		// LRU eviction possible?  Only if more sessions than its capacity could be live at once
+		// (k_walk_lru's comment): first the cheap count of candidate sessions, then the bound.
+		bool exact = false;
+		if (c->h_ctr[CTR_DIRTY] > c->carry_cap) {
+			const uint64_t nb = (uint64_t)c->max_events;
+			if (!c->d_lru_delta) {
+				HIP_TRY(hipMalloc(&c->d_lru_delta, nb * sizeof(int)));
+				HIP_TRY(hipMalloc(&c->d_lru_minus, nb));
+				HIP_TRY(hipMalloc(&c->d_lru_scan, nb * sizeof(int)));
+				HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, c->lru_tmp_bytes, c->d_lru_delta, c->d_lru_scan,
+						(int)c->max_events, c->stream));
+				HIP_TRY(hipMalloc(&c->d_lru_tmp, c->lru_tmp_bytes + 16));
+			}
+			HIP_TRY(hipMemsetAsync(c->d_lru_delta, 0, (size_t)n * sizeof(int), c->stream));
+			HIP_TRY(hipMemsetAsync(c->d_lru_minus, 0, n, c->stream));
+			size_t tb = c->lru_tmp_bytes;
+			HIP_TRY(launch_lru_bound(d, (uint32_t)nslow, c->d_lru_delta, c->d_lru_minus, c->d_lru_scan, c->d_lru_tmp, tb, c->stream,
+					c->cus));
+			HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+			HIP_TRY(hipStreamSynchronize(c->stream));
+			const unsigned long long pk = c->h_ctr[CTR_LRU_PEAK];
+			const long long peak = pk ? (long long)pk - (1ll << 31) : 0;
+			exact = (long long)c->n_carry + peak > (long long)c->carry_cap;
+		}
+		if (exact) {
+			c->lru_batches_exact++;
+			if (!c->d_lru_jpos) {
+				HIP_TRY(hipMalloc(&c->d_lru_jpos, (size_t)c->max_events * sizeof(uint32_t)));
+				HIP_TRY(hipMalloc(&c->d_lru_head, (size_t)c->max_events * sizeof(uint32_t)));
+				HIP_TRY(hipMalloc(&c->d_lru_sess, ((size_t)c->max_events + c->carry_cap) * sess_state_bytes()));
+				HIP_TRY(hipMalloc(&c->d_lru_live, ((size_t)c->carry_cap + 1) * sizeof(uint32_t)));
+			}
+			HIP_TRY(hipMemsetAsync(c->d_lru_jpos, 0xff, (size_t)n * sizeof(uint32_t), c->stream));
+			HIP_TRY(timed(c, KT_WALK, [&] {
+				return launch_walk_lru(d, (uint32_t)nslow, c->d_lru_jpos, c->d_lru_head, (SessState*)c->d_lru_sess, c->d_lru_live,
+						c->carry_cap, c->stream, c->cus);
+			}));
+		} else {
+			HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk(d, (uint32_t)nslow, c->stream, c->cus); }));
+			if (c->n_carry)
+				HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
+		}
 	}
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
@@ -682,6 +739,7 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_service* recs, uint32_t n, c
 	Dev d = make_dev(c);
 	d.n = 0;
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_EVICTIONS, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_merge(d, recs, n, strings, c->stream, c->cus));
 	HIP_TRY(launch_verify(d, c->stream, c->cus));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -703,6 +761,8 @@ int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 	s->live_sessions = c->n_carry;
 	s->max_live_sessions = c->max_live;
 	s->hash_collisions = c->h_ctr[CTR_COLLISIONS];
+	s->lru_evictions = c->h_ctr[CTR_EVICTIONS_TOTAL];
+	s->lru_exact_batches = c->lru_batches_exact;
 	s->services = c->h_ctr[CTR_SERVICES];
 	s->errors = c->h_ctr[CTR_ERRORS];
 	return 0;

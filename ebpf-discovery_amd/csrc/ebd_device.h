@@ -29,11 +29,14 @@ struct SSlot {
 	unsigned long long tag;
 	unsigned long long kv; // fd << 32 | pid
 	unsigned int sid;
-	unsigned int pad;
-	unsigned int carry; // 1 + index into the carried-session array, 0 = none
+	unsigned int first_c;  // ~(first event of the batch whose fresh parse was UNFINISHED), 0 = none (atomicMax)
+	unsigned int carry;    // 1 + index into the carried-session array, 0 = none
 	unsigned int visited;
+	unsigned int last_ev;  // 1 + the session's last event in the batch (atomicMax)
+	unsigned int pad;
+	unsigned long long pad2;
 };
-static_assert(sizeof(SSlot) == 32, "session slot is 32 bytes");
+static_assert(sizeof(SSlot) == 48, "session slot is 48 bytes");
 
 constexpr uint32_t kCarryBytes = 8200; // > DISCOVERY_MAX_HTTP_REQUEST_LENGTH + 1
 
@@ -41,6 +44,7 @@ constexpr uint32_t kCarryBytes = 8200; // > DISCOVERY_MAX_HTTP_REQUEST_LENGTH + 
 // its parser state and the bytes of the request in progress.
 struct Carry {
 	uint32_t pid, fd, sid, nbytes;
+	unsigned long long stamp; // global order of the event that last found or inserted it (LRU recency)
 	GenParser g;
 	uint8_t bytes[kCarryBytes];
 };
@@ -68,15 +72,18 @@ enum Ctr : uint32_t {
 	CTR_DIRTY,          // session-set slots claimed in this batch
 	CTR_INSERTS,        // LRU inserts in this batch
 	CTR_VERIFY,         // deferred service-key verifications
-	CTR_BATCH_END = 9,
-	CTR_SARENA = 9,     // service string arena bytes used
+	CTR_LRU_PEAK,       // 2^31 + max over the batch of (live sessions - carried), upper bound (k_lru_peak)
+	CTR_EVICTIONS,      // LRU evictions in this batch (exact path)
+	CTR_BATCH_END = 11,
+	CTR_SARENA = 11,    // service string arena bytes used
 	CTR_ERRORS,         // EBD_ERR_* bitmask
 	CTR_COLLISIONS,
 	CTR_KDELETES,
 	CTR_REQUESTS,
 	CTR_SESSION_EVENTS,
-	CTR_SERVICES,       // services in the table (sum of CTR_NEW over batches)
-	CTR_COUNT = 16,
+	CTR_SERVICES,       // length of the claimed-slot list (services in the table)
+	CTR_EVICTIONS_TOTAL,
+	CTR_COUNT = 19,
 };
 
 struct VerifyRec {

@@ -13,6 +13,8 @@
 //   k_reps          first-arrival domain / scheme / endpoint string for new services
 #include <hip/hip_runtime.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "ebd_device.h"
 #include "ebd_fresh.h"
 
@@ -168,7 +170,9 @@ __device__ __forceinline__ unsigned long long sset_tag(unsigned long long kv, ui
 	return fmix64(kv ^ ((unsigned long long)sid * 0x9E3779B97F4A7C15ull) ^ 0x5bd1e9955bd1e995ull) | 1ull;
 }
 
-__device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry) {
+// ev: the event whose fresh parse was UNFINISHED (kNone for a carried session): the first
+// such event of the batch bounds when the session can have entered the LRU (k_lru_delta).
+__device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry, uint32_t ev) {
 	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
 	const unsigned long long tag = sset_tag(kv, sid);
 	uint32_t idx = (uint32_t)tag & d.sset_mask;
@@ -198,6 +202,8 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 	}
 	if (carry)
 		d.sset[res].carry = carry;
+	if (ev != kNone)
+		atomicMax(&d.sset[res].first_c, ~ev);
 	return res;
 }
 
@@ -431,7 +437,7 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	d.res[i] = r;
 	const EventRec& ev = d.ev[i];
 	atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
+	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 }
 
 // A finished scan waiting for fresh_finalize: 16 words, kept in the ring as 16 arrays of
@@ -531,7 +537,7 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
 		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
-		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0);
+		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 	}
 	d.res[i] = fr.r;
 }
@@ -820,7 +826,7 @@ __device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_e
 __global__ void k_carry_insert(Dev d) {
 	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d.n_carry_in; c += gridDim.x * blockDim.x) {
 		const Carry& cr = d.carry_in[c];
-		sset_insert(d, cr.pid, cr.fd, cr.sid, c + 1);
+		sset_insert(d, cr.pid, cr.fd, cr.sid, c + 1, kNone);
 	}
 }
 
@@ -833,6 +839,7 @@ __global__ void k_slow_collect(Dev d) {
 			continue;
 		const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
 		if (slot >= 0) {
+			atomicMax(&d.sset[slot].last_ev, i + 1);
 			const unsigned long long k = atomicAdd(&d.ctr[CTR_SLOW], 1ull);
 			d.slow_keys[k] = ((unsigned long long)(uint32_t)slot << 32) | i;
 		}
@@ -961,108 +968,148 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	r.u.session.index = (uint32_t)q;
 }
 
-__device__ void walk_session(const Dev& d, uint32_t j, uint32_t nslow, uint32_t slot) {
+// A session as the walkers hold it: the parser (Session, Discovery.h), the request in
+// progress (Walk), whether it is in the LRU (savedSessions) and when it was last found or
+// inserted there (LRU recency; Discovery.cpp:114 find and :215 insert both touch it).
+struct SessState {
+	GenParser g;
+	Walk w;
+	unsigned long long stamp;
+	uint32_t live;
+	uint32_t li; // position in the exact walker's live list
+};
+
+enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
+
+// Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
+// session's state in S.  Returns the LRU operation it implies; an insert (saveSession,
+// Discovery.cpp:148-150) is left to the caller, which may have to evict first.
+__device__ uint32_t session_event(const Dev& d, SessState& S, uint32_t jj) {
+	const uint32_t i = slow_event(d, jj);
+	const EventRec& ev = d.ev[i];
+	const uint8_t flags = ev.flags;
+	const uint32_t L = d.len[i];
+	const KeyTrie* trie = d.trie;
+	ebd_event_result r;
+	r.consumed = 0;
+	r.status = EBD_STATUS_NONE;
+	r.info = EBD_INFO_SESSION;
+	r.u.session.index = 0xffffffffu;
+	r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
+	atomicAdd(&d.ctr[CTR_SESSION_EVENTS], 1ull);
+	uint32_t op = OP_NONE;
+	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
+		const uint8_t* buf = d.payload + d.off[i];
+		auto at = [buf](uint32_t k) { return (uint32_t)buf[k]; };
+		if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
+			S.stamp = d.seq_base + i;
+			r.info |= EBD_INFO_EXISTING;
+			const uint32_t c = gp_parse(S.g, trie, at, L, flags);
+			r.consumed = (uint16_t)c;
+			if (S.g.state == ST_INVALID) {
+				r.status = EBD_STATUS_INVALID;
+				atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
+				S.live = 0;
+				op = OP_ERASE;
+			} else if (S.g.state == ST_FINISHED) {
+				r.status = EBD_STATUS_FINISHED;
+				emit_session_request(d, S.w, jj, c, S.g, i, r);
+				gp_reset(S.g); // session.reset(); stays saved
+				S.w = Walk{nullptr, 0, jj + 1};
+			} else {
+				r.status = EBD_STATUS_UNFINISHED;
+			}
+		} else { // handleNewSession, Discovery.cpp:141-159
+			gp_init(S.g);
+			S.w = Walk{nullptr, 0, jj};
+			const uint32_t c = gp_parse(S.g, trie, at, L, flags);
+			r.consumed = (uint16_t)c;
+			if (S.g.state == ST_INVALID) {
+				r.status = EBD_STATUS_INVALID;
+			} else if (S.g.state == ST_FINISHED) {
+				r.status = EBD_STATUS_FINISHED;
+				emit_session_request(d, S.w, jj, c, S.g, i, r);
+			} else {
+				r.status = EBD_STATUS_UNFINISHED;
+				if (!(flags & FLAG_END))
+					op = OP_INSERT;
+			}
+		}
+	}
+	if ((flags & FLAG_END) && S.live) { // handleCloseEvent, Discovery.cpp:194-198
+		S.live = 0;
+		op = OP_ERASE;
+	}
+	d.res[i] = r;
+	return op;
+}
+
+// The session's state at its first event of the batch (sorted position j).
+__device__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t slot) {
 	SSlot* ss = d.sset + slot;
 	ss->visited = 1;
-	GenParser g;
-	bool live = false;
-	Walk w{nullptr, 0, j};
+	S.w = Walk{nullptr, 0, j};
+	S.li = kNone;
 	const uint32_t carry = ss->carry;
 	if (carry) { // saved session from an earlier batch (LRU entry)
 		const Carry& c = d.carry_in[carry - 1];
-		g = c.g;
-		live = true;
-		w.cb = c.bytes;
-		w.clen = c.nbytes;
+		S.g = c.g;
+		S.live = 1;
+		S.stamp = c.stamp;
+		S.w.cb = c.bytes;
+		S.w.clen = c.nbytes;
 	} else {
-		gp_init(g);
-	}
-	const KeyTrie* trie = d.trie;
-	uint32_t jj = j;
-	for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
-		const uint32_t i = slow_event(d, jj);
-		const EventRec& ev = d.ev[i];
-		const uint8_t flags = ev.flags;
-		const uint32_t L = d.len[i];
-		ebd_event_result r;
-		r.consumed = 0;
-		r.status = EBD_STATUS_NONE;
-		r.info = EBD_INFO_SESSION;
-		r.u.session.index = 0xffffffffu;
-		r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
-		atomicAdd(&d.ctr[CTR_SESSION_EVENTS], 1ull);
-		if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
-			const uint8_t* buf = d.payload + d.off[i];
-			auto at = [buf](uint32_t k) { return (uint32_t)buf[k]; };
-			if (live) { // handleExistingSession, Discovery.cpp:123-139
-				r.info |= EBD_INFO_EXISTING;
-				const uint32_t c = gp_parse(g, trie, at, L, flags);
-				r.consumed = (uint16_t)c;
-				if (g.state == ST_INVALID) {
-					r.status = EBD_STATUS_INVALID;
-					atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
-					live = false;
-				} else if (g.state == ST_FINISHED) {
-					r.status = EBD_STATUS_FINISHED;
-					emit_session_request(d, w, jj, c, g, i, r);
-					gp_reset(g); // session.reset(); stays saved
-					w = Walk{nullptr, 0, jj + 1};
-				} else {
-					r.status = EBD_STATUS_UNFINISHED;
-				}
-			} else { // handleNewSession, Discovery.cpp:141-159
-				gp_init(g);
-				w = Walk{nullptr, 0, jj};
-				const uint32_t c = gp_parse(g, trie, at, L, flags);
-				r.consumed = (uint16_t)c;
-				if (g.state == ST_INVALID) {
-					r.status = EBD_STATUS_INVALID;
-				} else if (g.state == ST_FINISHED) {
-					r.status = EBD_STATUS_FINISHED;
-					emit_session_request(d, w, jj, c, g, i, r);
-				} else {
-					r.status = EBD_STATUS_UNFINISHED;
-					if (!(flags & FLAG_END)) {
-						live = true; // saveSession
-						atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
-					}
-				}
-			}
-		}
-		if (flags & FLAG_END) // handleCloseEvent, Discovery.cpp:194-198
-			live = false;
-		d.res[i] = r;
-	}
-	if (live) { // saved for the next batch, with the bytes of the request in progress
-		const unsigned long long c = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
-		if (c >= d.carry_cap) {
-			set_error(d, EBD_ERR_LRU_OVERFLOW);
-			return;
-		}
-		Carry& out = d.carry_out[c];
-		const EventRec& ev = d.ev[slow_event(d, j)];
-		out.pid = ev.pid;
-		out.fd = ev.fd;
-		out.sid = ev.sessionID;
-		out.g = g;
-		const uint32_t nb = g.length < kCarryBytes ? g.length : kCarryBytes;
-		out.nbytes = nb;
-		uint32_t k = 0;
-		uint8_t* dst = out.bytes;
-		// the request in progress ends with the last event of this session (fully consumed)
-		stream_visit(d, w, jj - 1, piece_len(d, jj - 1), 0, nb, [&](uint8_t b) {
-			dst[k++] = b;
-			return true;
-		});
+		gp_init(S.g);
+		S.live = 0;
+		S.stamp = 0;
 	}
 }
 
+// A session still in the LRU after the batch, with the bytes of its request in progress
+// (which ends with the session's last event jlast of the batch, fully consumed).
+__device__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, uint32_t jlast) {
+	const unsigned long long c = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
+	if (c >= d.carry_cap) {
+		set_error(d, EBD_ERR_LRU_OVERFLOW);
+		return;
+	}
+	Carry& out = d.carry_out[c];
+	const EventRec& ev = d.ev[slow_event(d, j)];
+	out.pid = ev.pid;
+	out.fd = ev.fd;
+	out.sid = ev.sessionID;
+	out.stamp = S.stamp;
+	out.g = S.g;
+	const uint32_t nb = S.g.length < kCarryBytes ? S.g.length : kCarryBytes;
+	out.nbytes = nb;
+	uint32_t k = 0;
+	uint8_t* dst = out.bytes;
+	stream_visit(d, S.w, jlast, piece_len(d, jlast), 0, nb, [&](uint8_t b) {
+		dst[k++] = b;
+		return true;
+	});
+}
+
+// The parallel session path: one lane per session, events in order.  Exact while no LRU
+// eviction can happen (run_batch checks an upper bound of the live sessions first).
 __global__ void k_walk(Dev d, uint32_t nslow) {
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
 		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
 		if (j > 0 && (uint32_t)(d.slow_keys[j - 1] >> 32) == slot)
 			continue;
-		walk_session(d, j, nslow, slot);
+		SessState S;
+		session_begin(d, S, j, slot);
+		uint32_t jj = j;
+		for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
+			const uint32_t op = session_event(d, S, jj);
+			if (op == OP_INSERT) {
+				S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
+				S.stamp = d.seq_base + slow_event(d, jj);
+				atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
+			}
+		}
+		if (S.live)
+			session_carry_out(d, S, j, jj - 1);
 	}
 }
 
@@ -1082,10 +1129,230 @@ __global__ void k_carry_pass(Dev d) {
 		out.pid = cr.pid;
 		out.fd = cr.fd;
 		out.sid = cr.sid;
+		out.stamp = cr.stamp;
 		out.g = cr.g;
 		out.nbytes = cr.nbytes;
 		for (uint32_t b = 0; b < cr.nbytes; b++)
 			out.bytes[b] = cr.bytes[b];
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// Exact LRU (LRUCache.h:50-89, capacity EBD_MAX_SESSIONS, Discovery.cpp:39).
+//
+// Eviction couples sessions, so the parallel walker is exact only while the LRU never
+// holds more than its capacity.  An upper bound decides: a session can be in the LRU only
+// from its first event whose fresh parse was UNFINISHED (the only way in is saveSession
+// after such a parse) or from before the batch (carried), until its last event if that one
+// closes it.  k_lru_delta marks +1 / -1 at those events, a scan gives the running count,
+// and k_lru_peak its maximum.  When carried + peak <= capacity no insert can find the cache
+// full; otherwise the batch's session events run through k_walk_lru, which replays them in
+// event order with a real LRU: find / insert touch, an insert into a full cache evicts the
+// least recently used session (which then parses its next buffer as a new session,
+// Discovery.cpp:141), close and INVALID erase.
+// ---------------------------------------------------------------------------------
+__global__ void k_lru_delta(Dev d, uint32_t nslow, int* delta, uint8_t* minus) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
+		const uint32_t i = slow_event(d, j);
+		const SSlot& ss = d.sset[(uint32_t)(d.slow_keys[j] >> 32)];
+		const bool carried = ss.carry != 0;
+		const uint32_t first = ss.first_c ? ~ss.first_c : kNone;
+		const bool plus = !carried && first == i;
+		const bool close = (d.ev[i].flags & FLAG_END) && i + 1 == ss.last_ev && (carried || (first != kNone && first <= i));
+		delta[i] = (plus ? 1 : 0) - (close ? 1 : 0);
+		minus[i] = close ? 1 : 0;
+	}
+}
+
+// max over events of (running count before the event's close) = scan[i] + minus[i]
+__global__ void k_lru_peak(const int* scan, const uint8_t* minus, uint32_t n, unsigned long long* ctr) {
+	__shared__ int red[256];
+	int m = 0;
+	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+		m = max(m, scan[i] + (int)minus[i]);
+	red[threadIdx.x] = m;
+	__syncthreads();
+	for (uint32_t s = blockDim.x / 2; s > 0; s >>= 1) {
+		if (threadIdx.x < s)
+			red[threadIdx.x] = max(red[threadIdx.x], red[threadIdx.x + s]);
+		__syncthreads();
+	}
+	if (threadIdx.x == 0)
+		atomicMax(&ctr[CTR_LRU_PEAK], (unsigned long long)red[0] + (1ull << 31));
+}
+
+// Event -> sorted position (kNone for events of no session in the set) and each sorted
+// position's session head.
+__global__ void k_lru_index(Dev d, uint32_t nslow, uint32_t* jpos, uint32_t* head) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
+		jpos[slow_event(d, j)] = j;
+		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
+		if (j > 0 && (uint32_t)(d.slow_keys[j - 1] >> 32) == slot)
+			continue;
+		for (uint32_t jj = j; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++)
+			head[jj] = j;
+	}
+}
+
+constexpr int kLruThreads = 256;
+
+__device__ __forceinline__ void live_add(SessState* S, uint32_t* live, uint32_t& nlive, uint32_t h) {
+	S[h].li = nlive;
+	live[nlive++] = h;
+}
+__device__ __forceinline__ void live_remove(SessState* S, uint32_t* live, uint32_t& nlive, uint32_t h) {
+	const uint32_t k = S[h].li, last = live[--nlive];
+	live[k] = last;
+	S[last].li = k;
+	S[h].li = kNone;
+}
+
+// The exact walker: one workgroup.  Lane 0 replays the session events in event order; at an
+// insert into a full cache the workgroup finds the least recently used session together.
+__global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow, const uint32_t* jpos, const uint32_t* head,
+		SessState* S, uint32_t* live, uint32_t cap) {
+	__shared__ uint32_t ord[kLruThreads];
+	__shared__ uint32_t nord, nlive, k_next, evict_for;
+	__shared__ unsigned long long rs[kLruThreads];
+	__shared__ uint32_t ri[kLruThreads];
+	const uint32_t t = threadIdx.x;
+	if (t == 0)
+		nlive = 0;
+	__syncthreads();
+	// every session's state at the batch start; the carried ones are in the LRU
+	for (uint32_t j = t; j < nslow; j += kLruThreads)
+		if (head[j] == j) {
+			session_begin(d, S[j], j, (uint32_t)(d.slow_keys[j] >> 32));
+			if (S[j].live) {
+				const uint32_t k = atomicAdd(&nlive, 1u);
+				S[j].li = k;
+				live[k] = j;
+			}
+		}
+	__syncthreads();
+	// carried sessions without an event in this batch are in the LRU too (handles nslow + c)
+	for (uint32_t c = t; c < d.n_carry_in; c += kLruThreads) {
+		const Carry& cr = d.carry_in[c];
+		const int slot = sset_find(d, cr.pid, cr.fd, cr.sid);
+		if (slot >= 0 && d.sset[slot].visited)
+			continue;
+		SessState& x = S[nslow + c];
+		x.live = 1;
+		x.stamp = cr.stamp;
+		const uint32_t k = atomicAdd(&nlive, 1u);
+		x.li = k;
+		live[k] = nslow + c;
+	}
+	__syncthreads();
+	for (uint32_t base = 0; base < d.n; base += kLruThreads) {
+		// this chunk's session events, in event order
+		const uint32_t i = base + t;
+		const uint32_t jp = i < d.n ? jpos[i] : kNone;
+		if (t == 0)
+			nord = 0;
+		__syncthreads();
+		const unsigned long long b = __ballot(jp != kNone);
+		__shared__ uint32_t wcount[kLruThreads / 64];
+		if ((t & 63) == 0)
+			wcount[t >> 6] = (uint32_t)__popcll(b);
+		__syncthreads();
+		uint32_t off = 0;
+		for (uint32_t w = 0; w < (t >> 6); w++)
+			off += wcount[w];
+		if (jp != kNone)
+			ord[off + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))] = jp;
+		if (t == kLruThreads - 1)
+			nord = off + (uint32_t)__popcll(b);
+		__syncthreads();
+		uint32_t k = 0;
+		while (k < nord) { // uniform
+			if (t == 0) {
+				uint32_t e = kNone;
+				for (; k < nord; k++) {
+					const uint32_t jj = ord[k], h = head[jj];
+					const uint32_t op = session_event(d, S[h], jj);
+					if (op == OP_ERASE && S[h].li != kNone) {
+						live_remove(S, live, nlive, h);
+					} else if (op == OP_INSERT) {
+						if (nlive >= cap) { // LRUCache.h:56-58: pop the tail first
+							e = h;
+							k++;
+							break;
+						}
+						S[h].live = 1;
+						S[h].stamp = d.seq_base + slow_event(d, jj);
+						live_add(S, live, nlive, h);
+						atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
+					}
+				}
+				k_next = k;
+				evict_for = e;
+			}
+			__syncthreads();
+			k = k_next;
+			if (evict_for != kNone) { // the least recently used live session
+				unsigned long long best = ~0ull;
+				uint32_t bi = kNone;
+				for (uint32_t x = t; x < nlive; x += kLruThreads) {
+					const unsigned long long st = S[live[x]].stamp;
+					if (st < best) {
+						best = st;
+						bi = live[x];
+					}
+				}
+				rs[t] = best;
+				ri[t] = bi;
+				__syncthreads();
+				for (uint32_t s = kLruThreads / 2; s > 0; s >>= 1) {
+					if (t < s && rs[t + s] < rs[t]) {
+						rs[t] = rs[t + s];
+						ri[t] = ri[t + s];
+					}
+					__syncthreads();
+				}
+				if (t == 0) {
+					const uint32_t v = ri[0], h = evict_for;
+					if (v != kNone) {
+						S[v].live = 0; // evicted: its next buffer starts a new session
+						live_remove(S, live, nlive, v);
+						atomicAdd(&d.ctr[CTR_EVICTIONS], 1ull);
+					}
+					const uint32_t jj = ord[k - 1];
+					S[h].live = 1;
+					S[h].stamp = d.seq_base + slow_event(d, jj);
+					live_add(S, live, nlive, h);
+					atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
+				}
+			}
+			__syncthreads();
+		}
+	}
+	// the sessions left in the LRU are saved for the next batch
+	for (uint32_t x = t; x < nlive; x += kLruThreads) {
+		const uint32_t h = live[x];
+		if (h >= nslow) { // untouched carried session: saved unchanged
+			const Carry& cr = d.carry_in[h - nslow];
+			const unsigned long long c = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
+			if (c >= d.carry_cap) {
+				set_error(d, EBD_ERR_LRU_OVERFLOW);
+				continue;
+			}
+			Carry& out = d.carry_out[c];
+			out.pid = cr.pid;
+			out.fd = cr.fd;
+			out.sid = cr.sid;
+			out.stamp = cr.stamp;
+			out.g = cr.g;
+			out.nbytes = cr.nbytes;
+			for (uint32_t b = 0; b < cr.nbytes; b++)
+				out.bytes[b] = cr.bytes[b];
+			continue;
+		}
+		uint32_t jl = h;
+		const uint32_t slot = (uint32_t)(d.slow_keys[h] >> 32);
+		while (jl + 1 < nslow && (uint32_t)(d.slow_keys[jl + 1] >> 32) == slot)
+			jl++;
+		session_carry_out(d, S[h], h, jl);
 	}
 }
 
@@ -1226,6 +1493,8 @@ __global__ void k_verify(Dev d) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
 		if (d.slots[d.verify[k].slot].hi != d.verify[k].hi)
 			set_error(d, EBD_ERR_COLLISION);
+	if (blockIdx.x == 0 && threadIdx.x == 0) // the last kernel of a batch: batch totals into run totals
+		d.ctr[CTR_EVICTIONS_TOTAL] += d.ctr[CTR_EVICTIONS];
 }
 
 __device__ __forceinline__ Slot empty_slot() {
@@ -1256,9 +1525,12 @@ __global__ void k_sset_clear(Dev d) {
 		s->tag = 0;
 		s->kv = 0;
 		s->sid = 0;
-		s->pad = 0;
+		s->first_c = 0;
 		s->carry = 0;
 		s->visited = 0;
+		s->last_ev = 0;
+		s->pad = 0;
+		s->pad2 = 0;
 	}
 }
 
@@ -1422,6 +1694,23 @@ hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_slow_collect, dim3(grid_for(d.n, 256, cus * 8)), dim3(256), 0, st, d);
 	return hipGetLastError();
 }
+hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* minus, int* scan, void* tmp, size_t tmp_bytes,
+		hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_lru_delta, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, delta, minus);
+	hipError_t e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, delta, scan, (int)d.n, st);
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_lru_peak, dim3(grid_for(d.n, 256, cus * 4)), dim3(256), 0, st, scan, minus, d.n, d.ctr);
+	return hipGetLastError();
+}
+hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
+		uint32_t cap, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, jpos, head);
+	hipLaunchKernelGGL(k_walk_lru, dim3(1), dim3(kLruThreads), 0, st, d, nslow, (const uint32_t*)jpos, (const uint32_t*)head, S,
+			live, cap);
+	return hipGetLastError();
+}
+size_t sess_state_bytes() { return sizeof(SessState); }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, 64, cus * 16)), dim3(64), 0, st, d, nslow);
 	return hipGetLastError();

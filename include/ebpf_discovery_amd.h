@@ -152,11 +152,13 @@ typedef struct ebd_stats {
 	uint64_t services;          /* distinct (pid, endpoint) keys */
 	uint64_t hash_collisions;   /* 64-bit slot tag matched but the 128-bit key did not */
 	uint64_t errors;            /* bitmask of EBD_ERR_* conditions seen */
+	uint64_t lru_evictions;     /* sessions evicted from the full LRU (LRUCache.h:56-58) */
+	uint64_t lru_exact_batches; /* batches whose session events ran through the exact LRU walker */
 } ebd_stats;
 
 #define EBD_ERR_TABLE_FULL 1u      /* service table probe limit reached */
 #define EBD_ERR_ARENA_FULL 2u      /* string arena exhausted */
-#define EBD_ERR_LRU_OVERFLOW 4u    /* > EBD_MAX_SESSIONS live sessions: reference would evict */
+#define EBD_ERR_LRU_OVERFLOW 4u    /* more saved sessions than the carry store holds (internal) */
 #define EBD_ERR_SESSION_FULL 8u    /* session scratch exhausted */
 #define EBD_ERR_VERIFY_FULL 16u    /* deferred key-verification list exhausted */
 #define EBD_ERR_BAD_INPUT 32u      /* len > EBD_BUFFER_MAX_DATA_SIZE, bad offsets */

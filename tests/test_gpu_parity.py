@@ -320,3 +320,34 @@ def test_device_sharded_generator_matches_host():
         for i in range(0, k, 37):
             a = int(ho[i])
             assert pd[a:a + int(hl[i])].tobytes() == hp[a:a + int(hl[i])].tobytes()
+
+
+@pytest.mark.parametrize("cap,n_conn,window,batches", [(64, 600, 256, 1), (64, 600, 256, 4), (8192, 11000, 11000, 1),
+                                                       (8192, 11000, 11000, 3)])
+def test_lru_eviction_exact(cap, n_conn, window, batches):
+    """More live sessions than the LRU holds (LRUCache.h:50-89; Discovery.cpp:39): the full
+    cache evicts its least recently used session on insert, whose later buffers then parse
+    as new sessions.  The exact walker (k_walk_lru) must reproduce the oracle's LRU event for
+    event, within a batch and across batches (recency carried with the sessions)."""
+    ev, lens, offs, payload = T.fragmented_trace(n_conn, seed=31, window=window)
+    gv, gs, gst, _ = run_gpu(ev, lens, offs, payload, batches=batches, lru=cap)
+    ov, os_, ost = run_oracle(ev, lens, offs, payload, lru=cap)
+    assert ost["lru_evictions"] > 0
+    assert gst["errors"] == 0, gst
+    assert gst["lru_exact_batches"] >= 1
+    bad = [i for i in range(len(ov)) if gv[i] != ov[i]]
+    assert not bad, [(i, gv[i], ov[i]) for i in bad[:5]]
+    assert gs == os_
+    assert gst["kernel_deletes"] == ost["kernel_deletes"]
+    assert gst["live_sessions"] == ost["lru_size"]
+    assert gst["lru_evictions"] == ost["lru_evictions"]
+
+
+def test_lru_bound_keeps_parallel_walker_when_no_eviction():
+    """A window of live sessions below the capacity: the bound admits the parallel walker
+    (no exact batch) even though the batch holds far more sessions than the capacity."""
+    ev, lens, offs, payload = T.fragmented_trace(3000, seed=4, window=200)
+    gv, gs, gst, _ = run_gpu(ev, lens, offs, payload, lru=512)
+    ov, os_, ost = run_oracle(ev, lens, offs, payload, lru=512)
+    assert ost["lru_evictions"] == 0 and gst["lru_exact_batches"] == 0
+    assert gv == ov and gs == os_
