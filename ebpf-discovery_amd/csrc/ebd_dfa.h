@@ -37,16 +37,14 @@ struct DfaTable {
 	uint8_t next[256 * 256]; // next[s * 256 + byte]
 };
 
-// The table as the kernel keeps it in LDS.  Rows are kLdsRow = 260 bytes apart (65 dwords,
-// so consecutive states start one bank apart), and byte b of a row sits at column lds_col(b),
-// which moves b's low 5 bits to bits 6..2: the bank of entry (s, b) is (s + b[4:0]) mod 32.
-// Lanes in the same state never conflict (the 4 ASCII bytes that share b[4:0] share one
-// dword), and different states spread over the banks.  The plain (s << 8) | b layout puts
-// all lower-case letters on 7 banks (tools/ubench_lds.hip measures both).
-constexpr uint32_t kLdsRow = 260;
-EBD_HD constexpr uint32_t lds_col(uint32_t b) { return ((b & 0x1fu) << 2) | ((b >> 5) & 3u) | (b & 0x80u); }
-constexpr uint32_t kLdsRows = 200; // >= nstates (ebd_build_dfa checks)
-constexpr uint32_t kLdsTableBytes = kLdsRows * kLdsRow;
+// The table as the kernel keeps it in LDS: byte-major, entry (s, b) at b * kLdsStride + s.
+// A step's address is then one v_mad_u32_u24(b, kLdsStride, s) on the byte as loaded, with
+// no per-byte remapping.  kLdsStride = 196 bytes = 49 dwords, an odd count, so the bank of
+// (s, b) is (17 b + s / 4) mod 32: lanes reading different bytes in one state spread over the
+// banks, and so do lanes in different states on one byte.
+constexpr uint32_t kLdsStride = 196;
+constexpr uint32_t kLdsRows = kLdsStride; // >= nstates (ebd_build_dfa checks)
+constexpr uint32_t kLdsTableBytes = 256 * kLdsStride;
 void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes
 
 void build_key_trie(KeyTrie* t);

@@ -250,10 +250,10 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 // its scan record to the wave's queue in LDS; 64 records are finalized together (rescans,
 // spans, key), so the finalize code always runs on a full wave.
 // ---------------------------------------------------------------------------------
-// Logical index (s << 8) | b into the LDS image (ebd_dfa.h kLdsRow / lds_col).
+// Logical index (s << 8) | b into the LDS image (ebd_dfa.h: byte-major, kLdsStride).
 struct LdsTable {
 	const uint8_t* t;
-	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i >> 8) * kLdsRow + lds_col(i & 0xffu)]; }
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i & 0xffu) * kLdsStride + (i >> 8)]; }
 };
 
 // One 16-byte chunk as 4 little-endian words.
@@ -298,14 +298,9 @@ constexpr uint32_t kRing = EBD_RING; // finalize records in flight per workgroup
 // finalize wave waits on that same push.  Slots are pos & (kRing - 1).
 static_assert(kRing >= 128 && (kRing & (kRing - 1)) == 0, "ring: a power of two of at least 128 slots");
 
-// A chunk word with every byte b replaced by lds_col(b) (5 VALU per 4 bytes).
-__device__ __forceinline__ uint32_t lds_cols(uint32_t w) {
-	return ((w << 2) & 0x7c7c7c7cu) | ((w >> 5) & 0x03030303u) | (w & 0x80808080u);
-}
-
-// LDS address of entry (s, byte k of the column-mapped word wc): v_bfe + v_mad_u32_u24.
-__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t wc, int k) {
-	return s * kLdsRow + __builtin_amdgcn_ubfe(wc, 8 * (k & 3), 8);
+// LDS address of entry (s, byte k of word x): v_bfe (off the state chain) + v_mad_u32_u24.
+__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t x, int k) {
+	return __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8) * kLdsStride + s;
 }
 
 // Every byte of w in [0x20, 0x7e] (SWAR: no byte < 0x20, none >= 0x7f; exact tests).
@@ -329,12 +324,15 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 #pragma unroll
 	for (int q = 0; q < 4; q++) {
 		const uint32_t x = w.w[q];
+#ifndef EBD_NO_SKIP
 		const bool skip = (s == vl0 || s == vl1) && printable4(x);
+#else
+		const bool skip = false;
+#endif
 		if (!skip) {
-			const uint32_t wc = lds_cols(x);
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
-				s = T[tab_index(s, wc, k)];
+				s = T[tab_index(s, x, k)];
 				m = max(m, s);
 			}
 		} else {
