@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <sys/random.h>
+#include <time.h>
 #include <vector>
 
 #include "ebd_device.h"
@@ -45,14 +46,20 @@ hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long
 		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
 		hipStream_t st, int cus);
 hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
+hipError_t launch_net_clean(const Dev& d, unsigned long long now, unsigned long long retention, hipStream_t st, int cus);
+hipError_t launch_keep_collect(const Dev& d, KeepRec* keep, unsigned long long* kbytes, unsigned long long kcap, hipStream_t st,
+		int cus);
+hipError_t launch_keep_insert(const Dev& d, const KeepRec* keep, const uint8_t* kbytes, uint32_t* remap, hipStream_t st, int cus);
+hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap, hipStream_t st, int cus);
+hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus);
 } // namespace ebd
 
 using namespace ebd;
 
 // the layouts the Python binding (ebd/__init__.py) and tests/test_abi.py assume
-static_assert(sizeof(ebd_config) == 56, "ebd_config layout");
+static_assert(sizeof(ebd_config) == 64, "ebd_config layout");
 static_assert(sizeof(ebd_stats) == 88, "ebd_stats layout");
-static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 64, "result layouts");
+static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 80 && sizeof(ebd_service_net) == 32, "result layouts");
 
 #define HIP_TRY(x)                                                                                                   \
 	do {                                                                                                             \
@@ -132,6 +139,21 @@ struct ebd_ctx {
 	void* d_lru_sess = nullptr;
 	uint32_t* d_lru_live = nullptr;
 	uint64_t lru_batches_exact = 0;
+	// network counters (EBD_CFG_NETWORK_COUNTERS): map entries (two tables: a clear rebuilds
+	// into the other), the v6 prefix dictionary, and the network-counter clear's scratch
+	int net_on = 0;
+	NetEnt* d_nets[2] = {nullptr, nullptr};
+	int net_cur = 0;
+	uint32_t net_cap = 0;
+	unsigned long long* d_v6d = nullptr;
+	uint32_t v6d_cap = 0;
+	uint64_t clock_ns = 0; // ebd_set_clock (0: CLOCK_MONOTONIC per batch)
+	KeepRec* d_keep = nullptr;
+	uint64_t keep_cap = 0;
+	unsigned long long* d_kbytes = nullptr;
+	uint64_t kbytes_cap = 0;
+	uint32_t* d_remap = nullptr;
+	ebd_service_net* d_netdump = nullptr;
 	// bookkeeping
 	unsigned long long seq_base = 0;
 	uint32_t last_n = 0;
@@ -222,14 +244,31 @@ static Dev make_dev(ebd_ctx* c) {
 	d.sstr_cap = c->sstr_cap;
 	d.ctr = c->d_ctr;
 	d.seq_base = c->seq_base;
+	d.net_on = c->net_on;
+	d.nets = c->d_nets[c->net_cur];
+	d.net_mask = c->net_cap ? c->net_cap - 1 : 0;
+	d.v6d = c->d_v6d;
+	d.v6d_mask = c->v6d_cap ? c->v6d_cap - 1 : 0;
+	d.now = 1;
 	return d;
+}
+
+// Aggregator::getCurrentTime (A:211-213): std::chrono::steady_clock is CLOCK_MONOTONIC.
+static uint64_t ctx_now(const ebd_ctx* c) {
+	if (c->clock_ns)
+		return c->clock_ns;
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	const uint64_t t = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+	return t ? t : 1;
 }
 
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload, c->d_lru_delta, c->d_lru_minus,
-			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live};
+			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
+			c->d_v6d, c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
 	for (void* p : ptrs)
 		if (p)
 			(void)hipFree(p);
@@ -366,6 +405,17 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_COUNT * sizeof(unsigned long long), c->stream));
 	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
 	CTX_TRY(hipHostMalloc(&c->h_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long), hipHostMallocDefault));
+	if (cfg->flags & EBD_CFG_NETWORK_COUNTERS) {
+		c->net_on = 1;
+		c->net_cap = next_pow2(cfg->net_capacity ? cfg->net_capacity : (1u << 22));
+		c->v6d_cap = c->net_cap;
+		for (int k = 0; k < 2; k++) {
+			CTX_TRY(hipMalloc(&c->d_nets[k], (size_t)c->net_cap * sizeof(NetEnt)));
+			CTX_TRY(hipMemsetAsync(c->d_nets[k], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
+		}
+		CTX_TRY(hipMalloc(&c->d_v6d, (size_t)c->v6d_cap * sizeof(unsigned long long)));
+		CTX_TRY(hipMemsetAsync(c->d_v6d, 0, (size_t)c->v6d_cap * sizeof(unsigned long long), c->stream));
+	}
 	CTX_TRY(hipStreamSynchronize(c->stream));
 #undef CTX_TRY
 	*out = c;
@@ -423,6 +473,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	d.off = off;
 	d.payload = payload;
 	d.n = n;
+	d.now = ctx_now(c);
 	c->last_n = n;
 	c->last_slow_ran = 0;
 	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_BATCH_END * sizeof(unsigned long long), c->stream));
@@ -677,15 +728,118 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 	return 0;
 }
 
+// Aggregator::clear with network counters (A:138-149): the services with a non-empty map
+// survive, re-inserted into the emptied table with zeroed client counters; their map entries
+// move to a fresh table under the new slots (ebd_kernels.hip k_keep_collect .. k_net_remap).
+static int clear_keep_nets(ebd_ctx* c) {
+	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	const uint64_t nsvc = c->h_ctr[CTR_SERVICES], bytes = c->h_ctr[CTR_SARENA];
+	if (nsvc > c->keep_cap) {
+		if (c->d_keep)
+			HIP_TRY(hipFree(c->d_keep));
+		c->keep_cap = nsvc + nsvc / 2 + 1024;
+		HIP_TRY(hipMalloc(&c->d_keep, c->keep_cap * sizeof(KeepRec)));
+	}
+	if (bytes + 64 > c->kbytes_cap) {
+		if (c->d_kbytes)
+			HIP_TRY(hipFree(c->d_kbytes));
+		c->kbytes_cap = bytes + bytes / 2 + 4096;
+		HIP_TRY(hipMalloc(&c->d_kbytes, c->kbytes_cap + 64)); // claim_publish reads 8 bytes past
+	}
+	if (!c->d_remap)
+		HIP_TRY(hipMalloc(&c->d_remap, (size_t)c->slot_cap * sizeof(uint32_t)));
+	HIP_TRY(hipMemsetAsync(c->d_remap, 0xff, (size_t)c->slot_cap * sizeof(uint32_t), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_KEEP, 0, 2 * sizeof(unsigned long long), c->stream));
+	Dev d = make_dev(c);
+	HIP_TRY(launch_keep_collect(d, c->d_keep, c->d_kbytes, c->kbytes_cap, c->stream, c->cus));
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->stream, c->cus); }));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_keep_insert(d, c->d_keep, (const uint8_t*)c->d_kbytes, c->d_remap, c->stream, c->cus));
+	const int nxt = c->net_cur ^ 1;
+	HIP_TRY(hipMemsetAsync(c->d_nets[nxt], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_NETS, 0, sizeof(unsigned long long), c->stream));
+	Dev dn = d;
+	dn.nets = c->d_nets[nxt];
+	HIP_TRY(launch_net_remap(dn, c->d_nets[c->net_cur], c->net_cap - 1, c->d_remap, c->stream, c->cus));
+	c->net_cur = nxt;
+	return 0;
+}
+
 int ebd_clear(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
+	if (c->net_on)
+		return clear_keep_nets(c);
 	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->stream, c->cus); }));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	return 0;
+}
+
+int ebd_set_clock(ebd_ctx* c, uint64_t now_ns) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	c->clock_ns = now_ns;
+	return 0;
+}
+
+int ebd_network_counters_cleaning(ebd_ctx* c, uint64_t now_ns) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	if (!c->net_on)
+		return 0; // every map is empty
+	HIP_TRY(hipSetDevice(c->device));
+	const uint64_t now = now_ns ? now_ns : ctx_now(c);
+	HIP_TRY(launch_net_clean(make_dev(c), now, 3600ull * 1000000000ull, c->stream, c->cus)); // std::chrono::hours(1)
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_collect_networks(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_t* n) {
+	if (!c || !n)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	*n = 0;
+	if (!c->net_on)
+		return 0;
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_netdump)
+		HIP_TRY(hipMalloc(&c->d_netdump, (size_t)c->net_cap * sizeof(ebd_service_net)));
+	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_net_dump(make_dev(c), c->d_netdump, c->net_cap, c->d_cnt, c->stream, c->cus));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	const uint64_t cnt = c->h_ctr[CTR_COUNT];
+	*n = (uint32_t)cnt;
+	if (!out)
+		return 0;
+	if (cnt > cap)
+		return -ENOSPC;
+	if (cnt)
+		HIP_TRY(hipMemcpy(out, c->d_netdump, cnt * sizeof(ebd_service_net), hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int ebd_report_json(ebd_ctx* c, char* out, uint64_t cap, uint64_t* len) {
+	if (!c || !len)
+		return -EINVAL;
+	uint32_t n = 0;
+	uint64_t sl = 0;
+	int rc = ebd_collect_services(c, nullptr, 0, &n, nullptr, 0, &sl);
+	if (rc)
+		return rc;
+	std::vector<ebd_service> svc(n ? n : 1);
+	std::vector<char> str(sl ? sl : 1);
+	rc = ebd_collect_services(c, svc.data(), n, &n, str.data(), sl, &sl);
+	if (rc)
+		return rc;
+	return ebd_format_services_json(svc.data(), n, str.data(), sl, out, cap, len);
 }
 
 int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,

@@ -19,7 +19,8 @@ struct Slot {
 	unsigned int ep_len;
 	unsigned int internal_clients; // uint32, wraps like Service.h:53-54
 	unsigned int external_clients;
-	unsigned int pad[4];
+	unsigned int nets[3];          // network-map sizes: v4 /16, v4 /24, v6 /48 (Service.h:56-58)
+	unsigned int pad;
 };
 static_assert(sizeof(Slot) == 64, "slot is 64 bytes");
 
@@ -83,7 +84,32 @@ enum Ctr : uint32_t {
 	CTR_SESSION_EVENTS,
 	CTR_SERVICES,       // length of the claimed-slot list (services in the table)
 	CTR_EVICTIONS_TOTAL,
-	CTR_COUNT = 19,
+	CTR_KEEP,           // services kept by a network-counter clear
+	CTR_KEEP_BYTES,     // their endpoint bytes
+	CTR_NETS,           // network-map entries claimed (the table's fill)
+	CTR_V6D,            // v6 prefix-dictionary slots claimed
+	CTR_COUNT = 23,
+};
+
+// Network-counter maps of all services (Service.h:45-58): one open-addressing table of
+// (service slot, map, prefix) -> time last seen.  key = kind << 62 | slot << 31 | value, with
+// value = the prefix bytes (v4 /16: 2, /24: 3) or, for a v6 48-bit prefix, its index in the
+// prefix dictionary (v6d: 48-bit prefix | 1 << 63 per slot).  time = 0: erased (or never set).
+enum : uint32_t { NET_V4_16 = 1, NET_V4_24 = 2, NET_V6 = 3 };
+struct NetEnt {
+	unsigned long long key;
+	unsigned long long time;
+};
+EBD_HD unsigned long long net_key(uint32_t kind, uint32_t slot, uint32_t value) {
+	return ((unsigned long long)kind << 62) | ((unsigned long long)slot << 31) | value;
+}
+
+// A service kept by a network-counter clear (Aggregator.cpp:138-149): re-inserted into the
+// emptied table; its endpoint bytes wait in a side arena.
+struct KeepRec {
+	unsigned long long tag, hi, first, ep_off;
+	uint32_t pid, ep_len, old_slot, pad;
+	uint32_t nets[3], pad2;
 };
 
 struct VerifyRec {
@@ -129,6 +155,13 @@ struct Dev {
 	SessReq* sreq;
 	uint8_t* sstr;
 	unsigned long long sstr_cap;
+	// network counters (EBD_CFG_NETWORK_COUNTERS)
+	uint32_t net_on;
+	unsigned long long now; // Aggregator::getCurrentTime of this batch's requests (>= 1)
+	NetEnt* nets;
+	uint32_t net_mask;
+	unsigned long long* v6d;
+	uint32_t v6d_mask;
 	// counters
 	unsigned long long* ctr;
 };

@@ -236,7 +236,8 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 // runs from `cs` to the first ',' or the value's CR (value bytes are C-class, so a CR ends
 // it; the request's final CRLF bounds the search).  `at(k)` yields buffer byte k.
 template <typename At>
-EBD_HD void cip_token(const Interfaces& ifs, At at, uint32_t cs, uint32_t consumed, uint32_t* tb, uint32_t* te, uint8_t* cls) {
+EBD_HD void cip_token(const Interfaces& ifs, At at, uint32_t cs, uint32_t consumed, uint32_t* tb, uint32_t* te, uint8_t* cls,
+		unsigned long long* net = nullptr) {
 	uint32_t e = cs;
 	while (e < consumed && at(e) != ',' && at(e) != '\r')
 		e++;
@@ -250,7 +251,7 @@ EBD_HD void cip_token(const Interfaces& ifs, At at, uint32_t cs, uint32_t consum
 	front_token(v, e - cs, &b, &en);
 	*tb = cs + b;
 	*te = cs + en;
-	*cls = classify_token(ifs, View{at, cs + b}, en - b);
+	*cls = classify_token(ifs, View{at, cs + b}, en - b, net);
 }
 
 } // namespace ebd

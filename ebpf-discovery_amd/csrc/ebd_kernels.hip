@@ -162,6 +162,75 @@ __device__ void claim_publish(const Dev& d, uint32_t idx, unsigned long long lis
 }
 
 // ---------------------------------------------------------------------------------
+// Network counters (Aggregator.cpp:89-106, EBD_CFG_NETWORK_COUNTERS): an external client's
+// /24 and /16 (IPv4) or 48-bit prefix (IPv6) go into its service's maps, map[prefix] = now.
+// A claim is one CAS of the whole 64-bit key, so no second word is ever waited for; the time
+// is an atomicMax, and the request that finds the entry erased (time 0) adds one to the
+// map's size in the service slot.  A v6 prefix does not fit the key beside the slot, so it
+// is first interned in a dictionary whose slot index stands for it.
+// ---------------------------------------------------------------------------------
+__device__ uint32_t v6d_index(const Dev& d, unsigned long long pfx48) {
+	const unsigned long long key = pfx48 | (1ull << 63);
+	uint32_t idx = (uint32_t)fmix64(key) & d.v6d_mask;
+	for (uint32_t probe = 0; probe <= d.v6d_mask; probe++) {
+		unsigned long long t = d.v6d[idx]; // a stale 0 at worst: the CAS decides
+		if (t == 0) {
+			t = atomicCAS(&d.v6d[idx], 0ull, key);
+			if (t == 0) {
+				atomicAdd(&d.ctr[CTR_V6D], 1ull);
+				return idx;
+			}
+		}
+		if (t == key)
+			return idx;
+		idx = (idx + 1) & d.v6d_mask;
+	}
+	set_error(d, EBD_ERR_NET_FULL);
+	return kNone;
+}
+
+// Claims or finds (kind, slot, value) in `nets` and returns the entry (nullptr: table full).
+__device__ NetEnt* net_find_or_claim(const Dev& d, NetEnt* nets, uint32_t mask, unsigned long long key) {
+	uint32_t idx = (uint32_t)fmix64(key) & mask;
+	for (uint32_t probe = 0; probe <= mask; probe++) {
+		NetEnt* e = nets + idx;
+		unsigned long long t = e->key;
+		if (t == 0) {
+			t = atomicCAS(&e->key, 0ull, key);
+			if (t == 0) {
+				atomicAdd(&d.ctr[CTR_NETS], 1ull);
+				return e;
+			}
+		}
+		if (t == key)
+			return e;
+		idx = (idx + 1) & mask;
+	}
+	set_error(d, EBD_ERR_NET_FULL);
+	return nullptr;
+}
+
+__device__ void net_touch(const Dev& d, uint32_t slot, uint32_t kind, uint32_t value) {
+	NetEnt* e = net_find_or_claim(d, d.nets, d.net_mask, net_key(kind, slot, value));
+	if (e && atomicMax(&e->time, d.now) == 0) // new, or erased by networkCountersCleaning
+		atomicAdd(&d.slots[slot].nets[kind - 1], 1u);
+}
+
+// incrementServiceClientsNumber's network part for an external client (net: net_pack).
+__device__ void agg_nets(const Dev& d, uint32_t slot, unsigned long long net) {
+	if (slot == kNone)
+		return;
+	if (net & kNetV6) {
+		const uint32_t v = v6d_index(d, net & 0xffffffffffffull);
+		if (v != kNone)
+			net_touch(d, slot, NET_V6, v);
+	} else {
+		net_touch(d, slot, NET_V4_24, (uint32_t)(net & 0xffffffu));
+		net_touch(d, slot, NET_V4_16, (uint32_t)(net & 0xffffu));
+	}
+}
+
+// ---------------------------------------------------------------------------------
 // Session set: (pid, fd, sessionID) -> slot.  Claimed by a CAS on the 64-bit tag; the
 // full key is stored by the claimer and compared by sset_find in later kernels (a tag
 // shared by two keys is reported as EBD_ERR_COLLISION there).
@@ -793,7 +862,8 @@ constexpr int kAggThreads = 256;
 constexpr int kCipRaw = 64;
 constexpr int kCipStride = kCipRaw + 8; // rows 72 B apart: lanes spread over the banks
 
-__device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_event_result& r, uint8_t* row) {
+__device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_event_result& r, uint8_t* row,
+		unsigned long long* net) {
 	const uint8_t* p = d.payload + d.off[i];
 	const uint32_t cs = r.u.span.cip_off, lim = r.consumed; // the value ends before the final CRLF
 	unsigned long long v[kCipRaw / 8];
@@ -810,9 +880,9 @@ __device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_e
 	while (e < avail && row[e] != ',' && row[e] != '\r')
 		e++;
 	if (e < avail || avail == lim - cs) {
-		cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls);
+		cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls, net);
 	} else { // a value longer than the copy without ',' or CR in it: parse from the buffer
-		cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls);
+		cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls, net);
 		tb -= cs;
 		te -= cs;
 	}
@@ -932,12 +1002,13 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 			dst[k++] = c;
 			return true;
 		});
+	unsigned long long net = 0;
 	if (g.f & GPF_CIP_FOUND) {
 		front_token(dst + hl + ul, raw, &tb, &te);
 		info |= EBD_INFO_CIP;
-		cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb);
+		cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb, &net);
 	} else {
-		cls = classify_source(*d.ifs, ev.flags, ev.sourceIP);
+		cls = classify_source(*d.ifs, ev.flags, ev.sourceIP, &net);
 	}
 	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
 	kh.bytes(dst, hl + ul);
@@ -947,6 +1018,8 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	if (claimed) // a rare path: one reservation per claim
 		claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
 				atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
+	if (d.net_on && cls == CLS_EXTERNAL)
+		agg_nets(d, slot, net);
 	atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
 	const unsigned long long q = atomicAdd(&d.ctr[CTR_SREQ], 1ull);
 	SessReq sr;
@@ -1383,11 +1456,13 @@ struct AggShared {
 };
 
 __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
-		PendingClaim& pc, bool& has) {
+		PendingClaim& pc, bool& has, unsigned long long net) {
 	bool claimed;
 	const Hash128 key = d.keys[i];
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
 			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
+	if (d.net_on && cls == CLS_EXTERNAL)
+		agg_nets(d, slot, net);
 	if (claimed) {
 		const uint8_t* p = d.payload + d.off[i];
 		pc.slot = slot;
@@ -1404,10 +1479,11 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 
 __device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh, PendingClaim& pc, bool& has) {
 	ebd_event_result r = d.res[i];
-	const uint32_t cls = cip_classify(d, i, r, row);
+	unsigned long long net = 0;
+	const uint32_t cls = cip_classify(d, i, r, row, &net);
 	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 	d.res[i] = r;
-	agg_request(d, i, r, cls, sh, pc, has);
+	agg_request(d, i, r, cls, sh, pc, has, net);
 }
 
 __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
@@ -1440,10 +1516,11 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
 					uint8_t src[16];
 					__builtin_memcpy(src, &sv, 16);
-					const uint32_t cls = classify_source(*d.ifs, evb[32], src);
+					unsigned long long net = 0;
+					const uint32_t cls = classify_source(*d.ifs, evb[32], src, &net);
 					r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 					d.res[i] = r;
-					agg_request(d, i, r, cls, sh, pc[0], has[0]);
+					agg_request(d, i, r, cls, sh, pc[0], has[0], net);
 				}
 			}
 		}
@@ -1505,7 +1582,8 @@ __device__ __forceinline__ Slot empty_slot() {
 	s.ep_len = 0;
 	s.internal_clients = 0;
 	s.external_clients = 0;
-	s.pad[0] = s.pad[1] = s.pad[2] = s.pad[3] = 0;
+	s.nets[0] = s.nets[1] = s.nets[2] = 0;
+	s.pad = 0;
 	return s;
 }
 
@@ -1564,7 +1642,132 @@ __global__ void k_collect(const Slot* slots, const unsigned int* used, const uns
 		v.first_seq = s.first >> 16;
 		v.key_lo = s.tag;
 		v.key_hi = s.hi;
+		v.nets_v4_16 = s.nets[0];
+		v.nets_v4_24 = s.nets[1];
+		v.nets_v6 = s.nets[2];
+		v.pad2_ = 0;
 		out[k] = v;
+	}
+}
+
+// ---------------------------------------------------------------------------------
+// Network counters: networkCountersCleaning, the network-counter clear, and the set dump.
+// ---------------------------------------------------------------------------------
+// Aggregator::networkCountersCleaning (A:182-209): an entry seen retention or more before
+// now is erased (signed difference, like the steady_clock durations it restates).
+__global__ void k_net_clean(Dev d, unsigned long long now, unsigned long long retention) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= d.net_mask; k += gridDim.x * blockDim.x) {
+		NetEnt& e = d.nets[k];
+		const unsigned long long t = e.time;
+		if (e.key == 0 || t == 0 || (long long)(now - t) < (long long)retention)
+			continue;
+		e.time = 0;
+		const uint32_t kind = (uint32_t)(e.key >> 62), slot = (uint32_t)(e.key >> 31) & 0x7fffffffu;
+		atomicSub(&d.slots[slot].nets[kind - 1], 1u);
+	}
+}
+
+// Aggregator::clear with network counters (A:138-149), step 1: the services that keep a
+// non-empty map are copied out (slot words and endpoint bytes) before the table is emptied
+// (step 2, k_clear_used), then re-inserted with zeroed client counters (step 3) and their map
+// entries moved to the new slots in a fresh table (step 4).  The others are gone.
+__global__ void k_keep_collect(Dev d, KeepRec* keep, unsigned long long* kbytes, unsigned long long kcap) {
+	const unsigned long long n = d.ctr[CTR_SERVICES];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const uint32_t si = d.new_slots[k];
+		const Slot& s = d.slots[si];
+		if ((s.nets[0] | s.nets[1] | s.nets[2]) == 0)
+			continue;
+		KeepRec r;
+		r.tag = s.tag;
+		r.hi = s.hi;
+		r.first = s.first;
+		r.pid = s.pid;
+		r.ep_len = s.ep_len;
+		r.old_slot = si;
+		r.pad = r.pad2 = 0;
+		r.nets[0] = s.nets[0];
+		r.nets[1] = s.nets[1];
+		r.nets[2] = s.nets[2];
+		r.ep_off = ~0ull;
+		const unsigned long long nb = (s.ep_len + 7u) & ~7u;
+		const unsigned long long at = atomicAdd(&d.ctr[CTR_KEEP_BYTES], nb);
+		if (s.ep_off != ~0ull && at + nb <= kcap) {
+			const unsigned long long* src = (const unsigned long long*)(d.sarena + s.ep_off);
+			for (unsigned long long w = 0; w < nb / 8; w++)
+				kbytes[at / 8 + w] = src[w];
+			r.ep_off = at;
+		} else if (s.ep_off != ~0ull) {
+			set_error(d, EBD_ERR_ARENA_FULL);
+		}
+		keep[atomicAdd(&d.ctr[CTR_KEEP], 1ull)] = r;
+	}
+}
+
+__global__ void k_keep_insert(Dev d, const KeepRec* keep, const uint8_t* kbytes, uint32_t* remap) {
+	const unsigned long long n = d.ctr[CTR_KEEP];
+	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const KeepRec r = keep[k];
+		bool claimed;
+		const uint32_t slot = agg_insert(d, Hash128{r.tag, r.hi}, r.first, 0, 0, &claimed);
+		if (slot == kNone)
+			continue;
+		if (claimed) {
+			const uint32_t len = r.ep_off == ~0ull ? 0 : r.ep_len;
+			const uint8_t* ep = kbytes + (r.ep_off == ~0ull ? 0 : r.ep_off);
+			const uint32_t hl = min((uint32_t)(r.first & 0x7fffu), len);
+			claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
+					atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((len + 7u) & ~7u)), r.pid, ep, hl, ep + hl, len - hl);
+		} else {
+			set_error(d, EBD_ERR_INTERNAL); // kept keys are distinct and the table was empty
+		}
+		Slot& s = d.slots[slot];
+		s.nets[0] = r.nets[0];
+		s.nets[1] = r.nets[1];
+		s.nets[2] = r.nets[2];
+		remap[r.old_slot] = slot;
+	}
+}
+
+// Live entries of the old table into the (zeroed) new one under their services' new slots.
+__global__ void k_net_remap(Dev d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= old_mask; k += gridDim.x * blockDim.x) {
+		const NetEnt e = old[k];
+		if (e.key == 0 || e.time == 0)
+			continue;
+		const uint32_t kind = (uint32_t)(e.key >> 62), slot = (uint32_t)(e.key >> 31) & 0x7fffffffu;
+		const uint32_t ns = remap[slot];
+		if (ns == kNone) { // a live entry belongs to a service with a non-empty map: kept
+			set_error(d, EBD_ERR_INTERNAL);
+			continue;
+		}
+		NetEnt* ne = net_find_or_claim(d, d.nets, d.net_mask, net_key(kind, ns, (uint32_t)(e.key & 0x7fffffffu)));
+		if (ne)
+			ne->time = e.time;
+	}
+}
+
+// Every live map entry with its service's key and its prefix bytes (ebd_collect_networks).
+__global__ void k_net_dump(Dev d, ebd_service_net* out, uint32_t cap, unsigned long long* count) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= d.net_mask; k += gridDim.x * blockDim.x) {
+		const NetEnt e = d.nets[k];
+		if (e.key == 0 || e.time == 0)
+			continue;
+		const unsigned long long at = atomicAdd(count, 1ull);
+		if (at >= cap)
+			continue;
+		const uint32_t kind = (uint32_t)(e.key >> 62), slot = (uint32_t)(e.key >> 31) & 0x7fffffffu;
+		const uint32_t v = (uint32_t)(e.key & 0x7fffffffu);
+		unsigned long long pfx = kind == NET_V6 ? (d.v6d[v] & 0xffffffffffffull) : v;
+		ebd_service_net r;
+		r.key_lo = d.slots[slot].tag;
+		r.key_hi = d.slots[slot].hi;
+		r.kind = (uint8_t)kind;
+		for (int b = 0; b < 6; b++)
+			r.prefix[b] = (uint8_t)(pfx >> (8 * b));
+		r.pad_ = 0;
+		r.time_ns = e.time;
+		out[at] = r;
 	}
 }
 
@@ -1753,6 +1956,28 @@ hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, 
 		unsigned long long* off, uint8_t* payload, unsigned long long* gidx, hipStream_t st) {
 	hipLaunchKernelGGL(k_gen_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, T, config, (unsigned long long)seed,
 			(unsigned long long)first, n, keep, pos, boff, ev, len, off, payload, gidx);
+	return hipGetLastError();
+}
+
+hipError_t launch_net_clean(const Dev& d, unsigned long long now, unsigned long long retention, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_net_clean, dim3(grid_for((uint64_t)d.net_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, now, retention);
+	return hipGetLastError();
+}
+hipError_t launch_keep_collect(const Dev& d, KeepRec* keep, unsigned long long* kbytes, unsigned long long kcap, hipStream_t st,
+		int cus) {
+	hipLaunchKernelGGL(k_keep_collect, dim3(cus * 4), dim3(256), 0, st, d, keep, kbytes, kcap);
+	return hipGetLastError();
+}
+hipError_t launch_keep_insert(const Dev& d, const KeepRec* keep, const uint8_t* kbytes, uint32_t* remap, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_keep_insert, dim3(cus * 4), dim3(256), 0, st, d, keep, kbytes, remap);
+	return hipGetLastError();
+}
+hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_net_remap, dim3(grid_for((uint64_t)old_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, old, old_mask, remap);
+	return hipGetLastError();
+}
+hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_net_dump, dim3(grid_for((uint64_t)d.net_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, out, cap, count);
 	return hipGetLastError();
 }
 

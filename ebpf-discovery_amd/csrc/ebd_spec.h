@@ -541,11 +541,28 @@ EBD_HD bool v6_external(const Interfaces& ifs, const uint8_t a[16]) {
 // Source-address fallback (A:57-63).  ipv4ToString / ipv6ToString followed by
 // inet_pton is the identity on the address bytes (checked against glibc in the tests),
 // so the bytes are classified directly.
-EBD_HD uint8_t classify_source(const Interfaces& ifs, uint8_t flags, const uint8_t src[16]) {
-	if (flags & 2)
+// The client's networks for the network counters (A:89-106), packed: address bytes 0..5 at
+// bits 0..47 (in_addr / in6_addr order), bit 63 set for IPv6.  Meaningful for an external
+// client only.
+constexpr unsigned long long kNetV6 = 1ull << 63;
+EBD_HD unsigned long long net_pack(const uint8_t* a, bool v6) {
+	unsigned long long p = 0;
+	for (int k = 0; k < (v6 ? 6 : 3); k++)
+		p |= (unsigned long long)a[k] << (8 * k);
+	return v6 ? (p | kNetV6) : p;
+}
+
+EBD_HD uint8_t classify_source(const Interfaces& ifs, uint8_t flags, const uint8_t src[16], unsigned long long* net = nullptr) {
+	if (flags & 2) {
+		if (net)
+			*net = net_pack(src, false);
 		return v4_external(ifs, src) ? CLS_EXTERNAL : CLS_INTERNAL;
-	if (flags & 4)
+	}
+	if (flags & 4) {
+		if (net)
+			*net = net_pack(src, true);
 		return v6_external(ifs, src) ? CLS_EXTERNAL : CLS_INTERNAL;
+	}
 	return CLS_NONE;
 }
 
@@ -596,7 +613,7 @@ EBD_HD void front_token(const Src& raw, uint32_t n, uint32_t* tb, uint32_t* te) 
 
 // A:50-74 on clientIp.front(): >= 2 ':' selects AF_INET6, parse failure = no count.
 template <typename Src>
-EBD_HD uint8_t classify_token(const Interfaces& ifs, const Src& t, uint32_t n) {
+EBD_HD uint8_t classify_token(const Interfaces& ifs, const Src& t, uint32_t n, unsigned long long* net = nullptr) {
 	uint32_t colons = 0;
 	for (uint32_t k = 0; k < n; k++)
 		colons += t[k] == ':';
@@ -604,11 +621,15 @@ EBD_HD uint8_t classify_token(const Interfaces& ifs, const Src& t, uint32_t n) {
 		uint8_t a[16];
 		if (n > 45 || !inet_pton6(t, n, a)) // longer than any valid text form
 			return CLS_NONE;
+		if (net)
+			*net = net_pack(a, true);
 		return v6_external(ifs, a) ? CLS_EXTERNAL : CLS_INTERNAL;
 	}
 	uint8_t a[4];
 	if (n > 15 || !inet_pton4(t, n, a))
 		return CLS_NONE;
+	if (net)
+		*net = net_pack(a, false);
 	return v4_external(ifs, a) ? CLS_EXTERNAL : CLS_INTERNAL;
 }
 

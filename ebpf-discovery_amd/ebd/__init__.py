@@ -23,7 +23,8 @@ STATUS_NONE, STATUS_UNFINISHED, STATUS_FINISHED, STATUS_INVALID = 0, 1, 2, 3
 INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING = 0x01, 0x02, 0x04, 0x08, 0x40
 CLASS_NONE, CLASS_INTERNAL, CLASS_EXTERNAL = 0, 1, 2
 ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "VERIFY_FULL", 32: "BAD_INPUT",
-            64: "COLLISION", 128: "INTERNAL"}
+            64: "COLLISION", 128: "INTERNAL", 256: "NET_FULL"}
+NET_V4_16, NET_V4_24, NET_V6_48 = 1, 2, 3
 
 EVENT_DTYPE = np.dtype([("pid", "<u4"), ("fd", "<u4"), ("sessionID", "<u4"), ("bufferSeq", "<u4"),
                         ("sourceIP", "u1", (16,)), ("flags", "u1"), ("pad", "u1", (3,))])
@@ -36,10 +37,14 @@ SESSION_REQ_DTYPE = np.dtype([("seq", "<u8"), ("pid", "<u4"), ("str_off", "<u4")
 SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4"), ("https", "u1"),
                           ("pad", "u1", (3,)), ("endpoint_off", "<u8"), ("endpoint_len", "<u4"),
                           ("domain_off", "<u4"), ("domain_len", "<u4"), ("host_len", "<u4"), ("first_seq", "<u8"),
-                          ("key_lo", "<u8"), ("key_hi", "<u8")])
+                          ("key_lo", "<u8"), ("key_hi", "<u8"), ("nets_v4_16", "<u4"), ("nets_v4_24", "<u4"),
+                          ("nets_v6", "<u4"), ("pad2", "<u4")])
+SERVICE_NET_DTYPE = np.dtype([("key_lo", "<u8"), ("key_hi", "<u8"), ("kind", "u1"), ("prefix", "u1", (6,)), ("pad", "u1"),
+                              ("time_ns", "<u8")])
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
-assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 64
+assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 80 and SERVICE_NET_DTYPE.itemsize == 32
 CFG_TIMING = 2
+CFG_NETWORK_COUNTERS = 4
 # A fixed service-key PRF key for tests that compare keys across contexts or with the host
 # hooks; products leave the key to the library (a fresh random key per context).
 TEST_HASH_KEY = (0x0706050403020100, 0x0F0E0D0C0B0A0908)
@@ -48,7 +53,7 @@ TEST_HASH_KEY = (0x0706050403020100, 0x0F0E0D0C0B0A0908)
 class Config(C.Structure):
     _fields_ = [("device", C.c_int), ("max_events", C.c_uint32), ("max_payload", C.c_uint64),
                 ("service_capacity", C.c_uint32), ("string_arena", C.c_uint64), ("lru_capacity", C.c_uint32),
-                ("flags", C.c_uint32), ("hash_key", C.c_uint64 * 2)]
+                ("flags", C.c_uint32), ("hash_key", C.c_uint64 * 2), ("net_capacity", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class DeviceBatch(C.Structure):
@@ -101,6 +106,12 @@ _SIGS = {
     "ebd_collect_services": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
                                        C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_clear": (C.c_int, [C.c_void_p]),
+    "ebd_set_clock": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "ebd_network_counters_cleaning": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "ebd_collect_networks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "ebd_format_services_json": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                           C.POINTER(C.c_uint64)]),
+    "ebd_report_json": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_export_services_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.c_void_p, C.c_void_p]),
     "ebd_merge_services_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
@@ -189,16 +200,18 @@ class Context:
     """One GPU context: the Discovery consumer state (session LRU) + the Aggregator."""
 
     def __init__(self, max_events, device=0, max_payload=0, service_capacity=0, string_arena=0, lru_capacity=0,
-                 timing=False, hash_key=None):
+                 timing=False, hash_key=None, network_counters=False, net_capacity=0):
         cfg = Config(device=device, max_events=max_events, max_payload=max_payload,
                      service_capacity=service_capacity, string_arena=string_arena, lru_capacity=lru_capacity,
-                     flags=CFG_TIMING if timing else 0)
+                     flags=(CFG_TIMING if timing else 0) | (CFG_NETWORK_COUNTERS if network_counters else 0),
+                     net_capacity=net_capacity)
         if hash_key is not None:
             cfg.hash_key[0], cfg.hash_key[1] = int(hash_key[0]), int(hash_key[1])
         h = C.c_void_p()
         _check(lib().ebd_ctx_create(C.byref(cfg), C.byref(h)), "ebd_ctx_create")
         self.h = h
         self.max_events = max_events
+        self.network_counters = network_counters
 
     def close(self):
         if getattr(self, "h", None):
@@ -278,9 +291,10 @@ class Context:
                "ebd_collect_services")
         return out[:n.value].copy(), buf[:sl.value].copy()
 
-    def services(self, with_seq=False):
+    def services(self, with_seq=False, with_nets=False):
         """[(pid, endpoint, domain, scheme, internal, external)] sorted by (pid, endpoint);
-        with_seq appends the first-arrival sequence number (for cross-shard merges)."""
+        with_seq appends the first-arrival sequence number (for cross-shard merges), with_nets
+        the sizes of the /16, /24 and v6 network maps."""
         n, sl = C.c_uint32(), C.c_uint64()
         _check(lib().ebd_collect_services(self.h, None, 0, C.byref(n), None, 0, C.byref(sl)), "collect")
         out = np.zeros(max(n.value, 1), SERVICE_DTYPE)
@@ -294,12 +308,44 @@ class Context:
             ep = s[o:o + L]
             dom = ep[int(r["domain_off"]):int(r["domain_off"]) + int(r["domain_len"])]
             t = (int(r["pid"]), ep, dom, b"https" if r["https"] else b"http", int(r["internal"]), int(r["external"]))
-            res.append(t + (int(r["first_seq"]),) if with_seq else t)
+            if with_seq:
+                t += (int(r["first_seq"]),)
+            if with_nets:
+                t += (int(r["nets_v4_16"]), int(r["nets_v4_24"]), int(r["nets_v6"]))
+            res.append(t)
         res.sort(key=lambda t: (t[0], t[1]))
         return res
 
     def clear(self):
         _check(lib().ebd_clear(self.h), "ebd_clear")
+
+    def set_clock(self, now_ns):
+        """Aggregator::getCurrentTime (steady-clock ns) of the next batches' requests; 0 = CLOCK_MONOTONIC."""
+        _check(lib().ebd_set_clock(self.h, now_ns), "ebd_set_clock")
+
+    def network_counters_cleaning(self, now_ns=0):
+        _check(lib().ebd_network_counters_cleaning(self.h, now_ns), "ebd_network_counters_cleaning")
+
+    def networks_raw(self):
+        """ebd_collect_networks: SERVICE_NET_DTYPE records (one per live network-map entry)."""
+        n = C.c_uint32()
+        _check(lib().ebd_collect_networks(self.h, None, 0, C.byref(n)), "ebd_collect_networks")
+        out = np.zeros(max(n.value, 1), SERVICE_NET_DTYPE)
+        _check(lib().ebd_collect_networks(self.h, _p(out), out.size, C.byref(n)), "ebd_collect_networks")
+        return out[:n.value].copy()
+
+    def report_json(self):
+        """Discovery::outputServicesToStdout's text (bytes; b"" without services)."""
+        ln = C.c_uint64()
+        _check(lib().ebd_report_json(self.h, None, 0, C.byref(ln)), "ebd_report_json")
+        buf = C.create_string_buffer(max(ln.value, 1))
+        while True:  # the table may not change between the calls, but size the buffer from the answer
+            rc = lib().ebd_report_json(self.h, buf, len(buf), C.byref(ln))
+            if rc == 0:
+                return buf.raw[:ln.value]
+            if ln.value <= len(buf):
+                _check(rc, "ebd_report_json")
+            buf = C.create_string_buffer(ln.value)
 
     def export_services_device(self, world, device):
         """The services grouped by owner (key_lo % world) in device tensors:
@@ -329,6 +375,18 @@ class Context:
         d = {k: getattr(s, k) for k, _ in Stats._fields_}
         d["error_names"] = [v for b, v in ERR_BITS.items() if d["errors"] & b]
         return d
+
+
+def format_services_json(records, strings: bytes):
+    """ebd_format_services_json (host only): the report text of SERVICE_DTYPE records."""
+    records = np.ascontiguousarray(records, dtype=SERVICE_DTYPE)
+    sb = np.frombuffer(strings, np.uint8) if strings else np.zeros(1, np.uint8)
+    ln = C.c_uint64()
+    _check(lib().ebd_format_services_json(_p(records), len(records), _p(sb), len(strings), None, 0, C.byref(ln)), "json")
+    buf = C.create_string_buffer(max(ln.value, 1))
+    _check(lib().ebd_format_services_json(_p(records), len(records), _p(sb), len(strings), buf, len(buf), C.byref(ln)),
+           "ebd_format_services_json")
+    return buf.raw[:ln.value]
 
 
 def _ptrval(x):

@@ -240,6 +240,9 @@ def device_exchange_merge(ctx, device, group=None, map_first=None):
     this rank's context (cleared first).  map_first(first_seq int64 tensor) -> trace
     positions, applied before the exchange.  Returns (records sent, records received)."""
     import torch.distributed as dist
+    if getattr(ctx, "network_counters", False):
+        # the merge carries client counters only: network maps are per context (DESIGN.md section 7)
+        raise ValueError("device_exchange_merge: contexts with network counters are not merged across GPUs")
     world = dist.get_world_size(group)
     recs, strs, counts, scounts = ctx.export_services_device(world, device)
     if map_first is not None and recs.numel():

@@ -130,7 +130,8 @@ typedef struct ebd_service {
 	uint32_t pid;
 	uint32_t internal_clients; /* uint32, wraps like Service.h:53-54 */
 	uint32_t external_clients;
-	uint8_t https; /* scheme "https" / "http" of the first request that created the key */
+	uint8_t https; /* scheme "https" (1) / "http" (0) of the first request that created the key;
+	                  EBD_SCHEME_NONE: no scheme (only ebd_format_services_json reads it) */
 	uint8_t pad_[3];
 	uint64_t endpoint_off; /* into the caller's string buffer */
 	uint32_t endpoint_len;
@@ -140,7 +141,29 @@ typedef struct ebd_service {
 	uint64_t first_seq; /* global order of the request that created it (first arrival) */
 	uint64_t key_lo, key_hi; /* 128-bit hash of (pid, endpoint): identical on every GPU, so
 	                            shards merge and pick owners by it without comparing strings */
-} ebd_service; /* 64 bytes */
+	/* Network counters (EBD_CFG_NETWORK_COUNTERS; Service.h:56-58, Aggregator.cpp:89-106): the
+	 * sizes of externalIPv4_16ClientNets, externalIPv4_24ClientNets and externalIPv6ClientsNets
+	 * (48-bit prefixes), the numbers the JSON report prints (Service.h:84-98).  0 when off. */
+	uint32_t nets_v4_16;
+	uint32_t nets_v4_24;
+	uint32_t nets_v6;
+	uint32_t pad2_;
+} ebd_service; /* 80 bytes */
+#define EBD_SCHEME_NONE 2
+
+/* One entry of a service's network set (ebd_collect_networks): the service's key, the set
+ * (EBD_NET_*), the prefix bytes in address order (v4: 2 or 3 bytes of in_addr, v6: 6 bytes
+ * of in6_addr; the rest 0) and the steady-clock time it was last seen (ns). */
+#define EBD_NET_V4_16 1
+#define EBD_NET_V4_24 2
+#define EBD_NET_V6_48 3
+typedef struct ebd_service_net {
+	uint64_t key_lo, key_hi;
+	uint8_t kind;
+	uint8_t prefix[6];
+	uint8_t pad_;
+	uint64_t time_ns;
+} ebd_service_net; /* 32 bytes */
 
 typedef struct ebd_stats {
 	uint64_t events;            /* events submitted */
@@ -164,6 +187,7 @@ typedef struct ebd_stats {
 #define EBD_ERR_BAD_INPUT 32u      /* len > EBD_BUFFER_MAX_DATA_SIZE, bad offsets */
 #define EBD_ERR_COLLISION 64u      /* two keys share a 64-bit tag (results not trusted) */
 #define EBD_ERR_INTERNAL 128u      /* a kernel-internal consistency check failed (results not trusted) */
+#define EBD_ERR_NET_FULL 256u      /* network-counter sets exhausted (ebd_config.net_capacity) */
 
 typedef struct ebd_config {
 	int device;                /* HIP device ordinal */
@@ -177,9 +201,15 @@ typedef struct ebd_config {
 	 * {0, 0} = draw one from getrandom().  Contexts whose tables are merged (shards of one
 	 * trace on several GPUs) must share it: read it back with ebd_get_hash_key. */
 	uint64_t hash_key[2];
+	uint32_t net_capacity; /* network-counter set entries (power of two, 0 = default 1<<22) */
+	uint32_t pad_;
 } ebd_config;
 
 #define EBD_CFG_TIMING 2u /* time every kernel launch with HIP events (ebd_kernel_times) */
+/* Aggregator(ipChecker, enableNetworkCounters = true) (Aggregator.cpp:132-134; the
+ * --enable-network-counters option, main.cpp:78): every external client's /16 and /24 (IPv4)
+ * or 48-bit (IPv6) network is kept per service with the time it was last seen. */
+#define EBD_CFG_NETWORK_COUNTERS 4u
 
 typedef struct ebd_ctx ebd_ctx;
 
@@ -242,8 +272,35 @@ int ebd_fetch_session_requests(ebd_ctx* ctx, ebd_session_request* out, uint32_t 
  * Call with out == NULL to get the sizes.  Order is unspecified (unordered_map). */
 int ebd_collect_services(ebd_ctx* ctx, ebd_service* out, uint32_t cap, uint32_t* n, char* strings, uint64_t strcap,
 		uint64_t* strlen);
-/* Aggregator::clear (Aggregator.cpp:136-153, network counters off). */
+/* Aggregator::clear (Aggregator.cpp:136-153).  Network counters off: every service goes.
+ * On: a service whose three network sets are all empty goes; the others stay with their
+ * client counters zeroed (their domain, scheme and sets are kept). */
 int ebd_clear(ebd_ctx* ctx);
+
+/* --- network counters (EBD_CFG_NETWORK_COUNTERS) -------------------------------------- */
+/* Aggregator::getCurrentTime for the requests of the batches submitted from now on
+ * (steady-clock nanoseconds, like std::chrono::steady_clock on Linux).  0 (the default):
+ * CLOCK_MONOTONIC is read when each batch is submitted.  The reference reads the clock per
+ * request; one reading per poll cycle differs by at most the cycle's length. */
+int ebd_set_clock(ebd_ctx* ctx, uint64_t now_ns);
+/* Aggregator::networkCountersCleaning (Aggregator.cpp:182-209): every set entry last seen
+ * at least one hour before now_ns is erased (0 = the context clock). */
+int ebd_network_counters_cleaning(ebd_ctx* ctx, uint64_t now_ns);
+/* The network-set entries of every service (out == NULL: count only).  Order unspecified. */
+int ebd_collect_networks(ebd_ctx* ctx, ebd_service_net* out, uint32_t cap, uint32_t* n);
+
+/* --- the service report (Discovery::outputServicesToStdout, Discovery.cpp:60-71) ------- */
+/* The report text byte for byte: {"service":[...]} through boost::json::ext::print
+ * (Json.h:32-71; null and empty-string fields dropped, network sets printed as their
+ * sizes, Service.h:69-98) and the std::endl newline; empty (length 0) when there are no
+ * services.  Services appear in `s` order (the reference prints its unordered_map order).
+ * *len = the text length; out == NULL or cap < *len: nothing is written (-ENOSPC when out
+ * is given).  Host-only: needs no GPU. */
+int ebd_format_services_json(const ebd_service* s, uint32_t n, const char* strings, uint64_t strings_len, char* out,
+		uint64_t cap, uint64_t* len);
+/* The context's services (ebd_collect_services) as that report.  Like the reference, the
+ * caller clears the aggregator after printing (ebd_clear). */
+int ebd_report_json(ebd_ctx* ctx, char* out, uint64_t cap, uint64_t* len);
 
 /* --- cross-GPU merge of per-GPU service tables ------------------------ */
 /* The context's services grouped by owner GPU, owner = key_lo % world, into DEVICE arrays:

@@ -826,8 +826,20 @@ typedef struct svc {
 	dstr endpoint, domain, scheme;
 	uint32_t internal, external; /* uint32, wraps like Service.h:53-54 */
 	uint64_t first;              /* index of the event whose request created it (first arrival) */
+	uint32_t nets[3];            /* sizes of externalIPv4_16ClientNets, _24ClientNets, IPv6ClientsNets (S:56-58) */
 	struct svc* hnext;
 } svc;
+
+/* One entry of a service's network map (S:45-50: prefix -> time last seen).  The maps of all
+ * services live in one open-addressing table keyed by (service, kind, prefix); an erased
+ * entry keeps its key (alive = 0) until the next clear rebuilds the table. */
+typedef struct {
+	svc* s;            /* NULL: empty slot */
+	uint8_t kind;      /* 0: v4 /16, 1: v4 /24, 2: v6 48-bit prefix */
+	uint8_t prefix[6]; /* address bytes in network order */
+	uint8_t alive;
+	uint64_t time;     /* steady-clock ns of the last request (A:97-100: map[key] = currentTime) */
+} net_ent;
 
 typedef struct {
 	uint8_t addr[4], mask[4];
@@ -852,6 +864,10 @@ struct orc_ctx {
 	dstr blob;
 	orc_stats st;
 	uint64_t cur_event; /* index of the event being handled, over all orc_process calls */
+	int netcounters;    /* Aggregator(..., enableNetworkCounters) A:132-134 */
+	uint64_t now;       /* getCurrentTime() (A:211-213) for the next requests */
+	net_ent* nt;
+	uint64_t ntcap, ntused;
 };
 
 static void free_parser_value(void* v) {
@@ -879,8 +895,35 @@ static void svc_free_all(orc_ctx* c) {
 	memset(c->sb, 0, c->snb * sizeof(svc*));
 }
 
-/* A:136-153 with network counters disabled (the default, main.cpp:78) */
-void orc_clear(orc_ctx* c) { svc_free_all(c); }
+static void nets_rebuild(orc_ctx* c, uint64_t cap);
+static void svc_reindex(orc_ctx* c);
+
+/* A:136-153.  Network counters off (the default, main.cpp:78): every service goes.  On:
+ * services whose three network maps are all empty go, the others stay with their client
+ * counters zeroed. */
+void orc_clear(orc_ctx* c) {
+	if (!c->netcounters) {
+		svc_free_all(c);
+		return;
+	}
+	uint64_t k = 0;
+	for (uint64_t i = 0; i < c->nsvc; i++) {
+		svc* s = c->list[i];
+		if (s->nets[0] == 0 && s->nets[1] == 0 && s->nets[2] == 0) {
+			ds_free(&s->endpoint);
+			ds_free(&s->domain);
+			ds_free(&s->scheme);
+			free(s);
+		} else {
+			s->external = 0;
+			s->internal = 0;
+			c->list[k++] = s;
+		}
+	}
+	c->nsvc = k;
+	svc_reindex(c);
+	nets_rebuild(c, c->ntcap); /* only live entries (of kept services) survive */
+}
 
 void orc_destroy(orc_ctx* c) {
 	svc_free_all(c);
@@ -890,6 +933,7 @@ void orc_destroy(orc_ctx* c) {
 	free(c->v4);
 	free(c->v6);
 	free(c->mock);
+	free(c->nt);
 	ds_free(&c->blob);
 	free(c);
 }
@@ -1003,8 +1047,11 @@ static int checker_v6(orc_ctx* c, const uint8_t a[16]) {
 	return v6_external(c, a);
 }
 
-/* A:44-110 incrementServiceClientsNumber (network counters off).  Returns ORC_CLASS_*. */
-static int client_class(orc_ctx* c, const orc_request* r, uint8_t flags, const uint8_t* src) {
+static void net_touch(orc_ctx* c, svc* s, uint8_t kind, const uint8_t* pfx, int n);
+
+/* A:44-110 incrementServiceClientsNumber.  Returns ORC_CLASS_*; with network counters on,
+ * an external client's networks go into the service's maps (A:89-106). */
+static int client_class(orc_ctx* c, svc* sv, const orc_request* r, uint8_t flags, const uint8_t* src) {
 	char addr[64];
 	size_t alen;
 	int is6 = 0;
@@ -1037,19 +1084,96 @@ static int client_class(orc_ctx* c, const orc_request* r, uint8_t flags, const u
 		return ORC_CLASS_NONE; /* A:62-63 */
 	}
 	int ext, ok;
+	uint8_t b[16] = {0};
 	if (is6) {
-		uint8_t b[16];
 		ok = orc_inet_pton6(s, alen, b);
 		ext = ok ? checker_v6(c, b) : 0;
 	} else {
-		uint8_t b[4];
 		ok = orc_inet_pton4(s, alen, b);
 		ext = ok ? checker_v4(c, b) : 0;
 	}
 	ds_free(&tmp);
 	if (!ok)
 		return ORC_CLASS_NONE; /* A:66-84: parse failure is swallowed */
+	if (ext && c->netcounters) {
+		if (is6) {
+			net_touch(c, sv, 2, b, 6); /* A:91-94: the first ipv6NetworkPrefixBytesLen (6) bytes, S:41 */
+		} else {
+			net_touch(c, sv, 1, b, 3); /* A:96-97: s_addr & 0xFFFFFF = the first three bytes */
+			net_touch(c, sv, 0, b, 2); /* A:99-100: s_addr & 0xFFFF = the first two */
+		}
+	}
 	return ext ? ORC_CLASS_EXTERNAL : ORC_CLASS_INTERNAL;
+}
+
+/* ------------------------------------------------------------------------------- */
+/* Network maps (S:45-58; A:89-106 insert, A:182-209 networkCountersCleaning)       */
+/* ------------------------------------------------------------------------------- */
+static uint64_t net_hash(const svc* s, uint8_t kind, const uint8_t pfx[6]) {
+	uint64_t h = (uint64_t)(uintptr_t)s * 0x9E3779B97F4A7C15ull ^ kind;
+	for (int i = 0; i < 6; i++)
+		h = (h ^ pfx[i]) * 1099511628211ull;
+	return h ^ (h >> 29);
+}
+
+static net_ent* net_slot(orc_ctx* c, const svc* s, uint8_t kind, const uint8_t pfx[6]) {
+	uint64_t i = net_hash(s, kind, pfx) & (c->ntcap - 1);
+	for (;;) {
+		net_ent* e = &c->nt[i];
+		if (!e->s || (e->s == s && e->kind == kind && memcmp(e->prefix, pfx, 6) == 0))
+			return e;
+		i = (i + 1) & (c->ntcap - 1);
+	}
+}
+
+/* rehash the live entries into a table of `cap` slots (dead ones are dropped) */
+static void nets_rebuild(orc_ctx* c, uint64_t cap) {
+	net_ent* old = c->nt;
+	uint64_t oc = c->ntcap;
+	c->ntcap = cap < 1024 ? 1024 : cap;
+	c->nt = (net_ent*)calloc(c->ntcap, sizeof(net_ent));
+	c->ntused = 0;
+	for (uint64_t i = 0; i < oc; i++)
+		if (old[i].s && old[i].alive) {
+			*net_slot(c, old[i].s, old[i].kind, old[i].prefix) = old[i];
+			c->ntused++;
+		}
+	free(old);
+}
+
+/* map[prefix] = currentTime (A:94, 97, 100): a new or erased key adds one to the map's size */
+static void net_touch(orc_ctx* c, svc* s, uint8_t kind, const uint8_t* pfx, int n) {
+	if (2 * (c->ntused + 1) > c->ntcap)
+		nets_rebuild(c, c->ntcap ? 2 * c->ntcap : 1024);
+	uint8_t key[6] = {0};
+	memcpy(key, pfx, (size_t)n);
+	net_ent* e = net_slot(c, s, kind, key);
+	if (!e->s) {
+		e->s = s;
+		e->kind = kind;
+		memcpy(e->prefix, key, 6);
+		c->ntused++;
+	}
+	if (!e->alive) {
+		e->alive = 1;
+		s->nets[kind]++;
+	}
+	e->time = c->now;
+}
+
+void orc_set_network_counters(orc_ctx* c, int on) { c->netcounters = on; }
+void orc_set_time(orc_ctx* c, uint64_t now) { c->now = now; }
+
+/* A:182-209: erase every entry with currentTime - seen >= 1 h (std::chrono::hours(1)) */
+void orc_network_counters_cleaning(orc_ctx* c, uint64_t now) {
+	const uint64_t retention = 3600ull * 1000000000ull;
+	for (uint64_t i = 0; i < c->ntcap; i++) {
+		net_ent* e = &c->nt[i];
+		if (e->s && e->alive && (int64_t)(now - e->time) >= (int64_t)retention) {
+			e->alive = 0;
+			e->s->nets[e->kind]--;
+		}
+	}
 }
 
 static uint64_t svc_hash(uint32_t pid, const char* ep, size_t n) {
@@ -1059,6 +1183,17 @@ static uint64_t svc_hash(uint32_t pid, const char* ep, size_t n) {
 		h *= 1099511628211ull;
 	}
 	return h ^ (h >> 31);
+}
+
+/* the hash index over c->list after the list changed (clear with network counters) */
+static void svc_reindex(orc_ctx* c) {
+	memset(c->sb, 0, c->snb * sizeof(svc*));
+	for (uint64_t i = 0; i < c->nsvc; i++) {
+		svc* s = c->list[i];
+		uint32_t h = (uint32_t)svc_hash(s->pid, s->endpoint.p, s->endpoint.n) & (c->snb - 1);
+		s->hnext = c->sb[h];
+		c->sb[h] = s;
+	}
 }
 
 static void svc_index_grow(orc_ctx* c) {
@@ -1086,7 +1221,7 @@ static int agg_new_request(orc_ctx* c, const orc_request* r, uint32_t pid, uint8
 	uint32_t b = (uint32_t)svc_hash(pid, ep.p, ep.n) & (c->snb - 1);
 	for (svc* s = c->sb[b]; s; s = s->hnext) {
 		if (s->pid == pid && ds_eqds(&s->endpoint, &ep)) {
-			int cls = client_class(c, r, flags, src);
+			int cls = client_class(c, s, r, flags, src);
 			if (cls == ORC_CLASS_EXTERNAL)
 				s->external++;
 			else if (cls == ORC_CLASS_INTERNAL)
@@ -1132,7 +1267,7 @@ static int agg_new_request(orc_ctx* c, const orc_request* r, uint32_t pid, uint8
 		ds_set(&s->scheme, "https", 5);
 	else
 		ds_set(&s->scheme, "http", 4);
-	int cls = client_class(c, r, flags, src); /* A:128 */
+	int cls = client_class(c, s, r, flags, src); /* A:128 */
 	if (cls == ORC_CLASS_EXTERNAL)
 		s->external++;
 	else if (cls == ORC_CLASS_INTERNAL)
@@ -1181,6 +1316,126 @@ static uint64_t services_dump(orc_ctx* c, char* buf, uint64_t cap, int with_firs
 
 uint64_t orc_services_dump(orc_ctx* c, char* buf, uint64_t cap) { return services_dump(c, buf, cap, 0); }
 uint64_t orc_services_dump_first(orc_ctx* c, char* buf, uint64_t cap) { return services_dump(c, buf, cap, 1); }
+uint64_t orc_services_dump_nets(orc_ctx* c, char* buf, uint64_t cap) { return services_dump(c, buf, cap, 2); }
+
+static uint64_t ds_out(dstr* out, char* buf, uint64_t cap) {
+	uint64_t need = out->n;
+	if (buf && cap >= need && need)
+		memcpy(buf, out->p, need);
+	ds_free(out);
+	return need;
+}
+
+static void ds_puts(dstr* o, const char* p, size_t n) {
+	for (size_t k = 0; k < n; k++)
+		ds_push(o, p[k]);
+}
+
+/* Every live network-map entry: pid \t endpoint \t kind(1 /16, 2 /24, 3 v6) \t prefix hex (6 bytes)
+ * \t time \n, unsorted. */
+uint64_t orc_nets_dump(orc_ctx* c, char* buf, uint64_t cap) {
+	dstr out = {0};
+	char num[32];
+	static const char hx[] = "0123456789abcdef";
+	for (uint64_t i = 0; i < c->ntcap; i++) {
+		const net_ent* e = &c->nt[i];
+		if (!e->s || !e->alive)
+			continue;
+		char* q = put_u(num, e->s->pid);
+		ds_puts(&out, num, (size_t)(q - num));
+		ds_push(&out, '\t');
+		ds_puts(&out, e->s->endpoint.p, e->s->endpoint.n);
+		ds_push(&out, '\t');
+		ds_push(&out, (char)('1' + (e->kind == 0 ? 0 : e->kind == 1 ? 1 : 2)));
+		ds_push(&out, '\t');
+		for (int k = 0; k < 6; k++) {
+			ds_push(&out, hx[e->prefix[k] >> 4]);
+			ds_push(&out, hx[e->prefix[k] & 15]);
+		}
+		ds_push(&out, '\t');
+		q = put_u64(num, e->time);
+		ds_puts(&out, num, (size_t)(q - num));
+		ds_push(&out, '\n');
+	}
+	return ds_out(&out, buf, cap);
+}
+
+/* boost::json::serialize of a string (boost 1.83 serializer: '"' and '\\' escaped, \b \t \n
+ * \f \r by name, other bytes below 0x20 as \u00xx with lower-case hex; everything else,
+ * bytes >= 0x80 included, as is). */
+static void json_string(dstr* o, const char* p, size_t n) {
+	static const char hx[] = "0123456789abcdef";
+	ds_push(o, '"');
+	for (size_t k = 0; k < n; k++) {
+		unsigned char ch = (unsigned char)p[k];
+		switch (ch) {
+		case '"': ds_puts(o, "\\\"", 2); break;
+		case '\\': ds_puts(o, "\\\\", 2); break;
+		case '\b': ds_puts(o, "\\b", 2); break;
+		case '\t': ds_puts(o, "\\t", 2); break;
+		case '\n': ds_puts(o, "\\n", 2); break;
+		case '\f': ds_puts(o, "\\f", 2); break;
+		case '\r': ds_puts(o, "\\r", 2); break;
+		default:
+			if (ch < 0x20) {
+				ds_puts(o, "\\u00", 4);
+				ds_push(o, hx[ch >> 4]);
+				ds_push(o, hx[ch & 15]);
+			} else {
+				ds_push(o, (char)ch);
+			}
+		}
+	}
+	ds_push(o, '"');
+}
+
+/* Discovery::outputServicesToStdout (D:60-71): {"service": value_from(services)} through
+ * boost::json::ext::print (Json.h:32-71) and std::endl, services in creation order.  Service
+ * fields in BOOST_DESCRIBE_STRUCT order (S:69-80); an empty string or an empty map (null,
+ * S:84-98) is skipped, but "," is written before every field but the object's first (J:38-46).
+ * No services: nothing (D:62-64). */
+uint64_t orc_services_json(orc_ctx* c, char* buf, uint64_t cap) {
+	dstr out = {0};
+	if (c->nsvc == 0)
+		return ds_out(&out, buf, cap);
+	char num[32];
+	ds_puts(&out, "{\"service\":[", 12);
+	for (uint64_t i = 0; i < c->nsvc; i++) {
+		const svc* s = c->list[i];
+		if (i)
+			ds_push(&out, ',');
+		ds_push(&out, '{');
+		/* field 0 is pid, a number: never skipped, so every later field is preceded by ',' */
+		char* q = put_u(num, s->pid);
+		ds_puts(&out, "\"pid\":", 6);
+		ds_puts(&out, num, (size_t)(q - num));
+		const char* names[3] = {"endpoint", "domain", "scheme"};
+		const dstr* vals[3] = {&s->endpoint, &s->domain, &s->scheme};
+		for (int f = 0; f < 3; f++) {
+			if (vals[f]->n == 0)
+				continue;
+			ds_push(&out, ',');
+			json_string(&out, names[f], strlen(names[f]));
+			ds_push(&out, ':');
+			json_string(&out, vals[f]->p, vals[f]->n);
+		}
+		const char* cn[5] = {"internalClientsNumber", "externalClientsNumber", "externalIPv4_16ClientNets",
+				"externalIPv4_24ClientNets", "externalIPv6ClientsNets"};
+		const uint32_t cv[5] = {s->internal, s->external, s->nets[0], s->nets[1], s->nets[2]};
+		for (int f = 0; f < 5; f++) {
+			if (f >= 2 && cv[f] == 0) /* an empty map is null */
+				continue;
+			ds_push(&out, ',');
+			json_string(&out, cn[f], strlen(cn[f]));
+			ds_push(&out, ':');
+			q = put_u(num, cv[f]);
+			ds_puts(&out, num, (size_t)(q - num));
+		}
+		ds_push(&out, '}');
+	}
+	ds_puts(&out, "]}\n", 3);
+	return ds_out(&out, buf, cap);
+}
 
 static uint64_t services_dump(orc_ctx* c, char* buf, uint64_t cap, int with_first) {
 	svc** v = (svc**)malloc((c->nsvc ? c->nsvc : 1) * sizeof(svc*));
@@ -1210,12 +1465,19 @@ static uint64_t services_dump(orc_ctx* c, char* buf, uint64_t cap, int with_firs
 		e = put_u(num, s->external);
 		for (char* q = num; q < e; q++)
 			ds_push(&out, *q);
-		if (with_first) {
+		if (with_first & 1) {
 			ds_push(&out, '\t');
 			e = put_u64(num, s->first);
 			for (char* q = num; q < e; q++)
 				ds_push(&out, *q);
 		}
+		if (with_first & 2)
+			for (int k = 0; k < 3; k++) {
+				ds_push(&out, '\t');
+				e = put_u(num, s->nets[k]);
+				for (char* q = num; q < e; q++)
+					ds_push(&out, *q);
+			}
 		ds_push(&out, '\n');
 	}
 	free(v);

@@ -108,6 +108,18 @@ uint64_t orc_services_dump_first(orc_ctx* c, char* buf, uint64_t cap);
 uint64_t orc_service_count(orc_ctx* c);
 void orc_clear(orc_ctx* c);
 
+/* --- network counters (Aggregator.cpp:43, 89-106, 136-153, 182-209) -------------- */
+void orc_set_network_counters(orc_ctx* c, int on);
+/* getCurrentTime() (steady-clock ns) for the requests that follow */
+void orc_set_time(orc_ctx* c, uint64_t now);
+void orc_network_counters_cleaning(orc_ctx* c, uint64_t now);
+/* services_dump rows with three more columns: the sizes of the /16, /24 and v6 maps */
+uint64_t orc_services_dump_nets(orc_ctx* c, char* buf, uint64_t cap);
+/* pid \t endpoint \t kind (1: v4 /16, 2: v4 /24, 3: v6 48-bit) \t prefix as 12 hex digits \t time \n */
+uint64_t orc_nets_dump(orc_ctx* c, char* buf, uint64_t cap);
+/* Discovery::outputServicesToStdout text (Discovery.cpp:60-71, Json.h:32-71), creation order */
+uint64_t orc_services_json(orc_ctx* c, char* buf, uint64_t cap);
+
 /* Aggregator driven directly (AggregatorTest.cpp:53-156).  cip may be NULL.
  * A mock verdict queue, when set, answers the IpAddressChecker calls in order
  * (IpAddressCheckerMock, AggregatorTest.cpp:34-39). */

@@ -235,6 +235,59 @@ CONFIG1 = [
     dict(payload="GET / HTTP/1.1\r\nHost: 127.0.0.1", n=1000, services=[], saved_sessions=1000),
 ]
 
+# libebpfdiscovery/test/JsonTest.cpp:62-173 — services (Service.h fields; nets = sizes of the
+# externalIPv4_16 / _24 / IPv6 maps) and the exact text boost::json::ext::print writes.
+# scheme "" is a default-constructed Service's (JsonTest builds them without one).
+def _svc(pid, ep, dom, sch, i, e, nets=(0, 0, 0)):
+    return dict(pid=pid, endpoint=ep, domain=dom, scheme=sch, internal=i, external=e, nets=list(nets))
+
+
+JSON_CASES = [
+    dict(name="servicesToJson", services=[
+        _svc(1, "/endpoint/1", "", "", 1, 2), _svc(2, "/endpoint/1", "", "", 1, 2), _svc(3, "/endpoint/2", "", "", 1, 2),
+        _svc(4, "google.com/endpoint/3", "google.com", "http", 1, 2),
+        _svc(5, "dynatrace.com/endpoint/4", "dynatrace.com", "https", 1, 2)],
+        expected='{"service":['
+                 '{"pid":1,"endpoint":"/endpoint/1","internalClientsNumber":1,"externalClientsNumber":2},'
+                 '{"pid":2,"endpoint":"/endpoint/1","internalClientsNumber":1,"externalClientsNumber":2},'
+                 '{"pid":3,"endpoint":"/endpoint/2","internalClientsNumber":1,"externalClientsNumber":2},'
+                 '{"pid":4,"endpoint":"google.com/endpoint/3","domain":"google.com","scheme":"http",'
+                 '"internalClientsNumber":1,"externalClientsNumber":2},'
+                 '{"pid":5,"endpoint":"dynatrace.com/endpoint/4","domain":"dynatrace.com","scheme":"https",'
+                 '"internalClientsNumber":1,"externalClientsNumber":2}]}'),
+    dict(name="servicesToJsonNetworkCounters", services=[
+        _svc(1, "/endpoint/1", "", "", 1, 3, (2, 3, 0)), _svc(2, "/endpoint/1", "", "", 1, 3, (2, 3, 0)),
+        _svc(3, "/endpoint/2", "", "", 1, 3, (2, 3, 0)),
+        _svc(4, "google.com/endpoint/3", "google.com", "http", 1, 2, (0, 0, 2)),
+        _svc(5, "dynatrace.com/endpoint/4", "dynatrace.com", "https", 1, 2, (0, 0, 2))],
+        expected='{"service":[{"pid":1,"endpoint":"/endpoint/1","internalClientsNumber":1,"externalClientsNumber":3,'
+                 '"externalIPv4_16ClientNets":2,"externalIPv4_24ClientNets":3},{"pid":2,"endpoint":"/endpoint/1",'
+                 '"internalClientsNumber":1,"externalClientsNumber":3,"externalIPv4_16ClientNets":2,'
+                 '"externalIPv4_24ClientNets":3},{"pid":3,"endpoint":"/endpoint/2","internalClientsNumber":1,'
+                 '"externalClientsNumber":3,"externalIPv4_16ClientNets":2,"externalIPv4_24ClientNets":3},'
+                 '{"pid":4,"endpoint":"google.com/endpoint/3","domain":"google.com","scheme":"http",'
+                 '"internalClientsNumber":1,"externalClientsNumber":2,"externalIPv6ClientsNets":2},'
+                 '{"pid":5,"endpoint":"dynatrace.com/endpoint/4","domain":"dynatrace.com","scheme":"https",'
+                 '"internalClientsNumber":1,"externalClientsNumber":2,"externalIPv6ClientsNets":2}]}'),
+]
+
+# libservice/test/AggregatorTest.cpp:174-285 aggregateNetworkCounters: every request at time
+# point 0 with the checker mocked to "external"; the expected maps (keys as in_addr s_addr
+# values on little-endian x86, i.e. the address bytes in order) and sizes after cleaning at
+# 59 min (kept) and 60 min (erased), each followed by clear().
+_NC_REQ = [("172.143.4.5", FLAG_IPV4), ("172.143.6.89", FLAG_IPV4), ("172.199.45.55", FLAG_IPV4),
+           ("1234:2345:3456:4567:5678:6789:7890:8901", FLAG_IPV6), ("2001:4860:4860:0000:0000:0000:0000:8888", FLAG_IPV6)]
+AGG_NETCOUNTERS = dict(
+    requests=[dict(pid=pid, host="host", url="/url", client_ip=ip, flags=fl | extra, time_ns=0)
+              for pid, extra in ((100, FLAG_UNENC), (200, FLAG_SSL)) for ip, fl in _NC_REQ],
+    expected=[dict(pid=100, endpoint="host/url", domain="host", scheme="http", internal=0, external=5),
+              dict(pid=200, endpoint="host/url", domain="host", scheme="https", internal=0, external=5)],
+    nets_v4_16=["ac8f", "acc7"], nets_v4_24=["ac8f04", "ac8f06", "acc72d"],
+    nets_v6=["200148604860", "123423453456"],
+    after_59min=dict(services=2, external=0, sizes=[2, 3, 2]),
+    after_60min=dict(services=0),
+)
+
 
 def main():
     out = dict(
@@ -246,6 +299,7 @@ def main():
         v6_iface=V6_IFACE_CASE, ntop=NTOP, lru=LRU_SCRIPTS,
         probe_parser=PROBE_PARSER, probe_split=[dict(value=v, expected=e) for v, e in PROBE_SPLIT],
         probe_pton4=[dict(text=t, expected=e) for t, e in PROBE_PTON4], config1=CONFIG1,
+        json_services=JSON_CASES, agg_netcounters=AGG_NETCOUNTERS,
     )
     with open(os.path.join(HERE, "reference_vectors.json"), "w") as f:
         json.dump(out, f, indent=1, ensure_ascii=True)

@@ -88,6 +88,12 @@ def lib():
         L.orc_lru_update.argtypes = [vp, C.c_uint32, C.c_int64]
         L.orc_lru_size.argtypes = [vp]
         L.orc_lru_size.restype = C.c_uint32
+        L.orc_set_network_counters.argtypes = [vp, C.c_int]
+        L.orc_set_time.argtypes = [vp, C.c_uint64]
+        L.orc_network_counters_cleaning.argtypes = [vp, C.c_uint64]
+        for f in ("orc_services_dump_nets", "orc_nets_dump", "orc_services_json"):
+            getattr(L, f).argtypes = [vp, vp, C.c_uint64]
+            getattr(L, f).restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -193,9 +199,11 @@ def parse_services(text: bytes):
 class Oracle:
     """Discovery + Aggregator replay (Discovery.cpp:73-198, Aggregator.cpp:155-168)."""
 
-    def __init__(self, lru_capacity=8192, v4_ifaces=None, v6_ifaces=None):
+    def __init__(self, lru_capacity=8192, v4_ifaces=None, v6_ifaces=None, network_counters=False):
         self.h = lib().orc_create(lru_capacity)
         self.set_interfaces(v4_ifaces or [], v6_ifaces or [])
+        if network_counters:
+            lib().orc_set_network_counters(self.h, 1)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -240,6 +248,39 @@ class Oracle:
             f = line.split(b"\t")
             rows.append((int(f[0]), f[1], f[2], f[3], int(f[4]), int(f[5]), int(f[6])))
         return rows
+
+    def _text(self, fn):
+        n = fn(self.h, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        fn(self.h, buf, n)
+        return buf.raw[:n]
+
+    def services_nets(self):
+        """services() rows with the sizes of the /16, /24 and v6 network maps appended."""
+        rows = []
+        for line in self._text(lib().orc_services_dump_nets).split(b"\n"):
+            if line:
+                f = line.split(b"\t")
+                rows.append((int(f[0]), f[1], f[2], f[3]) + tuple(int(x) for x in f[4:]))
+        return rows
+
+    def nets(self):
+        """sorted [(pid, endpoint, kind, prefix hex, time)] of every live network-map entry."""
+        rows = []
+        for line in self._text(lib().orc_nets_dump).split(b"\n"):
+            if line:
+                f = line.split(b"\t")
+                rows.append((int(f[0]), f[1], int(f[2]), f[3].decode(), int(f[4])))
+        return sorted(rows)
+
+    def services_json(self):
+        return self._text(lib().orc_services_json)
+
+    def set_time(self, now_ns):
+        lib().orc_set_time(self.h, now_ns)
+
+    def network_counters_cleaning(self, now_ns):
+        lib().orc_network_counters_cleaning(self.h, now_ns)
 
     def stats(self):
         s = Stats()

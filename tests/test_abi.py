@@ -35,8 +35,8 @@ def test_struct_layouts_match_header():
     assert ebd.EVENT_DTYPE.itemsize == 36          # DiscoveryEvent, Types.h:201-205
     assert ebd.RESULT_DTYPE.itemsize == 16
     assert ebd.SESSION_REQ_DTYPE.itemsize == 32
-    assert ebd.SERVICE_DTYPE.itemsize == 64
-    assert C.sizeof(ebd.Config) == 56  # static_assert in ebd_api.hip
+    assert ebd.SERVICE_DTYPE.itemsize == 80
+    assert C.sizeof(ebd.Config) == 64  # static_assert in ebd_api.hip
     assert C.sizeof(ebd.Stats) == 88
 
 

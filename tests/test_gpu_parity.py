@@ -248,7 +248,7 @@ def test_device_export_by_owner_and_merge_equals_whole_trace():
             ctx.submit(ev[idx], lens[idx], offs[idx], payload)
             recs, strs, counts, scounts = ctx.export_services_device(W, dev)
             if recs.numel():
-                words = recs.view(torch.int64).view(-1, 8)
+                words = recs.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)
                 words[:, 5] = torch.tensor(idx.astype(np.int64), device=dev)[words[:, 5]]
                 owner = (words[:, 6].cpu().numpy().view(np.uint64) % np.uint64(W)).astype(np.int64)
                 assert np.all(np.diff(owner) >= 0)  # grouped by owner
@@ -260,7 +260,7 @@ def test_device_export_by_owner_and_merge_equals_whole_trace():
             for r, s in segs[w]:
                 r = r.clone()
                 if r.numel():
-                    r.view(torch.int64).view(-1, 8)[:, 2] += base
+                    r.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)[:, 2] += base
                 rparts.append(r)
                 sparts.append(s)
                 base += s.numel()
