@@ -7,7 +7,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <sys/random.h>
 #include <time.h>
 #include <vector>
@@ -122,12 +124,6 @@ struct ebd_ctx {
 	unsigned long long* h_ctr = nullptr; // pinned
 	unsigned long long* d_cnt = nullptr;
 	ebd_service* d_collect = nullptr;
-	// host-batch staging
-	EventRec* d_ev = nullptr;
-	uint32_t* d_len = nullptr;
-	uint64_t* d_off = nullptr;
-	uint8_t* d_payload = nullptr;
-	uint64_t payload_cap = 0;
 	// exact LRU (allocated on first need): bound arrays, event -> position, session states
 	int* d_lru_delta = nullptr;
 	uint8_t* d_lru_minus = nullptr;
@@ -154,6 +150,35 @@ struct ebd_ctx {
 	uint64_t kbytes_cap = 0;
 	uint32_t* d_remap = nullptr;
 	ebd_service_net* d_netdump = nullptr;
+	// ingest pipeline (ebd_stage_batch / ebd_submit_staged): two device staging slots filled
+	// on the copy stream, pinned bounce buffers for pageable sources, results read back on the
+	// D2H stream.  Events: up = the slot's upload is done, used = the batch that read the slot
+	// is done (the slot may be refilled).
+	struct StageSlot {
+		EventRec* ev = nullptr;
+		uint32_t* len = nullptr;
+		uint64_t* off = nullptr;
+		uint8_t* payload = nullptr;
+		uint64_t pay_cap = 0;
+		uint32_t n = 0;
+		uint64_t ticket = 0;
+		int staged = 0, used_valid = 0;
+		hipEvent_t up = nullptr, used = nullptr;
+	};
+	hipStream_t cstream = nullptr, dstream = nullptr;
+	StageSlot stg[2];
+	int next_slot = 0;
+	uint64_t next_ticket = 1;
+	uint8_t* bounce[2] = {nullptr, nullptr};
+	hipEvent_t bounce_ev[2] = {nullptr, nullptr};
+	int bounce_valid[2] = {0, 0};
+	int bounce_next = 0;
+	// batch completion: mid = counters after the fresh pass are on the host; end = the
+	// session path's counters (h_end) are; batch = every kernel of the last batch finished;
+	// res = the async results read-back finished
+	hipEvent_t ev_mid = nullptr, ev_end = nullptr, ev_batch = nullptr, ev_res = nullptr;
+	int pending_end = 0, res_pending = 0, batch_valid = 0;
+	unsigned long long* h_end = nullptr; // pinned
 	// bookkeeping
 	unsigned long long seq_base = 0;
 	uint32_t last_n = 0;
@@ -266,7 +291,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
-			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_ev, c->d_len, c->d_off, c->d_payload, c->d_lru_delta, c->d_lru_minus,
+			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d, c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
 	for (void* p : ptrs)
@@ -274,6 +299,30 @@ static void ctx_free(ebd_ctx* c) {
 			(void)hipFree(p);
 	if (c->h_ctr)
 		(void)hipHostFree(c->h_ctr);
+	if (c->h_end)
+		(void)hipHostFree(c->h_end);
+	for (int k = 0; k < 2; k++) {
+		auto& g = c->stg[k];
+		void* sp[] = {g.ev, g.len, g.off, g.payload};
+		for (void* p : sp)
+			if (p)
+				(void)hipFree(p);
+		if (g.up)
+			(void)hipEventDestroy(g.up);
+		if (g.used)
+			(void)hipEventDestroy(g.used);
+		if (c->bounce[k])
+			(void)hipHostFree(c->bounce[k]);
+		if (c->bounce_ev[k])
+			(void)hipEventDestroy(c->bounce_ev[k]);
+	}
+	for (hipEvent_t e : {c->ev_mid, c->ev_end, c->ev_batch, c->ev_res})
+		if (e)
+			(void)hipEventDestroy(e);
+	if (c->cstream)
+		(void)hipStreamDestroy(c->cstream);
+	if (c->dstream)
+		(void)hipStreamDestroy(c->dstream);
 	for (auto& t : c->pending) {
 		(void)hipEventDestroy(t.a);
 		(void)hipEventDestroy(t.b);
@@ -350,6 +399,11 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		}                                                                                                            \
 	} while (0)
 	CTX_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+	CTX_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+	CTX_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+	for (hipEvent_t* e : {&c->ev_mid, &c->ev_end, &c->ev_batch, &c->ev_res, &c->stg[0].up, &c->stg[0].used, &c->stg[1].up,
+			 &c->stg[1].used, &c->bounce_ev[0], &c->bounce_ev[1]})
+		CTX_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
 	// tables derived from the parser semantics (ebd_spec.h)
 	build_key_trie(&c->trie_host);
 	c->dfa_host = new DfaTable();
@@ -405,6 +459,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_COUNT * sizeof(unsigned long long), c->stream));
 	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
 	CTX_TRY(hipHostMalloc(&c->h_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long), hipHostMallocDefault));
+	CTX_TRY(hipHostMalloc(&c->h_end, CTR_COUNT * sizeof(unsigned long long), hipHostMallocDefault));
 	if (cfg->flags & EBD_CFG_NETWORK_COUNTERS) {
 		c->net_on = 1;
 		c->net_cap = next_pow2(cfg->net_capacity ? cfg->net_capacity : (1u << 22));
@@ -462,11 +517,39 @@ int ebd_set_interfaces(ebd_ctx* c, const ebd_ipv4_network* v4, uint32_t n4, cons
 	return 0;
 }
 
+// The session path's end-of-batch counters (carried sessions, session requests) of the
+// previous batch: read when the next call needs them, not at the end of the batch.
+static int finish_pending(ebd_ctx* c) {
+	if (!c->pending_end)
+		return 0;
+	HIP_TRY(hipEventSynchronize(c->ev_end));
+	c->pending_end = 0;
+	const uint64_t co = c->h_end[CTR_CARRY_OUT];
+	c->n_carry = (uint32_t)(co < c->carry_cap ? co : c->carry_cap);
+	c->carry_cur ^= 1;
+	c->last_sreq = c->h_end[CTR_SREQ];
+	c->last_sstr = c->h_end[CTR_SSTR];
+	const uint64_t bound = c->n_carry + c->h_end[CTR_INSERTS];
+	if (bound > c->max_live)
+		c->max_live = bound;
+	return 0;
+}
+
+// One poll cycle on the context stream.  The host waits once, for the counters after the
+// fresh pass (is there session work?), while k_agg_fast already runs; a batch without session
+// work returns with its kernels still queued, and a batch with some returns once the session
+// path is queued (its carried-session count is read by the next call, finish_pending).
 static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const uint64_t* off, const uint8_t* payload,
 		uint32_t n) {
 	if (n > c->max_events)
 		return -EINVAL;
 	HIP_TRY(hipSetDevice(c->device));
+	if (int rc = finish_pending(c))
+		return rc;
+	if (c->res_pending) { // the previous results are being read back: k_fresh rewrites them
+		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_res, 0));
+		c->res_pending = 0;
+	}
 	Dev d = make_dev(c);
 	d.ev = ev;
 	d.len = len;
@@ -479,6 +562,8 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_BATCH_END * sizeof(unsigned long long), c->stream));
 	if (n == 0) {
 		c->last_sreq = c->last_sstr = 0;
+		HIP_TRY(hipEventRecord(c->ev_batch, c->stream));
+		c->batch_valid = 1;
 		return 0;
 	}
 	if (c->n_carry)
@@ -486,8 +571,13 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	HIP_TRY(timed(c, KT_FRESH, [&] { return launch_fresh(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipEventRecord(c->ev_mid, c->stream));
+	// Aggregator::newRequest for the fast-path requests: independent of the session path
+	// (k_slow_collect marked the session events, counters and first arrival are order-free)
+	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
+	HIP_TRY(hipEventSynchronize(c->ev_mid));
 	const uint64_t nslow = c->h_ctr[CTR_SLOW];
+	const uint64_t dirty = c->h_ctr[CTR_DIRTY];
 	if (nslow > 0) {
 		c->last_slow_ran = 1;
 		int end_bit = 32;
@@ -502,7 +592,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		// LRU eviction possible?  Only if more sessions than its capacity could be live at once
 		// (k_walk_lru's comment): first the cheap count of candidate sessions, then the bound.
 		bool exact = false;
-		if (c->h_ctr[CTR_DIRTY] > c->carry_cap) {
+		if (dirty > c->carry_cap) {
 			const uint64_t nb = (uint64_t)c->max_events;
 			if (!c->d_lru_delta) {
 				HIP_TRY(hipMalloc(&c->d_lru_delta, nb * sizeof(int)));
@@ -542,24 +632,18 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 				HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
 		}
 	}
-	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
-	if (c->h_ctr[CTR_DIRTY])
+	if (dirty)
 		HIP_TRY(timed(c, KT_SSET_CLEAR, [&] { return launch_sset_clear(d, c->stream, c->cus); }));
 	if (nslow > 0) {
-		HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-		HIP_TRY(hipStreamSynchronize(c->stream));
-		uint64_t co = c->h_ctr[CTR_CARRY_OUT];
-		c->n_carry = (uint32_t)(co < c->carry_cap ? co : c->carry_cap);
-		c->carry_cur ^= 1;
-		c->last_sreq = c->h_ctr[CTR_SREQ];
-		c->last_sstr = c->h_ctr[CTR_SSTR];
-		uint64_t bound = c->n_carry + c->h_ctr[CTR_INSERTS];
-		if (bound > c->max_live)
-			c->max_live = bound;
+		HIP_TRY(hipMemcpyAsync(c->h_end, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(hipEventRecord(c->ev_end, c->stream));
+		c->pending_end = 1;
 	} else {
 		c->last_sreq = c->last_sstr = 0;
 	}
+	HIP_TRY(hipEventRecord(c->ev_batch, c->stream));
+	c->batch_valid = 1;
 	c->seq_base += n;
 	c->events_total += n;
 	return 0;
@@ -616,49 +700,216 @@ int ebd_reset_kernel_times(ebd_ctx* c) {
 int ebd_sync(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipStreamSynchronize(c->cstream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipStreamSynchronize(c->dstream));
+	c->res_pending = 0;
+	return finish_pending(c);
+}
+
+// ---- ingest pipeline ---------------------------------------------------------------
+// Discovery::fetchAndHandleEvents drains the BPF queue and copies every event's 8196-B saved
+// buffer (Discovery.cpp:73-110).  Here a host batch is uploaded into one of two device
+// staging slots on the copy stream while the compute stream works on the previous batch.
+// Pinned sources (ebd_host_alloc, or hipHostRegister'ed) are DMAed directly; pageable ones go
+// through two pinned bounce buffers, the CPU copy of one chunk overlapping the DMA of the other.
+static constexpr size_t kBounce = 32ull << 20;
+
+static bool host_pinned(const void* p) {
+	hipPointerAttribute_t a;
+	if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+		(void)hipGetLastError();
+		return false;
+	}
+	return a.type == hipMemoryTypeHost;
+}
+
+// memcpy with up to 4 threads for large chunks (one core copies ~10 GB/s, below PCIe).
+static void par_memcpy(void* dst, const void* src, size_t n) {
+	constexpr size_t kPart = 4ull << 20;
+	if (n < 2 * kPart) {
+		std::memcpy(dst, src, n);
+		return;
+	}
+	const int t = 4;
+	const size_t part = (n + t - 1) / t;
+	std::thread th[t - 1];
+	for (int k = 1; k < t; k++) {
+		const size_t a = k * part, z = std::min(n, a + part);
+		th[k - 1] = std::thread([=] { std::memcpy((char*)dst + a, (const char*)src + a, z - a); });
+	}
+	std::memcpy(dst, src, std::min(n, part));
+	for (auto& x : th)
+		x.join();
+}
+
+static int upload(ebd_ctx* c, void* dst, const void* src, size_t bytes) {
+	if (!bytes)
+		return 0;
+	if (host_pinned(src)) {
+		HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->cstream));
+		return 0;
+	}
+	for (int k = 0; k < 2; k++)
+		if (!c->bounce[k])
+			HIP_TRY(hipHostMalloc(&c->bounce[k], kBounce, hipHostMallocDefault));
+	for (size_t o = 0; o < bytes; o += kBounce) {
+		const size_t m = std::min(kBounce, bytes - o);
+		const int b = c->bounce_next;
+		c->bounce_next ^= 1;
+		if (c->bounce_valid[b]) // its previous chunk has left for the device
+			HIP_TRY(hipEventSynchronize(c->bounce_ev[b]));
+		par_memcpy(c->bounce[b], (const char*)src + o, m);
+		HIP_TRY(hipMemcpyAsync((char*)dst + o, c->bounce[b], m, hipMemcpyHostToDevice, c->cstream));
+		HIP_TRY(hipEventRecord(c->bounce_ev[b], c->cstream));
+		c->bounce_valid[b] = 1;
+	}
 	return 0;
 }
 
-int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+static int validate_batch(const ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
 		const uint8_t* payload, uint64_t payload_bytes, uint32_t n) {
-	if (!c || (n && (!events || !len || !off || (!payload && payload_bytes))))
+	if (n && (!events || !len || !off || (!payload && payload_bytes)))
 		return -EINVAL;
 	if (n > c->max_events)
 		return -EINVAL;
 	for (uint32_t i = 0; i < n; i++) // buffers must lie inside the arena
 		if (len[i] != EBD_NO_BUFFER && (len[i] > EBD_BUFFER_MAX_DATA_SIZE || off[i] > payload_bytes || payload_bytes - off[i] < len[i]))
 			return -EINVAL;
-	std::lock_guard<std::mutex> lk(c->mu);
+	return 0;
+}
+
+static int stage_locked(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n, uint64_t* ticket) {
 	HIP_TRY(hipSetDevice(c->device));
-	if (!c->d_ev) {
-		HIP_TRY(hipMalloc(&c->d_ev, (size_t)c->max_events * sizeof(EventRec)));
-		HIP_TRY(hipMalloc(&c->d_len, (size_t)c->max_events * sizeof(uint32_t)));
-		HIP_TRY(hipMalloc(&c->d_off, (size_t)c->max_events * sizeof(uint64_t)));
+	const int s = c->next_slot;
+	auto& g = c->stg[s];
+	if (g.staged)
+		return -EBUSY; // two batches are already staged and not submitted
+	c->next_slot ^= 1;
+	if (!g.ev) {
+		HIP_TRY(hipMalloc(&g.ev, (size_t)c->max_events * sizeof(EventRec)));
+		HIP_TRY(hipMalloc(&g.len, (size_t)c->max_events * sizeof(uint32_t)));
+		HIP_TRY(hipMalloc(&g.off, (size_t)c->max_events * sizeof(uint64_t)));
 	}
 	const uint64_t need = payload_bytes + EBD_PAYLOAD_PAD;
-	if (need > c->payload_cap) {
-		if (c->d_payload)
-			HIP_TRY(hipFree(c->d_payload));
-		c->payload_cap = need < c->cfg.max_payload ? c->cfg.max_payload : need;
-		HIP_TRY(hipMalloc(&c->d_payload, c->payload_cap));
+	if (need > g.pay_cap) {
+		if (g.payload) {
+			if (g.used_valid)
+				HIP_TRY(hipEventSynchronize(g.used));
+			HIP_TRY(hipFree(g.payload));
+		}
+		g.pay_cap = need < c->cfg.max_payload ? c->cfg.max_payload : need;
+		HIP_TRY(hipMalloc(&g.payload, g.pay_cap));
 	}
-	if (n) {
-		HIP_TRY(hipMemcpyAsync(c->d_ev, events, (size_t)n * sizeof(EventRec), hipMemcpyHostToDevice, c->stream));
-		HIP_TRY(hipMemcpyAsync(c->d_len, len, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-		HIP_TRY(hipMemcpyAsync(c->d_off, off, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-		if (payload_bytes)
-			HIP_TRY(hipMemcpyAsync(c->d_payload, payload, payload_bytes, hipMemcpyHostToDevice, c->stream));
-	}
+	if (g.used_valid) // the batch that last read this slot must be done with it
+		HIP_TRY(hipStreamWaitEvent(c->cstream, g.used, 0));
+	if (int rc = upload(c, g.ev, events, (size_t)n * sizeof(EventRec)))
+		return rc;
+	if (int rc = upload(c, g.len, len, (size_t)n * sizeof(uint32_t)))
+		return rc;
+	if (int rc = upload(c, g.off, off, (size_t)n * sizeof(uint64_t)))
+		return rc;
+	if (int rc = upload(c, g.payload, payload, payload_bytes))
+		return rc;
+	HIP_TRY(hipEventRecord(g.up, c->cstream));
+	g.n = n;
+	g.staged = 1;
+	g.ticket = c->next_ticket++;
+	*ticket = g.ticket;
+	return 0;
+}
+
+static int submit_staged_locked(ebd_ctx* c, uint64_t ticket) {
+	int s = -1;
+	for (int k = 0; k < 2; k++)
+		if (c->stg[k].staged && c->stg[k].ticket == ticket)
+			s = k;
+	if (s < 0)
+		return -EINVAL;
+	auto& g = c->stg[s];
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipStreamWaitEvent(c->stream, g.up, 0)); // the device waits for the upload, not the host
 	if (std::getenv("EBD_DEBUG_PTRS")) // fault triage: the device ranges a batch uses
-		std::fprintf(stderr, "ebd: batch n=%u payload=[%p, +%llu) ev=%p len=%p off=%p res=%p keys=%p sset=%p carry=%p/%p\n", n,
-				(void*)c->d_payload, (unsigned long long)c->payload_cap, (void*)c->d_ev, (void*)c->d_len, (void*)c->d_off,
-				(void*)c->d_res, (void*)c->d_keys, (void*)c->d_sset, (void*)c->d_carry[0], (void*)c->d_carry[1]);
-	int rc = run_batch(c, c->d_ev, c->d_len, c->d_off, c->d_payload, n);
-	if (rc)
+		std::fprintf(stderr, "ebd: batch n=%u payload=[%p, +%llu) ev=%p len=%p off=%p res=%p keys=%p sset=%p carry=%p/%p\n", g.n,
+				(void*)g.payload, (unsigned long long)g.pay_cap, (void*)g.ev, (void*)g.len, (void*)g.off, (void*)c->d_res,
+				(void*)c->d_keys, (void*)c->d_sset, (void*)c->d_carry[0], (void*)c->d_carry[1]);
+	g.staged = 0;
+	const int rc = run_batch(c, g.ev, g.len, g.off, g.payload, g.n);
+	HIP_TRY(hipEventRecord(g.used, c->stream));
+	g.used_valid = 1;
+	return rc;
+}
+
+int ebd_stage_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n, uint64_t* ticket) {
+	if (!c || !ticket)
+		return -EINVAL;
+	if (int rc = validate_batch(c, events, len, off, payload, payload_bytes, n))
+		return rc;
+	std::lock_guard<std::mutex> lk(c->mu);
+	return stage_locked(c, events, len, off, payload, payload_bytes, n, ticket);
+}
+
+int ebd_submit_staged(ebd_ctx* c, uint64_t ticket) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	return submit_staged_locked(c, ticket);
+}
+
+int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n) {
+	if (!c)
+		return -EINVAL;
+	if (int rc = validate_batch(c, events, len, off, payload, payload_bytes, n))
+		return rc;
+	std::lock_guard<std::mutex> lk(c->mu);
+	uint64_t t = 0;
+	if (int rc = stage_locked(c, events, len, off, payload, payload_bytes, n, &t))
+		return rc;
+	if (int rc = submit_staged_locked(c, t))
 		return rc;
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	return finish_pending(c);
+}
+
+void* ebd_host_alloc(ebd_ctx* c, uint64_t bytes) {
+	if (!c || !bytes)
+		return nullptr;
+	void* p = nullptr;
+	if (hipSetDevice(c->device) != hipSuccess || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+		(void)hipGetLastError();
+		return nullptr;
+	}
+	return p;
+}
+
+int ebd_host_free(ebd_ctx* c, void* p) {
+	if (!c)
+		return -EINVAL;
+	if (p)
+		HIP_TRY(hipHostFree(p));
+	return 0;
+}
+
+int ebd_fetch_results_async(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t* n) {
+	if (!c || !n || (cap && !out))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	*n = c->last_n;
+	if (cap < c->last_n)
+		return -ENOSPC;
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->last_n)
+		return 0;
+	if (c->batch_valid)
+		HIP_TRY(hipStreamWaitEvent(c->dstream, c->ev_batch, 0));
+	HIP_TRY(hipMemcpyAsync(out, c->d_res, (size_t)c->last_n * sizeof(ebd_event_result), hipMemcpyDeviceToHost, c->dstream));
+	HIP_TRY(hipEventRecord(c->ev_res, c->dstream));
+	c->res_pending = 1;
 	return 0;
 }
 
@@ -683,6 +934,8 @@ int ebd_fetch_session_requests(ebd_ctx* c, ebd_session_request* out, uint32_t ca
 	if (!c || !n || !strlen)
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
+	if (int rc = finish_pending(c))
+		return rc;
 	*n = (uint32_t)c->last_sreq;
 	*strlen = c->last_sstr < c->sstr_cap ? c->last_sstr : c->sstr_cap;
 	if (!out)
@@ -905,6 +1158,8 @@ int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
+	if (int rc = finish_pending(c))
+		return rc;
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	std::memset(s, 0, sizeof(*s));

@@ -907,6 +907,7 @@ __global__ void k_slow_collect(Dev d) {
 			continue;
 		const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
 		if (slot >= 0) {
+			d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
 			atomicMax(&d.sset[slot].last_ev, i + 1);
 			const unsigned long long k = atomicAdd(&d.ctr[CTR_SLOW], 1ull);
 			d.slow_keys[k] = ((unsigned long long)(uint32_t)slot << 32) | i;
@@ -1502,8 +1503,8 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 	const uint32_t per = (steps + gridDim.x - 1) / gridDim.x;
 	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
 	for (uint32_t st = s0; st < s1; st++) { // uniform trip count: the barriers below are safe
-		PendingClaim pc[2];
-		bool has[2] = {false, false};
+		PendingClaim pc[3];
+		bool has[3] = {false, false, false};
 		const uint32_t i = st * kAggThreads + threadIdx.x;
 		if (i < d.n) {
 			ebd_event_result r = d.res[i];
@@ -1538,6 +1539,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 				sh.qn = m >= kAggThreads ? m - kAggThreads : 0;
 		}
 		__syncthreads();
+		if (last && m > kAggThreads) { // the block's last step: what one drain left goes too
+			if (threadIdx.x < m - kAggThreads)
+				agg_cip_one(d, sh.q[threadIdx.x], row, sh, pc[2], has[2]);
+			if (threadIdx.x == 0)
+				sh.qn = 0;
+			__syncthreads();
+		}
 		// this step's claims: one reservation of list entries and arena bytes for the block
 		if (threadIdx.x == 0) {
 			const uint32_t cn = sh.cn;
@@ -1550,7 +1558,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 		}
 		__syncthreads();
 #pragma unroll
-		for (int k = 0; k < 2; k++)
+		for (int k = 0; k < 3; k++)
 			if (has[k])
 				claim_publish(d, pc[k].slot, sh.list_base + pc[k].li, sh.arena_base + pc[k].ab, pc[k].pid, pc[k].host, pc[k].hl,
 						pc[k].url, pc[k].ul);

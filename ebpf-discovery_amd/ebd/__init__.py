@@ -95,6 +95,12 @@ _SIGS = {
     "ebd_submit_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                    C.c_uint32]),
     "ebd_submit_batch_device": (C.c_int, [C.c_void_p, C.POINTER(DeviceBatch)]),
+    "ebd_stage_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32,
+                                  C.POINTER(C.c_uint64)]),
+    "ebd_submit_staged": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "ebd_host_alloc": (C.c_void_p, [C.c_void_p, C.c_uint64]),
+    "ebd_host_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ebd_fetch_results_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     "ebd_sync": (C.c_int, [C.c_void_p]),
     "ebd_set_seq_base": (C.c_int, [C.c_void_p, C.c_uint64]),
     "ebd_kernel_times": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -242,6 +248,38 @@ class Context:
         payload = np.ascontiguousarray(payload, dtype=np.uint8)
         _check(lib().ebd_submit_batch(self.h, _p(events), _p(lens), _p(offs), _p(payload), payload.size,
                                       len(events)), "ebd_submit_batch")
+
+    def stage(self, events, lens, offs, payload):
+        """ebd_stage_batch: uploads a host batch on the copy stream; returns its ticket."""
+        events = np.ascontiguousarray(events, dtype=EVENT_DTYPE)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        t = C.c_uint64()
+        _check(lib().ebd_stage_batch(self.h, _p(events), _p(lens), _p(offs), _p(payload), payload.size, len(events),
+                                     C.byref(t)), "ebd_stage_batch")
+        return t.value
+
+    def submit_staged(self, ticket):
+        _check(lib().ebd_submit_staged(self.h, ticket), "ebd_submit_staged")
+
+    def pinned_empty(self, n, dtype):
+        """A numpy array over pinned host memory (ebd_host_alloc), freed with the array."""
+        import weakref
+        dtype = np.dtype(dtype)
+        nbytes = max(int(n) * dtype.itemsize, 1)
+        p = lib().ebd_host_alloc(self.h, nbytes)
+        if not p:
+            raise EbdError("ebd_host_alloc failed")
+        buf = (C.c_uint8 * nbytes).from_address(p)
+        weakref.finalize(buf, lib().ebd_host_free, self.h, C.c_void_p(p))
+        return np.frombuffer(buf, dtype=dtype, count=int(n))
+
+    def results_async(self, out):
+        """ebd_fetch_results_async into `out` (RESULT_DTYPE, ideally pinned); valid after sync()."""
+        n = C.c_uint32()
+        _check(lib().ebd_fetch_results_async(self.h, _p(out), out.size, C.byref(n)), "ebd_fetch_results_async")
+        return n.value
 
     def submit_device(self, events, lens, offs, payload, n):
         """Device-resident batch (torch tensors on the context's device or raw pointers)."""

@@ -237,14 +237,31 @@ int ebd_get_hash_key(ebd_ctx* ctx, uint64_t out[2]);
  * InterfacesReader.cpp:50-78) — injected, because it is host dependent. */
 int ebd_set_interfaces(ebd_ctx* ctx, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6);
 
-/* One poll cycle (Discovery::fetchAndHandleEvents): events[i] with its saved buffer at
- * payload + off[i], len[i] bytes (len <= 8192, or EBD_NO_BUFFER).  Host memory: the
- * batch is staged through pinned memory.  Blocks until the batch is processed. */
+/* One poll cycle (Discovery::fetchAndHandleEvents, Discovery.cpp:73-121): events[i] with its
+ * saved buffer at payload + off[i], len[i] bytes (len <= 8192, or EBD_NO_BUFFER).  Host
+ * memory, uploaded as ebd_stage_batch does.  Blocks until the batch is processed. */
 int ebd_submit_batch(ebd_ctx* ctx, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
 		const uint8_t* payload, uint64_t payload_bytes, uint32_t n);
-/* The same with the batch already in HBM.  Asynchronous: enqueued on the context stream. */
+/* The same with the batch already in HBM.  The host waits only for the fresh pass's counters
+ * (is there session work?); the rest stays queued on the context stream (ebd_sync). */
 int ebd_submit_batch_device(ebd_ctx* ctx, const ebd_device_batch* batch);
+/* Waits for every queued upload, batch and read-back of the context. */
 int ebd_sync(ebd_ctx* ctx);
+
+/* --- ingest pipeline (Discovery.cpp:73-110: drain, saved-buffer fetch) ------------------
+ * ebd_stage_batch uploads a host batch into one of two device staging slots on the context's
+ * copy stream and returns without waiting for the DMA; ebd_submit_staged runs it (the compute
+ * stream, not the host, waits for the upload).  Staging batch k+1 before submitting batch k
+ * overlaps its H2D with batch k's kernels.  Pinned sources (ebd_host_alloc) are DMAed as they
+ * are and must stay unchanged until the batch is submitted and synced; pageable sources are
+ * copied through pinned bounce buffers (CPU copy overlapping the DMA) and may be reused as
+ * soon as the call returns.  At most two batches are staged and not yet submitted (-EBUSY). */
+int ebd_stage_batch(ebd_ctx* ctx, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
+		const uint8_t* payload, uint64_t payload_bytes, uint32_t n, uint64_t* ticket);
+int ebd_submit_staged(ebd_ctx* ctx, uint64_t ticket);
+/* Pinned host memory for producers that fill batches in place (no staging copy). */
+void* ebd_host_alloc(ebd_ctx* ctx, uint64_t bytes);
+int ebd_host_free(ebd_ctx* ctx, void* p);
 /* Global order of the next submitted event (default: events submitted so far).  Shards of
  * one trace set it to their first global event index so first-arrival ties resolve in
  * trace order after the cross-GPU merge. */
@@ -262,6 +279,9 @@ int ebd_reset_kernel_times(ebd_ctx* ctx);
 
 /* Per-event results of the last batch (host copy), n <= cap. */
 int ebd_fetch_results(ebd_ctx* ctx, ebd_event_result* out, uint32_t cap, uint32_t* n);
+/* The same read back on the context's D2H stream once the batch is done, without blocking
+ * (out should be pinned); complete after ebd_sync.  The next batch's kernels wait for it. */
+int ebd_fetch_results_async(ebd_ctx* ctx, ebd_event_result* out, uint32_t cap, uint32_t* n);
 /* Device pointer to the last batch's per-event results (valid until the next submit). */
 const ebd_event_result* ebd_results_device(ebd_ctx* ctx);
 /* Session-path requests of the last batch and their strings. */
