@@ -864,6 +864,10 @@ struct orc_ctx {
 	dstr blob;
 	orc_stats st;
 	uint64_t cur_event; /* index of the event being handled, over all orc_process calls */
+	struct {
+		uint32_t length;
+		uint8_t data[8192 + 16]; /* + the 16 readable pad bytes some callers pass after a buffer */
+	} saved;                    /* DiscoverySavedBuffer, Types.h:58-61 */
 	int netcounters;    /* Aggregator(..., enableNetworkCounters) A:132-134 */
 	uint64_t now;       /* getCurrentTime() (A:211-213) for the next requests */
 	net_ent* nt;
@@ -1586,7 +1590,14 @@ int orc_process(orc_ctx* c, const orc_event* ev, const uint32_t* len, const uint
 			if (len[i] == UINT32_MAX) {
 				c->st.missing_buffers++;
 			} else {
-				const uint8_t* buf = payload + off[i];
+				/* D:102-103: bpf_map_lookup_and_delete_elem copies the whole DiscoverySavedBuffer
+				 * (4-B length + 8192-B data, Types.h:58-61) into a stack object, whatever the
+				 * length: the same copy here keeps the baseline's cost faithful */
+				memcpy(c->saved.data, payload + off[i], len[i] <= sizeof(c->saved.data) ? len[i] : sizeof(c->saved.data));
+				memset(c->saved.data + (len[i] < sizeof(c->saved.data) ? len[i] : sizeof(c->saved.data)), 0,
+						sizeof(c->saved.data) - (len[i] < sizeof(c->saved.data) ? len[i] : sizeof(c->saved.data)));
+				c->saved.length = len[i];
+				const uint8_t* buf = c->saved.data;
 				/* D:112-121 handleBufferLookupSuccess: find() touches the LRU entry */
 				uint32_t k[3] = {e->pid, e->fd, e->sessionID};
 				lru_node* nd = lru_find(&c->sessions, k);
