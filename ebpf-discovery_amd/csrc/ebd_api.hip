@@ -32,9 +32,10 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_publish(const Dev& d, hipStream_t st, int cus);
+uint32_t agg_stage_per_block(uint32_t n, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
-hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
-		ebd_service* out, hipStream_t st, int cus);
+hipError_t launch_collect(const Dev& d, ebd_service* out, hipStream_t st, int cus);
 hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
 		uint32_t count, uint32_t index, unsigned long long* alen, uint32_t* keep, hipStream_t st);
@@ -72,6 +73,8 @@ static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 80 && siz
 		}                                                                                                            \
 	} while (0)
 
+static constexpr uint32_t kMaxAggBlocks = 2048; // k_agg_fast's grid: at most cus * 8 (k_pub_scan scans 2 per thread)
+
 static uint32_t next_pow2(uint64_t v) {
 	uint64_t p = 1;
 	while (p < v)
@@ -98,6 +101,11 @@ struct ebd_ctx {
 	Slot* d_slots = nullptr;
 	uint32_t slot_cap = 0;
 	uint32_t* d_new_slots = nullptr;
+	uint32_t* d_cstage = nullptr; // claim stage: slots then events, max_events + blocks of slack each
+	uint64_t cstage_cap = 0;
+	uint32_t* d_blk = nullptr;    // blk_cnt, blk_bytes (u32) then blk_lbase, blk_abase (u64)
+	unsigned long long* d_list_ep = nullptr;
+	unsigned long long* d_list_pl = nullptr;
 	uint32_t new_cap = 0;
 	VerifyRec* d_verify = nullptr;
 	uint32_t verify_cap = 0;
@@ -198,8 +206,8 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_reps", "k_sset_clear", "k_verify", "k_clear_used"};
-enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_REPS, KT_SSET_CLEAR, KT_VERIFY,
+		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used"};
+enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_PUBLISH, KT_SSET_CLEAR, KT_VERIFY,
 	KT_CLEAR, KT_N };
 
 static hipEvent_t take_event(ebd_ctx* c) {
@@ -251,6 +259,15 @@ static Dev make_dev(ebd_ctx* c) {
 	d.slots = c->d_slots;
 	d.slot_mask = c->slot_cap - 1;
 	d.new_slots = c->d_new_slots;
+	d.cstage_slot = c->d_cstage;
+	d.cstage_ev = c->d_cstage + c->cstage_cap;
+	d.cstage_per = 0;
+	d.blk_cnt = c->d_blk;
+	d.blk_bytes = c->d_blk + kMaxAggBlocks;
+	d.blk_lbase = (unsigned long long*)(c->d_blk + 2 * kMaxAggBlocks);
+	d.blk_abase = d.blk_lbase + kMaxAggBlocks;
+	d.list_ep = c->d_list_ep;
+	d.list_pl = c->d_list_pl;
 	d.new_cap = c->new_cap;
 	d.verify = c->d_verify;
 	d.verify_cap = c->verify_cap;
@@ -289,7 +306,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 }
 
 static void ctx_free(ebd_ctx* c) {
-	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
+	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
@@ -427,6 +444,13 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(launch_slots_init(c->d_slots, c->slot_cap, c->stream));
 	c->new_cap = c->slot_cap; // claimed-slot list, cumulative until ebd_clear
 	CTX_TRY(hipMalloc(&c->d_new_slots, (size_t)c->new_cap * sizeof(uint32_t)));
+	// one stretch of per-block capacity per k_agg_fast block: grid * ceil(steps / grid) steps of
+	// kAggThreads events, below (steps + grid) * kAggThreads for any batch up to max_events
+	c->cstage_cap = (((uint64_t)c->max_events + 255) / 256 + kMaxAggBlocks) * 256;
+	CTX_TRY(hipMalloc(&c->d_cstage, 2 * c->cstage_cap * sizeof(uint32_t)));
+	CTX_TRY(hipMalloc(&c->d_blk, (size_t)kMaxAggBlocks * (2 * sizeof(uint32_t) + 2 * sizeof(unsigned long long))));
+	CTX_TRY(hipMalloc(&c->d_list_ep, (size_t)c->new_cap * sizeof(unsigned long long)));
+	CTX_TRY(hipMalloc(&c->d_list_pl, (size_t)c->new_cap * sizeof(unsigned long long)));
 	c->verify_cap = c->max_events;
 	CTX_TRY(hipMalloc(&c->d_verify, (size_t)c->verify_cap * sizeof(VerifyRec)));
 	c->sarena_cap = cfg->string_arena ? cfg->string_arena : (256ull << 20);
@@ -557,6 +581,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	d.payload = payload;
 	d.n = n;
 	d.now = ctx_now(c);
+	d.cstage_per = agg_stage_per_block(n, c->cus);
 	c->last_n = n;
 	c->last_slow_ran = 0;
 	HIP_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_BATCH_END * sizeof(unsigned long long), c->stream));
@@ -575,6 +600,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	// Aggregator::newRequest for the fast-path requests: independent of the session path
 	// (k_slow_collect marked the session events, counters and first arrival are order-free)
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_PUBLISH, [&] { return launch_publish(d, c->stream, c->cus); }));
 	HIP_TRY(hipEventSynchronize(c->ev_mid));
 	const uint64_t nslow = c->h_ctr[CTR_SLOW];
 	const uint64_t dirty = c->h_ctr[CTR_DIRTY];
@@ -972,7 +998,7 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 	if (cnt) {
 		if (!c->d_collect)
 			HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-		HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_sarena, c->d_collect, c->stream, c->cus));
+		HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
 		HIP_TRY(hipMemcpyAsync(out, c->d_collect, cnt * sizeof(ebd_service), hipMemcpyDeviceToHost, c->stream));
 	}
 	if (used)
@@ -1106,7 +1132,7 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, ui
 	unsigned long long* own = nullptr; // cnt, bytes, cur, scur, sbase: world each
 	HIP_TRY(hipMallocAsync((void**)&own, 5 * 64 * sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(own, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
-	HIP_TRY(launch_collect(c->d_slots, c->d_new_slots, c->d_ctr, c->d_sarena, c->d_collect, c->stream, c->cus));
+	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
 	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, own, own + 64, c->stream, c->cus));
 	unsigned long long h[5 * 64];
 	HIP_TRY(hipMemcpyAsync(h, own, 2 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));

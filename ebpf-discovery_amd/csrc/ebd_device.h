@@ -14,9 +14,8 @@ struct Slot {
 	unsigned long long tag;    // Hash128.lo of (pid, endpoint); 0 = empty; claimed by CAS
 	unsigned long long hi;     // Hash128.hi, published by the claimer
 	unsigned long long first;  // min over requests of seq << 16 | isHttps << 15 | host length (atomicMin)
-	unsigned long long ep_off; // endpoint bytes in the string arena (claimer)
-	unsigned int pid;          // (claimer, one 8-byte store with ep_len)
-	unsigned int ep_len;
+	unsigned long long pad0[2]; // (the endpoint's arena offset, pid and length live beside the
+	                            //  claimed-slot list, Dev::list_ep / list_pl: written in list order)
 	unsigned int internal_clients; // uint32, wraps like Service.h:53-54
 	unsigned int external_clients;
 	unsigned int nets[3];          // network-map sizes: v4 /16, v4 /24, v6 /48 (Service.h:56-58)
@@ -138,7 +137,18 @@ struct Dev {
 	Slot* slots;
 	uint32_t slot_mask;
 	uint32_t* new_slots;
+	unsigned long long* list_ep; // beside new_slots: the endpoint's arena offset (~0: none)
+	unsigned long long* list_pl; // beside new_slots: pid | endpoint length << 32
 	uint32_t new_cap;
+	// k_agg_fast's claims, block b's at [b * cstage_per, + blk_cnt[b]): slot and claiming event;
+	// the publication kernels' per-block byte counts and list / arena bases
+	uint32_t* cstage_slot;
+	uint32_t* cstage_ev;
+	uint32_t cstage_per;
+	uint32_t* blk_cnt;
+	uint32_t* blk_bytes;
+	unsigned long long* blk_lbase;
+	unsigned long long* blk_abase;
 	VerifyRec* verify;
 	uint32_t verify_cap;
 	uint8_t* sarena;

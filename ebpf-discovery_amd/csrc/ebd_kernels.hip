@@ -144,11 +144,12 @@ __device__ __forceinline__ void copy_endpoint(unsigned long long* dst, const uin
 // list_at: its position in the claimed-slot list; ep_at: its (8-aligned) arena offset.
 __device__ void claim_publish(const Dev& d, uint32_t idx, unsigned long long list_at, unsigned long long ep_at, uint32_t pid,
 		const uint8_t* host, uint32_t hl, const uint8_t* url, uint32_t ul) {
-	Slot* s = d.slots + idx;
-	if (list_at < d.new_cap)
+	if (list_at < d.new_cap) {
 		d.new_slots[list_at] = idx;
-	else
+	} else {
 		set_error(d, EBD_ERR_TABLE_FULL);
+		return;
+	}
 	const uint32_t n = hl + ul;
 	unsigned long long off = ~0ull;
 	if (ep_at + n <= d.sarena_cap) {
@@ -157,8 +158,8 @@ __device__ void claim_publish(const Dev& d, uint32_t idx, unsigned long long lis
 	} else {
 		set_error(d, EBD_ERR_ARENA_FULL);
 	}
-	atomicExch(&s->ep_off, off);
-	atomicExch((unsigned long long*)&s->pid, (unsigned long long)pid | ((unsigned long long)n << 32)); // pid, ep_len
+	d.list_ep[list_at] = off;
+	d.list_pl[list_at] = (unsigned long long)pid | ((unsigned long long)n << 32);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1435,56 +1436,52 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // with a client-IP header (~30 % in config 3) are queued in LDS and parsed kAggThreads at a
 // time, so the token parse, the longest code path, runs on full waves instead of on the
 // few lanes of each wave that have one.  Aggregation is order-free (counters, atomicMin of
-// the first-arrival word), so queueing does not change the result.  Services created in a
-// step reserve their list entries and arena bytes with one global atomic per block and step
-// (a single hot counter serialises at ~12 ns per atomic); requests are counted per block.
+// the first-arrival word), so queueing does not change the result.
+//
+// A service created here only claims its slot: the claim (slot, claiming event) goes to the
+// block's own stretch of the claim stage, counted in LDS, with no global atomic.  The
+// publication kernels then give every block's claims their list entries and arena bytes from
+// a scan of the per-block counts (k_pub_count, k_pub_scan) and copy the endpoint bytes
+// (k_publish).  A single global counter serialises at ~12 ns per atomic: reserving per block
+// and step cost ~5 ms per 100 M-event batch that creates 30 M services.
 constexpr uint32_t kCipQueue = 2 * kAggThreads;
-
-// A service this thread created in the current step, waiting for its reservations.
-struct PendingClaim {
-	uint32_t slot, pid, hl, ul, li;
-	unsigned long long ab;
-	const uint8_t *host, *url;
-};
 
 struct AggShared {
 	uint32_t q[kCipQueue]; // queued client-IP requests
 	uint32_t qn;
-	uint32_t cn;           // claims of this step (list entries)
-	unsigned long long cb; // their arena bytes
-	unsigned long long list_base, arena_base;
+	uint32_t cn;           // claims of this block
 	unsigned long long nreq;
 };
 
 __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
-		PendingClaim& pc, bool& has, unsigned long long net) {
+		unsigned long long net) {
 	bool claimed;
 	const Hash128 key = d.keys[i];
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
 			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (d.net_on && cls == CLS_EXTERNAL)
 		agg_nets(d, slot, net);
-	if (claimed) {
-		const uint8_t* p = d.payload + d.off[i];
-		pc.slot = slot;
-		pc.pid = d.ev[i].pid;
-		pc.host = p + r.u.span.host_off;
-		pc.hl = r.u.span.host_len;
-		pc.url = p + r.u.span.url_off;
-		pc.ul = r.u.span.url_len;
-		pc.li = atomicAdd(&sh.cn, 1u);
-		pc.ab = atomicAdd(&sh.cb, (unsigned long long)((pc.hl + pc.ul + 7u) & ~7u));
-		has = true;
+	if (claimed) { // at most one claim per event: the block's stretch holds them all
+		const uint32_t k = atomicAdd(&sh.cn, 1u);
+		const unsigned long long at = (unsigned long long)blockIdx.x * d.cstage_per + k;
+		d.cstage_slot[at] = slot;
+		d.cstage_ev[at] = i;
 	}
 }
 
-__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh, PendingClaim& pc, bool& has) {
+__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh) {
 	ebd_event_result r = d.res[i];
 	unsigned long long net = 0;
 	const uint32_t cls = cip_classify(d, i, r, row, &net);
 	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 	d.res[i] = r;
-	agg_request(d, i, r, cls, sh, pc, has, net);
+	agg_request(d, i, r, cls, sh, net);
+}
+
+// Steps (of kAggThreads events) per block; the claim stage holds per * kAggThreads per block.
+EBD_HD uint32_t agg_steps_per_block(uint32_t n, uint32_t grid) {
+	const uint32_t steps = (n + kAggThreads - 1) / kAggThreads;
+	return (steps + grid - 1) / grid;
 }
 
 __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
@@ -1495,16 +1492,13 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 		sh.nreq = 0;
 		sh.qn = 0;
 		sh.cn = 0;
-		sh.cb = 0;
 	}
 	__syncthreads();
 	uint32_t cnt = 0;
 	const uint32_t steps = (d.n + kAggThreads - 1) / kAggThreads;
-	const uint32_t per = (steps + gridDim.x - 1) / gridDim.x;
+	const uint32_t per = agg_steps_per_block(d.n, gridDim.x);
 	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
 	for (uint32_t st = s0; st < s1; st++) { // uniform trip count: the barriers below are safe
-		PendingClaim pc[3];
-		bool has[3] = {false, false, false};
 		const uint32_t i = st * kAggThreads + threadIdx.x;
 		if (i < d.n) {
 			ebd_event_result r = d.res[i];
@@ -1521,7 +1515,7 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 					const uint32_t cls = classify_source(*d.ifs, evb[32], src, &net);
 					r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 					d.res[i] = r;
-					agg_request(d, i, r, cls, sh, pc[0], has[0], net);
+					agg_request(d, i, r, cls, sh, net);
 				}
 			}
 		}
@@ -1531,43 +1525,159 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 		const bool last = st + 1 == s1;
 		if (m >= kAggThreads || (last && m > 0)) { // full waves; the block's last step drains the rest
 			if (threadIdx.x < min(m, (uint32_t)kAggThreads))
-				agg_cip_one(d, sh.q[threadIdx.x], row, sh, pc[1], has[1]);
+				agg_cip_one(d, sh.q[threadIdx.x], row, sh);
 			__syncthreads();
 			if (m >= kAggThreads && threadIdx.x < m - kAggThreads) // [kAggThreads, m) -> [0, m - kAggThreads)
 				sh.q[threadIdx.x] = sh.q[kAggThreads + threadIdx.x];
 			if (threadIdx.x == 0)
 				sh.qn = m >= kAggThreads ? m - kAggThreads : 0;
-		}
-		__syncthreads();
-		if (last && m > kAggThreads) { // the block's last step: what one drain left goes too
-			if (threadIdx.x < m - kAggThreads)
-				agg_cip_one(d, sh.q[threadIdx.x], row, sh, pc[2], has[2]);
-			if (threadIdx.x == 0)
-				sh.qn = 0;
 			__syncthreads();
 		}
-		// this step's claims: one reservation of list entries and arena bytes for the block
-		if (threadIdx.x == 0) {
-			const uint32_t cn = sh.cn;
-			if (cn) {
-				sh.list_base = atomicAdd(&d.ctr[CTR_SERVICES], (unsigned long long)cn);
-				sh.arena_base = atomicAdd(&d.ctr[CTR_SARENA], sh.cb);
-			}
-			sh.cn = 0;
-			sh.cb = 0;
+		if (last && m > kAggThreads) { // the block's last step: what one drain left goes too
+			if (threadIdx.x < m - kAggThreads)
+				agg_cip_one(d, sh.q[threadIdx.x], row, sh);
 		}
-		__syncthreads();
-#pragma unroll
-		for (int k = 0; k < 3; k++)
-			if (has[k])
-				claim_publish(d, pc[k].slot, sh.list_base + pc[k].li, sh.arena_base + pc[k].ab, pc[k].pid, pc[k].host, pc[k].hl,
-						pc[k].url, pc[k].ul);
-		__syncthreads(); // list_base / arena_base are read before the next step's reservation
 	}
 	atomicAdd(&sh.nreq, (unsigned long long)cnt);
 	__syncthreads();
-	if (threadIdx.x == 0 && sh.nreq)
-		atomicAdd(&d.ctr[CTR_REQUESTS], sh.nreq);
+	if (threadIdx.x == 0) {
+		d.blk_cnt[blockIdx.x] = sh.cn;
+		if (sh.nreq)
+			atomicAdd(&d.ctr[CTR_REQUESTS], sh.nreq);
+	}
+}
+
+// ---- publication of the services k_agg_fast created (one block per k_agg_fast block) ----
+constexpr int kPubThreads = 256, kPubClaims = kPubThreads / 4;
+
+__device__ __forceinline__ uint32_t claim_bytes(const Dev& d, uint32_t i) {
+	const ebd_event_result r = d.res[i];
+	return (r.u.span.host_len + r.u.span.url_len + 7u) & ~7u;
+}
+
+// Inclusive prefix of x over the block (kPubThreads); `part` is LDS scratch of 4 words.
+__device__ __forceinline__ uint32_t block_scan(uint32_t x, uint32_t* part, uint32_t* total) {
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= (uint32_t)o)
+			x += y;
+	}
+	if (lane == 63)
+		part[wave] = x;
+	__syncthreads();
+	uint32_t before = 0, t = 0;
+	for (uint32_t w = 0; w < kPubThreads / 64; w++) {
+		before += w < wave ? part[w] : 0u;
+		t += part[w];
+	}
+	__syncthreads(); // part may be rewritten by the next call
+	*total = t;
+	return before + x;
+}
+
+// Pass 1: the arena bytes of each block's claims.
+__global__ __launch_bounds__(kPubThreads) void k_pub_count(Dev d) {
+	__shared__ uint32_t part[kPubThreads / 64];
+	const uint32_t b = blockIdx.x, cn = d.blk_cnt[b];
+	const unsigned long long at0 = (unsigned long long)b * d.cstage_per;
+	unsigned long long sum = 0;
+	for (uint32_t j = threadIdx.x; j < cn; j += kPubThreads)
+		sum += claim_bytes(d, d.cstage_ev[at0 + j]);
+	uint32_t total;
+	block_scan((uint32_t)sum, part, &total);
+	if (threadIdx.x == 0)
+		d.blk_bytes[b] = total;
+}
+
+// Pass 2 (one block): each block's first list entry and arena offset; the list and arena grow.
+__global__ __launch_bounds__(1024) void k_pub_scan(Dev d, uint32_t nblk) {
+	__shared__ unsigned long long cs[1024], bs[1024];
+	const uint32_t t = threadIdx.x;
+	// nblk <= 2 * 1024: each thread sums two blocks, a Hillis-Steele scan over the pairs
+	const uint32_t b0 = 2 * t, b1 = 2 * t + 1;
+	const unsigned long long c0 = b0 < nblk ? d.blk_cnt[b0] : 0, c1 = b1 < nblk ? d.blk_cnt[b1] : 0;
+	const unsigned long long y0 = b0 < nblk ? d.blk_bytes[b0] : 0, y1 = b1 < nblk ? d.blk_bytes[b1] : 0;
+	cs[t] = c0 + c1;
+	bs[t] = y0 + y1;
+	__syncthreads();
+	for (uint32_t o = 1; o < 1024; o <<= 1) {
+		const unsigned long long a = t >= o ? cs[t - o] : 0, z = t >= o ? bs[t - o] : 0;
+		__syncthreads();
+		cs[t] += a;
+		bs[t] += z;
+		__syncthreads();
+	}
+	const unsigned long long lbase = d.ctr[CTR_SERVICES], abase = d.ctr[CTR_SARENA];
+	const unsigned long long ce = cs[t] - c0 - c1, be = bs[t] - y0 - y1; // exclusive prefix of the pair
+	if (b0 < nblk) {
+		d.blk_lbase[b0] = lbase + ce;
+		d.blk_abase[b0] = abase + be;
+	}
+	if (b1 < nblk) {
+		d.blk_lbase[b1] = lbase + ce + c0;
+		d.blk_abase[b1] = abase + be + y0;
+	}
+	__syncthreads();
+	if (t == 0) {
+		d.ctr[CTR_SERVICES] = lbase + cs[1023];
+		d.ctr[CTR_SARENA] = abase + bs[1023];
+	}
+}
+
+// Pass 3: list entries and endpoint bytes.  Four lanes per claim copy 8-byte pieces round
+// robin (a claim's loads go out together); offset, pid and length go beside the list entry.
+// The bytes are the claiming request's host + url: every request of the key has the same.
+__global__ __launch_bounds__(kPubThreads) void k_publish(Dev d) {
+	__shared__ uint32_t part[kPubThreads / 64];
+	const uint32_t b = blockIdx.x, cn = d.blk_cnt[b], r = threadIdx.x & 3;
+	const unsigned long long at0 = (unsigned long long)b * d.cstage_per;
+	const unsigned long long lbase = d.blk_lbase[b];
+	unsigned long long abase = d.blk_abase[b];
+	for (uint32_t j0 = 0; j0 < cn; j0 += kPubClaims) { // uniform
+		const uint32_t j = j0 + (threadIdx.x >> 2);
+		uint32_t i = kNone, slot = 0, hl = 0, ul = 0;
+		const uint8_t *host = d.payload, *url = d.payload;
+		if (j < cn) {
+			i = d.cstage_ev[at0 + j];
+			slot = d.cstage_slot[at0 + j];
+			const ebd_event_result res = d.res[i];
+			const uint8_t* p = d.payload + d.off[i];
+			host = p + res.u.span.host_off;
+			hl = res.u.span.host_len;
+			url = p + res.u.span.url_off;
+			ul = res.u.span.url_len;
+		}
+		const uint32_t n = hl + ul;
+		const uint32_t nb = (i != kNone && r == 0) ? ((n + 7u) & ~7u) : 0u; // counted once per claim
+		uint32_t total;
+		const uint32_t incl = block_scan(nb, part, &total);
+		const uint32_t excl = __shfl(incl - nb, (int)((threadIdx.x & 63) & ~3u), 64); // the quad leader's
+		if (i != kNone) {
+			const unsigned long long ep_at = abase + excl, li = lbase + j;
+			const bool fits = ep_at + n <= d.sarena_cap, listed = li < d.new_cap;
+			if (fits) {
+				unsigned long long* dst = (unsigned long long*)(d.sarena + ep_at);
+				for (uint32_t oo = 8 * r; oo < n; oo += 32) {
+					const unsigned long long A = gload8u(host + (oo < hl ? oo : 0));
+					const unsigned long long B = gload8u(url + ((oo > hl && oo - hl < ul) ? oo - hl : 0));
+					dst[oo >> 3] = endpoint_piece(hl, n, oo, A, B);
+				}
+			}
+			if (r == 0) {
+				if (!fits)
+					set_error(d, EBD_ERR_ARENA_FULL);
+				if (listed) {
+					d.new_slots[li] = slot;
+					d.list_ep[li] = fits ? ep_at : ~0ull;
+					d.list_pl[li] = (unsigned long long)d.ev[i].pid | ((unsigned long long)n << 32);
+				} else {
+					set_error(d, EBD_ERR_TABLE_FULL);
+				}
+			}
+		}
+		abase += total;
+	}
 }
 
 __global__ void k_verify(Dev d) {
@@ -1585,9 +1695,7 @@ __device__ __forceinline__ Slot empty_slot() {
 	s.tag = 0;
 	s.hi = 0;
 	s.first = ~0ull;
-	s.ep_off = 0;
-	s.pid = 0;
-	s.ep_len = 0;
+	s.pad0[0] = s.pad0[1] = 0;
 	s.internal_clients = 0;
 	s.external_clients = 0;
 	s.nets[0] = s.nets[1] = s.nets[2] = 0;
@@ -1627,23 +1735,23 @@ __global__ void k_slots_init(Slot* slots, uint32_t n) {
 // and scheme come from the first-arrival word (the earliest request's host length and
 // isHttps, Aggregator.cpp:112-130): the domain is "[...]" through the first ']' after the
 // host's first '[' (empty without one), else the host up to its first ':'.
-__global__ void k_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
-		ebd_service* out) {
-	const unsigned long long n = ctr[CTR_SERVICES];
+__global__ void k_collect(Dev d, ebd_service* out) {
+	const unsigned long long n = min(d.ctr[CTR_SERVICES], (unsigned long long)d.new_cap);
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		const Slot& s = slots[used[k]];
+		const Slot& s = d.slots[d.new_slots[k]];
+		const unsigned long long ep = d.list_ep[k], pl = d.list_pl[k];
 		const uint32_t hl = (uint32_t)(s.first & 0x7fffu);
 		uint32_t doff = 0, dlen = 0;
-		if (s.ep_off != ~0ull)
-			host_domain(arena + s.ep_off, hl, &doff, &dlen);
+		if (ep != ~0ull)
+			host_domain(d.sarena + ep, hl, &doff, &dlen);
 		ebd_service v;
-		v.pid = s.pid;
+		v.pid = (uint32_t)pl;
 		v.internal_clients = s.internal_clients;
 		v.external_clients = s.external_clients;
 		v.https = (uint8_t)((s.first >> 15) & 1u);
 		v.pad_[0] = v.pad_[1] = v.pad_[2] = 0;
-		v.endpoint_off = s.ep_off;
-		v.endpoint_len = s.ep_len;
+		v.endpoint_off = ep;
+		v.endpoint_len = (uint32_t)(pl >> 32);
 		v.domain_off = doff;
 		v.domain_len = dlen;
 		v.host_len = hl;
@@ -1690,22 +1798,23 @@ __global__ void k_keep_collect(Dev d, KeepRec* keep, unsigned long long* kbytes,
 		r.tag = s.tag;
 		r.hi = s.hi;
 		r.first = s.first;
-		r.pid = s.pid;
-		r.ep_len = s.ep_len;
+		const unsigned long long ep = d.list_ep[k], pl = d.list_pl[k];
+		r.pid = (uint32_t)pl;
+		r.ep_len = (uint32_t)(pl >> 32);
 		r.old_slot = si;
 		r.pad = r.pad2 = 0;
 		r.nets[0] = s.nets[0];
 		r.nets[1] = s.nets[1];
 		r.nets[2] = s.nets[2];
 		r.ep_off = ~0ull;
-		const unsigned long long nb = (s.ep_len + 7u) & ~7u;
+		const unsigned long long nb = (r.ep_len + 7u) & ~7u;
 		const unsigned long long at = atomicAdd(&d.ctr[CTR_KEEP_BYTES], nb);
-		if (s.ep_off != ~0ull && at + nb <= kcap) {
-			const unsigned long long* src = (const unsigned long long*)(d.sarena + s.ep_off);
+		if (ep != ~0ull && at + nb <= kcap) {
+			const unsigned long long* src = (const unsigned long long*)(d.sarena + ep);
 			for (unsigned long long w = 0; w < nb / 8; w++)
 				kbytes[at / 8 + w] = src[w];
 			r.ep_off = at;
-		} else if (s.ep_off != ~0ull) {
+		} else if (ep != ~0ull) {
 			set_error(d, EBD_ERR_ARENA_FULL);
 		}
 		keep[atomicAdd(&d.ctr[CTR_KEEP], 1ull)] = r;
@@ -1887,6 +1996,8 @@ static int grid_for(uint64_t items, int block, int cap) {
 		g = 1;
 	return (int)(g > (uint64_t)cap ? cap : g);
 }
+static uint32_t agg_grid(uint32_t n, int cus) { return (uint32_t)grid_for(n, kAggThreads, min(cus * 8, 2048)); } // k_pub_scan: <= 2048
+uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n, agg_grid(n, cus)) * kAggThreads; }
 
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
@@ -1929,7 +2040,14 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
 	return hipGetLastError();
 }
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_agg_fast, dim3(grid_for(d.n, kAggThreads, cus * 8)), dim3(kAggThreads), 0, st, d);
+	hipLaunchKernelGGL(k_agg_fast, dim3(agg_grid(d.n, cus)), dim3(kAggThreads), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_publish(const Dev& d, hipStream_t st, int cus) {
+	const uint32_t g = agg_grid(d.n, cus);
+	hipLaunchKernelGGL(k_pub_count, dim3(g), dim3(kPubThreads), 0, st, d);
+	hipLaunchKernelGGL(k_pub_scan, dim3(1), dim3(1024), 0, st, d, g);
+	hipLaunchKernelGGL(k_publish, dim3(g), dim3(kPubThreads), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus) {
@@ -1944,9 +2062,8 @@ hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st) {
 	hipLaunchKernelGGL(k_slots_init, dim3(grid_for(n, 256, 4096)), dim3(256), 0, st, slots, n);
 	return hipGetLastError();
 }
-hipError_t launch_collect(const Slot* slots, const unsigned int* used, const unsigned long long* ctr, const uint8_t* arena,
-		ebd_service* out, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, slots, used, ctr, arena, out);
+hipError_t launch_collect(const Dev& d, ebd_service* out, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, d, out);
 	return hipGetLastError();
 }
 hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus) {
