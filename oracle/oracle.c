@@ -1693,3 +1693,19 @@ uint64_t orc_parse_client_ip(const char* data, size_t len, char* buf, uint64_t c
 	req_free(&r);
 	return need;
 }
+
+/* Calibration helper: HttpRequestParser::parse only, a fresh parser per buffer
+ * (P:85-106), as the survey timed the compiled reference.  Returns the bytes consumed. */
+uint64_t orc_parse_only(const uint8_t* payload, const uint64_t* off, const uint32_t* len, uint32_t n) {
+	uint64_t total = 0;
+	orc_parser p;
+	parser_init(&p);
+	for (uint32_t i = 0; i < n; i++) {
+		if (len[i] == UINT32_MAX)
+			continue;
+		parser_reset(&p);
+		total += parser_parse(&p, payload + off[i], len[i], ORC_FLAG_UNENCRYPTED);
+	}
+	parser_destroy(&p);
+	return total;
+}

@@ -136,6 +136,8 @@ int orc_parser_state(const orc_parser* p);
 void orc_parser_reset(orc_parser* p);
 /* method \n url \n protocol \n host \n clientIPKey \n isHttps \n ip0 \x1f ip1 ... \n */
 uint64_t orc_parser_result(const orc_parser* p, char* buf, uint64_t cap);
+/* Calibration: parse() only over n buffers, a reset parser per buffer; returns bytes consumed */
+uint64_t orc_parse_only(const uint8_t* payload, const uint64_t* off, const uint32_t* len, uint32_t n);
 /* parseClientIPValue (HttpRequestParser.cpp:392-409) on a fresh parser: tokens joined by \x1f */
 uint64_t orc_parse_client_ip(const char* data, size_t len, char* buf, uint64_t cap, uint32_t* count);
 
