@@ -49,6 +49,12 @@ hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long
 		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
 		hipStream_t st, int cus);
 hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
+hipError_t launch_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt, hipStream_t st);
+hipError_t launch_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
+		const uint32_t* stt, unsigned long long* alen, hipStream_t st);
+hipError_t launch_gen4_write(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, const uint32_t* stt,
+		const unsigned long long* boff, EventRec* ev, uint32_t* len, unsigned long long* off, uint8_t* payload,
+		unsigned long long* gidx, hipStream_t st);
 hipError_t launch_net_clean(const Dev& d, unsigned long long now, unsigned long long retention, hipStream_t st, int cus);
 hipError_t launch_keep_collect(const Dev& d, KeepRec* keep, unsigned long long* kbytes, unsigned long long kcap, hipStream_t st,
 		int cus);
@@ -1219,7 +1225,77 @@ static const GenTables* host_tables() {
 
 static bool single_config(uint32_t cfg) { return cfg == 1 || cfg == 11 || cfg == 2 || cfg == 3 || cfg == 5; }
 static bool trace_ok(const ebd_trace_config* t) {
+	if (t && t->config == 4) // a whole trace from position 0, unsharded (its connections interleave)
+		return t->first == 0 && t->shard_count <= 1 && !(t->align & (t->align - 1));
 	return t && single_config(t->config) && !(t->align & (t->align - 1)) && (t->shard_count <= 1 || t->shard_index < t->shard_count);
+}
+
+// Config 4 (ebd_gen.h): connections per slot that cover ceil(n / kSlots4) rounds (>= 3 events each).
+static uint32_t gen4_J(uint64_t n) { return (uint32_t)(((n + kSlots4 - 1) / kSlots4) / 3 + 2); }
+
+// Config 4 on the host: the device passes in order (per-slot first rounds, piece lengths,
+// offsets, bytes).  ev == nullptr: sizes only.
+static int gen4_host(const ebd_trace_config* t, EventRec* ev, uint32_t* len, uint64_t* off, uint8_t* payload, uint64_t cap,
+		uint64_t* gidx, uint64_t* total_out) {
+	const GenTables* T = host_tables();
+	const uint64_t n = t->n;
+	const uint32_t a = t->align ? t->align : 1, J = gen4_J(n);
+	std::vector<uint32_t> r0((size_t)kSlots4 * J);
+	for (uint32_t slot = 0; slot < kSlots4; slot++) {
+		uint32_t acc = 0;
+		for (uint32_t j = 0; j < J; j++) {
+			Conn4 c;
+			conn4(t->seed, (uint64_t)j * kSlots4 + slot, c);
+			r0[(size_t)slot * J + j] = acc;
+			acc += conn4_events(c);
+		}
+	}
+	std::vector<uint64_t> boff(n + 1, 0);
+	for (uint32_t slot = 0; slot < kSlots4; slot++)
+		for (uint32_t j = 0; j < J; j++)
+			conn4_visit(*T, t->seed, slot, j, r0[(size_t)slot * J + j], n, [&](uint64_t p0, const Conn4&, const Req4* r, uint32_t) {
+				if (!r)
+					return;
+				for (uint32_t f = 0; f < r->k && p0 + (uint64_t)f * kSlots4 < n; f++)
+					boff[p0 + (uint64_t)f * kSlots4] = align_up(r->cut[f + 1] - r->cut[f], a);
+			});
+	uint64_t acc = 0;
+	for (uint64_t p = 0; p <= n; p++) {
+		const uint64_t x = boff[p];
+		boff[p] = acc;
+		acc += x;
+	}
+	*total_out = boff[n];
+	if (!ev)
+		return 0;
+	if (boff[n] > cap)
+		return -ENOSPC;
+	for (uint32_t slot = 0; slot < kSlots4; slot++)
+		for (uint32_t j = 0; j < J; j++)
+			conn4_visit(*T, t->seed, slot, j, r0[(size_t)slot * J + j], n, [&](uint64_t p0, const Conn4& c, const Req4* r, uint32_t e) {
+				if (!r) {
+					conn4_record(c, e, true, ev[p0]);
+					len[p0] = EBD_NO_BUFFER;
+					off[p0] = boff[p0];
+					if (gidx)
+						gidx[p0] = p0;
+					return;
+				}
+				uint8_t* dst[4] = {nullptr, nullptr, nullptr, nullptr};
+				for (uint32_t f = 0; f < r->k; f++) {
+					const uint64_t p = p0 + (uint64_t)f * kSlots4;
+					if (p >= n)
+						break;
+					dst[f] = payload + boff[p];
+					conn4_record(c, e + f, false, ev[p]);
+					len[p] = r->cut[f + 1] - r->cut[f];
+					off[p] = boff[p];
+					if (gidx)
+						gidx[p] = p;
+				}
+				write_req4(*r, dst);
+			});
+	return 0;
 }
 // config 5 is config 3's distribution, sharded by connection
 static uint32_t gen_config(uint32_t c) { return c == 5 ? 3 : c; }
@@ -1227,6 +1303,11 @@ static uint32_t gen_config(uint32_t c) { return c == 5 ? 3 : c; }
 int ebd_trace_size(const ebd_trace_config* t, uint32_t* n_events, uint64_t* payload_bytes) {
 	if (!trace_ok(t) || !payload_bytes)
 		return -EINVAL;
+	if (t->config == 4) {
+		if (n_events)
+			*n_events = t->n;
+		return gen4_host(t, nullptr, nullptr, nullptr, nullptr, 0, nullptr, payload_bytes);
+	}
 	const GenTables* T = host_tables();
 	const uint32_t a = t->align ? t->align : 1;
 	uint64_t total = 0;
@@ -1249,6 +1330,10 @@ int ebd_trace_generate_host(const ebd_trace_config* t, ebd_discovery_event* even
 		uint8_t* payload, uint64_t payload_cap, uint64_t* gidx) {
 	if (!trace_ok(t) || (t->n && (!events || !len || !off || !payload)))
 		return -EINVAL;
+	if (t->config == 4) {
+		uint64_t total = 0;
+		return gen4_host(t, (EventRec*)events, len, off, payload, payload_cap, gidx, &total);
+	}
 	const GenTables* T = host_tables();
 	const uint32_t a = t->align ? t->align : 1;
 	uint64_t at = 0;
@@ -1291,11 +1376,57 @@ struct GenOut {
 	uint64_t* gidx;
 };
 
+static int trace_device4(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out, uint32_t* n_events, uint64_t* bytes) {
+	const uint64_t n = t->n;
+	const uint32_t a = t->align ? t->align : 1, J = gen4_J(n);
+	const uint64_t tasks = (uint64_t)kSlots4 * J;
+	uint32_t *cnt = nullptr, *st = nullptr;
+	unsigned long long *alen = nullptr, *boff = nullptr;
+	HIP_TRY(hipMallocAsync((void**)&cnt, tasks * 4 + 4, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&st, tasks * 4 + 4, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&alen, n * 8 + 8, c->stream));
+	HIP_TRY(hipMallocAsync((void**)&boff, n * 8 + 8, c->stream));
+	HIP_TRY(launch_gen4_count(t->seed, J, cnt, c->stream));
+	size_t b1 = 0, b2 = 0;
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, cnt, st, (int)tasks, c->stream)); // wraps mod 2^32: differences stay exact
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, alen, boff, (int)(n + 1), c->stream));
+	void* tmp = nullptr;
+	HIP_TRY(hipMallocAsync(&tmp, (b1 > b2 ? b1 : b2) + 16, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, cnt, st, (int)tasks, c->stream));
+	HIP_TRY(hipMemsetAsync(alen, 0, n * 8 + 8, c->stream));
+	HIP_TRY(launch_gen4_len(c->d_gen, t->seed, J, n, a, st, alen, c->stream));
+	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, alen, boff, (int)(n + 1), c->stream));
+	unsigned long long total = 0;
+	HIP_TRY(hipMemcpyAsync(&total, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	int rc = 0;
+	if (out) {
+		if (total > out->cap)
+			rc = -ENOSPC;
+		else
+			HIP_TRY(launch_gen4_write(c->d_gen, t->seed, J, n, st, boff, out->ev, out->len, (unsigned long long*)out->off,
+					out->payload, (unsigned long long*)out->gidx, c->stream));
+	}
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipFreeAsync(cnt, c->stream));
+	HIP_TRY(hipFreeAsync(st, c->stream));
+	HIP_TRY(hipFreeAsync(alen, c->stream));
+	HIP_TRY(hipFreeAsync(boff, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	if (n_events)
+		*n_events = (uint32_t)n;
+	if (bytes)
+		*bytes = total;
+	return rc;
+}
+
 static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out, uint32_t* n_events, uint64_t* bytes) {
 	HIP_TRY(hipSetDevice(c->device));
 	int rc = ensure_gen_tables(c);
 	if (rc)
 		return rc;
+	if (t->config == 4)
+		return trace_device4(c, t, out, n_events, bytes);
 	const uint32_t n = t->n, a = t->align ? t->align : 1, cfg = gen_config(t->config);
 	unsigned long long *alen = nullptr, *boff = nullptr;
 	uint32_t *keep = nullptr, *pos = nullptr;

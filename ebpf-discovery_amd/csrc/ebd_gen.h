@@ -106,7 +106,8 @@ EBD_HD void gen_draws(uint64_t seed, uint32_t config, uint64_t idx, uint32_t str
 }
 
 // fixed 64-byte GET, one endpoint.
-EBD_HD void compose_fixed64(Sink& s) { s.str("GET /index.html HTTP/1.1\r\nHost: 10.0.0.1:8080\r\nAccept: */*xx\r\n\r\n"); }
+template <typename Out>
+EBD_HD void compose_fixed64(Out& s) { s.str("GET /index.html HTTP/1.1\r\nHost: 10.0.0.1:8080\r\nAccept: */*xx\r\n\r\n"); }
 
 EBD_HD const char* path_segment(uint32_t k) {
 	switch (k & 15) {
@@ -129,7 +130,8 @@ EBD_HD const char* path_segment(uint32_t k) {
 	}
 }
 
-EBD_HD void put_path(Sink& s, uint32_t k) {
+template <typename Out>
+EBD_HD void put_path(Out& s, uint32_t k) {
 	s.put('/');
 	s.str(path_segment(k));
 	s.put('/');
@@ -142,7 +144,8 @@ EBD_HD void put_path(Sink& s, uint32_t k) {
 	}
 }
 
-EBD_HD void put_host(Sink& s, uint32_t j) {
+template <typename Out>
+EBD_HD void put_host(Out& s, uint32_t j) {
 	switch (j & 3) {
 	case 0:
 		s.str("svc");
@@ -170,7 +173,8 @@ EBD_HD void put_host(Sink& s, uint32_t j) {
 	}
 }
 
-EBD_HD void put_v4(Sink& s, uint32_t r) {
+template <typename Out>
+EBD_HD void put_v4(Out& s, uint32_t r) {
 	// first octet from a mix of internal (10, 172.16, 192.168, 127) and external ranges
 	// {10, 172, 192, 127, 8, 34, 52, 81, 93, 104, 151, 185, 203, 66, 23, 100} packed by byte
 	const uint64_t lo = 0x51342208'7fc0ac0aull, hi = 0x641742cb'b997685dull;
@@ -190,7 +194,8 @@ EBD_HD void put_v4(Sink& s, uint32_t r) {
 	s.dec((r >> 20) & 255);
 }
 
-EBD_HD void put_v6(Sink& s, uint32_t r) {
+template <typename Out>
+EBD_HD void put_v6(Out& s, uint32_t r) {
 	switch (r & 3) {
 	case 0: s.str("2001:db8:"); break;
 	case 1: s.str("fd00:"); break;
@@ -204,7 +209,8 @@ EBD_HD void put_v6(Sink& s, uint32_t r) {
 }
 
 // Client-IP header value forms (HttpRequestParserTest.cpp:75-150 shapes).
-EBD_HD void put_cip_value(Sink& s, uint32_t r0, uint32_t r1) {
+template <typename Out>
+EBD_HD void put_cip_value(Out& s, uint32_t r0, uint32_t r1) {
 	switch (r0 % 7) {
 	case 0: put_v4(s, r1); break;
 	case 1:
@@ -269,7 +275,8 @@ EBD_HD void mixed_params(const GenTables& T, const GenDraws& d, MixedReq& q) {
 
 // SURVEY 8(d) config 3 request: request line, Host, optional client-IP header,
 // User-Agent padding to the sampled length, Accept, end of headers, POST body.
-EBD_HD void compose_mixed(Sink& s, const MixedReq& q) {
+template <typename Out>
+EBD_HD void compose_mixed(Out& s, const MixedReq& q) {
 	const uint32_t start = s.n;
 	s.str(q.post ? "POST " : "GET ");
 	put_path(s, q.path);
@@ -386,6 +393,198 @@ EBD_HD uint32_t gen_single(const GenTables* T, uint32_t config, uint64_t seed, u
 }
 
 EBD_HD uint64_t align_up(uint64_t x, uint32_t a) { return (x + a - 1) & ~(uint64_t)(a - 1); }
+
+// ---------------------------------------------------------------------------------
+// config-3 requests (seed 4) cut into 2-4 consecutive recv() events
+// (the first >= 16 bytes, so it still starts "GET /" or "POST /", DataFunctions.h:45-50; a
+// POST body stays in the last piece), 1-8 keep-alive requests per connection, then a
+// DATA_END event.  kSlots4 connections are open at a time and interleaved round robin:
+// event position p = round * kSlots4 + slot, each slot running its connections j = 0, 1, ...
+// back to back.  So at most kSlots4 (<= 8192) sessions are ever live and the LRU never
+// evicts.  Connection j of a slot is cid = j * kSlots4 + slot (independent of the trace
+// length, so a longer trace extends a shorter one).
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kSlots4 = 4096, kMaxReq4 = 8;
+
+struct Conn4 {
+	uint32_t nreq, flags, pid, fd, sid;
+	uint32_t kfrag[kMaxReq4];
+	uint8_t src[16];
+};
+
+EBD_HD void conn4(uint64_t seed, uint64_t cid, Conn4& c) {
+	GenDraws d;
+	gen_draws(seed, 4, cid, 8, d); // stream 8: connection draws (streams 0.. are per request)
+	c.nreq = 1 + d.u[0] % kMaxReq4;
+	const bool v6 = (d.u[1] % 100) < 20, ssl = ((d.u[1] >> 8) % 100) < 15;
+	c.flags = (v6 ? FLAG6 : FLAG4) | (ssl ? FLAG_SSL : FLAG_PLAIN);
+	c.pid = 2000 + d.u[2] % kPids;
+	c.fd = 5 + (uint32_t)(cid % 1000);
+	c.sid = (uint32_t)(cid + 1);
+	for (int k = 0; k < 16; k++)
+		c.src[k] = 0;
+	if (!v6) {
+		for (int k = 0; k < 4; k++)
+			c.src[k] = (uint8_t)(d.u[3] >> (8 * k));
+	} else {
+		for (int k = 0; k < 16; k++)
+			c.src[k] = (uint8_t)(d.u[3 + (k >> 2)] >> (8 * (k & 3)));
+		if (d.u[15] & 1) { // half external 2001:db8::/32, half internal fd00::/8
+			c.src[0] = 0x20;
+			c.src[1] = 0x01;
+			c.src[2] = 0x0d;
+			c.src[3] = 0xb8;
+		} else {
+			c.src[0] = 0xfd;
+		}
+	}
+	for (uint32_t q = 0; q < kMaxReq4; q++)
+		c.kfrag[q] = 2 + d.u[7 + q] % 3;
+}
+
+EBD_HD uint32_t conn4_events(const Conn4& c) {
+	uint32_t e = 1; // DATA_END
+	for (uint32_t q = 0; q < c.nreq; q++)
+		e += c.kfrag[q];
+	return e;
+}
+
+// Request q of connection cid: its config-3 content, its length and its cut points
+// cut[0] = 0 < cut[1] < ... < cut[k] = length.
+struct Req4 {
+	MixedReq m;
+	uint32_t len, hdr, k;
+	uint32_t cut[5];
+};
+
+EBD_HD void req4(const GenTables& T, uint64_t seed, uint64_t cid, uint32_t q, uint32_t kfrag, Req4& r) {
+	GenDraws d;
+	gen_draws(seed, 4, cid * kMaxReq4 + q, 0, d);
+	mixed_params(T, d, r.m);
+	Sink s{nullptr, 0};
+	compose_mixed(s, r.m);
+	r.len = s.n;
+	r.hdr = s.n - r.m.body; // header section: the cuts stay in it
+	const uint32_t span = r.hdr > 16 ? r.hdr - 16 : 0;
+	r.k = kfrag; // span >= 50 > 4: every request carries its request line, Host, User-Agent and Accept
+	r.cut[0] = 0;
+	for (uint32_t f = 1; f < r.k; f++) { // one cut per k-th of [16, hdr), jittered inside it
+		const uint32_t seg = span / r.k;
+		r.cut[f] = 16 + (span * f) / r.k - (seg ? d.u[15 - f] % seg : 0) / 2;
+	}
+	r.cut[r.k] = r.len;
+}
+
+// Writes the request's bytes into its pieces: byte b of the request goes to piece f with
+// cut[f] <= b < cut[f + 1], at dst[f] + (b - cut[f]).
+struct SplitSink {
+	uint8_t* dst[4];
+	uint32_t cut[5];
+	uint32_t k, n;
+	EBD_HD void put(uint32_t c) {
+		uint32_t f = 0;
+		while (f + 1 < k && n >= cut[f + 1])
+			f++;
+		if (dst[f]) // a piece past the trace's end is not written
+			dst[f][n - cut[f]] = (uint8_t)c;
+		n++;
+	}
+	EBD_HD void str(const char* s) {
+		while (*s)
+			put((uint8_t)*s++);
+	}
+	EBD_HD void dec(uint32_t v) {
+		char b[10];
+		int m = 0;
+		do {
+			b[m++] = (char)('0' + v % 10);
+			v /= 10;
+		} while (v);
+		while (m)
+			put((uint8_t)b[--m]);
+	}
+	EBD_HD void hex(uint32_t v) {
+		char b[8];
+		int m = 0;
+		do {
+			b[m++] = "0123456789abcdef"[v & 15];
+			v >>= 4;
+		} while (v);
+		while (m)
+			put((uint8_t)b[--m]);
+	}
+};
+
+// The request's pieces into their buffers (dst[f], length cut[f + 1] - cut[f]); ~1 % of
+// requests carry an invalid byte in the header section, as in config 3.
+EBD_HD void write_req4(const Req4& r, uint8_t* const* dst) {
+	SplitSink s;
+	for (uint32_t f = 0; f < 4; f++)
+		s.dst[f] = f < r.k ? dst[f] : nullptr;
+	for (uint32_t f = 0; f <= r.k; f++)
+		s.cut[f] = r.cut[f];
+	s.k = r.k;
+	s.n = 0;
+	compose_mixed(s, r.m);
+	if (r.m.inval) {
+		const uint32_t b = r.m.invpos % r.hdr;
+		uint32_t f = 0;
+		while (f + 1 < r.k && b >= r.cut[f + 1])
+			f++;
+		if (dst[f])
+			dst[f][b - r.cut[f]] = 0x01;
+	}
+}
+
+// Event e (0-based) of connection cid: request q and piece f of it, or the DATA_END event
+// (q = nreq).  bufferSeq counts the connection's data events from 1 (Handlers.h:121-125).
+EBD_HD void conn4_event(const Conn4& c, uint32_t e, uint32_t* q, uint32_t* f) {
+	uint32_t at = 0;
+	for (uint32_t k = 0; k < c.nreq; k++) {
+		if (e < at + c.kfrag[k]) {
+			*q = k;
+			*f = e - at;
+			return;
+		}
+		at += c.kfrag[k];
+	}
+	*q = c.nreq;
+	*f = 0;
+}
+
+// Visits the events of connection task t = slot * J + j (slot-major, so that a scan of the
+// per-task event counts gives each connection's first round): fn(position, conn, request
+// (nullptr for DATA_END), piece, event number).  r0: the connection's first round.
+template <typename Fn>
+EBD_HD void conn4_visit(const GenTables& T, uint64_t seed, uint32_t slot, uint32_t j, uint64_t r0, uint64_t n, Fn fn) {
+	Conn4 c;
+	const uint64_t cid = (uint64_t)j * kSlots4 + slot;
+	conn4(seed, cid, c);
+	uint64_t e = 0;
+	for (uint32_t q = 0; q < c.nreq; q++) {
+		const uint64_t p0 = (r0 + e) * kSlots4 + slot;
+		if (p0 >= n)
+			return;
+		Req4 r;
+		req4(T, seed, cid, q, c.kfrag[q], r);
+		fn(p0, c, &r, (uint32_t)e);
+		e += r.k;
+	}
+	const uint64_t pe = (r0 + e) * kSlots4 + slot;
+	if (pe < n)
+		fn(pe, c, (const Req4*)nullptr, (uint32_t)e);
+}
+
+EBD_HD void conn4_record(const Conn4& c, uint32_t e, bool end, EventRec& ev) {
+	ev.pid = c.pid;
+	ev.fd = c.fd;
+	ev.sessionID = c.sid;
+	ev.bufferSeq = end ? e : e + 1;
+	for (int k = 0; k < 16; k++)
+		ev.sourceIP[k] = end ? 0 : c.src[k];
+	ev.flags = (uint8_t)(end ? FLAG_END : (c.flags | FLAG_NEW));
+	ev.pad[0] = ev.pad[1] = ev.pad[2] = 0;
+}
 
 // Shard of a connection (pid, fd, sessionID) among `count` GPUs: every
 // event of a connection lands on one GPU, so parser sessions never cross GPUs.  Same

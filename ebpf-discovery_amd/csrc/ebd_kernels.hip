@@ -1987,6 +1987,67 @@ __global__ void k_gen_write(const GenTables* T, uint32_t config, unsigned long l
 	}
 }
 
+// Config 4 (ebd_gen.h conn4_*): one thread per connection task t = slot * J + j.
+__global__ void k_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt) {
+	const uint64_t tasks = (uint64_t)kSlots4 * J;
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < tasks; t += (uint64_t)gridDim.x * blockDim.x) {
+		Conn4 c;
+		conn4(seed, (t % J) * kSlots4 + t / J, c);
+		cnt[t] = conn4_events(c);
+	}
+}
+
+// Aligned piece length at every position < n (DATA_END: 0); st = exclusive scan of cnt.
+__global__ void k_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
+		const uint32_t* st, unsigned long long* alen) {
+	const uint64_t tasks = (uint64_t)kSlots4 * J;
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < tasks; t += (uint64_t)gridDim.x * blockDim.x) {
+		const uint32_t slot = (uint32_t)(t / J), j = (uint32_t)(t % J);
+		const uint64_t r0 = st[t] - st[(uint64_t)slot * J];
+		conn4_visit(*T, seed, slot, j, r0, n, [&](uint64_t p0, const Conn4&, const Req4* r, uint32_t) {
+			if (!r) {
+				alen[p0] = 0;
+				return;
+			}
+			for (uint32_t f = 0; f < r->k && p0 + (uint64_t)f * kSlots4 < n; f++)
+				alen[p0 + (uint64_t)f * kSlots4] = align_up(r->cut[f + 1] - r->cut[f], align);
+		});
+	}
+}
+
+__global__ void k_gen4_write(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, const uint32_t* st,
+		const unsigned long long* boff, EventRec* ev, uint32_t* len, unsigned long long* off, uint8_t* payload,
+		unsigned long long* gidx) {
+	const uint64_t tasks = (uint64_t)kSlots4 * J;
+	for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < tasks; t += (uint64_t)gridDim.x * blockDim.x) {
+		const uint32_t slot = (uint32_t)(t / J), j = (uint32_t)(t % J);
+		const uint64_t r0 = st[t] - st[(uint64_t)slot * J];
+		conn4_visit(*T, seed, slot, j, r0, n, [&](uint64_t p0, const Conn4& c, const Req4* r, uint32_t e) {
+			if (!r) {
+				conn4_record(c, e, true, ev[p0]);
+				len[p0] = EBD_NO_BUFFER;
+				off[p0] = boff[p0];
+				if (gidx)
+					gidx[p0] = p0;
+				return;
+			}
+			uint8_t* dst[4] = {nullptr, nullptr, nullptr, nullptr};
+			for (uint32_t f = 0; f < r->k; f++) {
+				const uint64_t p = p0 + (uint64_t)f * kSlots4;
+				if (p >= n)
+					break;
+				dst[f] = payload + boff[p];
+				conn4_record(c, e + f, false, ev[p]);
+				len[p] = r->cut[f + 1] - r->cut[f];
+				off[p] = boff[p];
+				if (gidx)
+					gidx[p] = p;
+			}
+			write_req4(*r, dst);
+		});
+	}
+}
+
 // ---------------------------------------------------------------------------------
 // launch wrappers (called from ebd_api.cpp)
 // ---------------------------------------------------------------------------------
@@ -2103,6 +2164,23 @@ hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, 
 }
 hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_net_dump, dim3(grid_for((uint64_t)d.net_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, out, cap, count);
+	return hipGetLastError();
+}
+
+hipError_t launch_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt, hipStream_t st) {
+	hipLaunchKernelGGL(k_gen4_count, dim3(grid_for((uint64_t)kSlots4 * J, 256, 8192)), dim3(256), 0, st, seed, J, cnt);
+	return hipGetLastError();
+}
+hipError_t launch_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
+		const uint32_t* stt, unsigned long long* alen, hipStream_t st) {
+	hipLaunchKernelGGL(k_gen4_len, dim3(grid_for((uint64_t)kSlots4 * J, 256, 8192)), dim3(256), 0, st, T, seed, J, n, align, stt, alen);
+	return hipGetLastError();
+}
+hipError_t launch_gen4_write(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, const uint32_t* stt,
+		const unsigned long long* boff, EventRec* ev, uint32_t* len, unsigned long long* off, uint8_t* payload,
+		unsigned long long* gidx, hipStream_t st) {
+	hipLaunchKernelGGL(k_gen4_write, dim3(grid_for((uint64_t)kSlots4 * J, 256, 8192)), dim3(256), 0, st, T, seed, J, n, stt, boff, ev,
+			len, off, payload, gidx);
 	return hipGetLastError();
 }
 

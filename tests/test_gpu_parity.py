@@ -453,3 +453,59 @@ def test_full_scale_config3_properties():
     ctx.sync()
     res2 = ctx.results()
     assert np.array_equal(res2.view(np.uint8), res.view(np.uint8))
+
+
+def _device_trace(ctx, cfg, seed, n, dev, align=1):
+    import torch
+    k, size = ebd.trace_size_device(ctx, cfg, seed, 0, n, align=align, with_events=True)
+    ev = torch.empty(k * 36, dtype=torch.uint8, device=dev)
+    ln = torch.empty(k, dtype=torch.int32, device=dev)
+    of = torch.empty(k, dtype=torch.int64, device=dev)
+    pay = torch.empty(size + 64, dtype=torch.uint8, device=dev)
+    ebd.generate_device(ctx, cfg, seed, 0, n, ev, ln, of, pay, pay.numel(), align=align)
+    torch.cuda.synchronize()
+    return k, size, ev, ln, of, pay
+
+
+def test_config4_device_generator_matches_host():
+    import torch
+    dev = torch.device("cuda:0")
+    ctx = ebd.Context(max_events=16)
+    n = 300_000
+    k, size, ev, ln, of, pay = _device_trace(ctx, 4, 4, n, dev)
+    hev, hl, ho, hp = ebd.generate_host(4, 4, 0, n)
+    assert k == len(hev) and size + 16 == hp.size
+    assert np.array_equal(ev.cpu().numpy(), hev.view(np.uint8).reshape(-1))
+    assert np.array_equal(ln.cpu().numpy().view(np.uint32), hl)
+    assert np.array_equal(of.cpu().numpy().view(np.uint64), ho)
+    assert np.array_equal(pay[:size].cpu().numpy(), hp[:size])
+
+
+@pytest.mark.parametrize("batches", [1, 4])
+def test_config4_fragmented_keepalive_parity_1m(batches):
+    """Config 4 at 1.2 M events (device-generated): every request arrives in 2-4 pieces, so
+    nearly every event takes the session path, with sessions carried across batches."""
+    import torch
+    dev = torch.device("cuda:0")
+    n = 1_200_000
+    ctx = ebd.Context(max_events=n)
+    k, size, ev, ln, of, pay = _device_trace(ctx, 4, 4, n, dev)
+    hev = ev.cpu().numpy().view(ebd.EVENT_DTYPE)
+    hl = ln.cpu().numpy().view(np.uint32)
+    ho = of.cpu().numpy().view(np.uint64)
+    hp = pay.cpu().numpy()
+    views = []
+    bounds = np.linspace(0, k, batches + 1).astype(int)
+    for a, z in zip(bounds[:-1], bounds[1:]):
+        ctx.submit_device(ev[a * 36:], ln[a:], of[a:], pay, int(z - a))
+        ctx.sync()
+        sreq, sstr = ctx.session_requests()
+        views += T.gpu_view(ctx.results(), ho[a:z], hp, sreq, sstr)
+    st = ctx.stats()
+    assert st["errors"] == 0, st
+    ov, os_, ost = run_oracle(hev, hl, ho, hp)
+    bad = [i for i in range(k) if views[i] != ov[i]]
+    assert not bad, [(i, views[i], ov[i]) for i in bad[:5]]
+    assert ctx.services() == os_
+    assert st["kernel_deletes"] == ost["kernel_deletes"] and st["live_sessions"] == ost["lru_size"]
+    assert st["lru_evictions"] == 0 and st["session_events"] > 0.9 * k
