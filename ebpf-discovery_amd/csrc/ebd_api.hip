@@ -621,6 +621,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 					end_bit, c->stream);
 		}));
 		d.slow_keys = c->d_slow[1];
+		d.heads = (uint32_t*)c->d_slow[0]; // the sort's input, free after it
 		// LRU eviction possible?  Only if more sessions than its capacity could be live at once
 		// (k_walk_lru's comment): first the cheap count of candidate sessions, then the bound.
 		bool exact = false;

@@ -74,8 +74,9 @@ enum Ctr : uint32_t {
 	CTR_VERIFY,         // deferred service-key verifications
 	CTR_LRU_PEAK,       // 2^31 + max over the batch of (live sessions - carried), upper bound (k_lru_peak)
 	CTR_EVICTIONS,      // LRU evictions in this batch (exact path)
-	CTR_BATCH_END = 11,
-	CTR_SARENA = 11,    // service string arena bytes used
+	CTR_HEADS,          // sessions with events in this batch (k_walk_heads)
+	CTR_BATCH_END = 12,
+	CTR_SARENA = 12,    // service string arena bytes used
 	CTR_ERRORS,         // EBD_ERR_* bitmask
 	CTR_COLLISIONS,
 	CTR_KDELETES,
@@ -87,7 +88,7 @@ enum Ctr : uint32_t {
 	CTR_KEEP_BYTES,     // their endpoint bytes
 	CTR_NETS,           // network-map entries claimed (the table's fill)
 	CTR_V6D,            // v6 prefix-dictionary slots claimed
-	CTR_COUNT = 23,
+	CTR_COUNT = 24,
 };
 
 // Network-counter maps of all services (Service.h:45-58): one open-addressing table of
@@ -158,6 +159,7 @@ struct Dev {
 	uint32_t sset_mask;
 	uint32_t* dirty;
 	unsigned long long* slow_keys;
+	uint32_t* heads; // sorted position of each session's first event (k_walk_heads)
 	Carry* carry_in;
 	uint32_t n_carry_in;
 	Carry* carry_out;

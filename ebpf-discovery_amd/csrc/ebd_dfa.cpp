@@ -33,6 +33,8 @@ void build_key_trie(KeyTrie* t) {
 		}
 	}
 	t->nodes = (uint8_t)name.size();
+	for (int c = 0; c < 256; c++)
+		t->cls[c] = byte_class((uint32_t)c);
 	for (int n = 0; n < (int)name.size(); n++) {
 		t->type[n] = KT_OTHER;
 		for (int k = 0; k < 6; k++)

@@ -921,6 +921,8 @@ __global__ void k_slow_collect(Dev d) {
 // carried bytes (if the request started in an earlier batch) followed by the buffers
 // of this batch's events from position j0 on.
 // ---------------------------------------------------------------------------------
+constexpr int kWalkThreads = 256;
+
 struct Walk {
 	const uint8_t* cb; // carried bytes of the request in progress
 	uint32_t clen;
@@ -935,6 +937,27 @@ __device__ __forceinline__ uint32_t piece_len(const Dev& d, uint32_t j) {
 	return ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) ? L : 0;
 }
 
+// Sequential byte reads through a 16-B register window: one aligned dwordx4 load per 16
+// bytes instead of one byte load each.  The aligned block holding a valid byte never
+// leaves that byte's page, so the over-read cannot fault.
+struct ByteWin {
+	const uint8_t* base;
+	uintptr_t blk;
+	uint32_t w0, w1, w2, w3;
+	__device__ explicit ByteWin(const uint8_t* b) : base(b), blk(~(uintptr_t)0), w0(0), w1(0), w2(0), w3(0) {}
+	__device__ __forceinline__ uint32_t operator()(uint32_t k) {
+		const uintptr_t a = (uintptr_t)(base + k), b = a & ~(uintptr_t)15;
+		if (b != blk) {
+			const uint4 v = *(const uint4*)b;
+			w0 = v.x, w1 = v.y, w2 = v.z, w3 = v.w;
+			blk = b;
+		}
+		const uint32_t q = (uint32_t)(a >> 2) & 3u;
+		const uint32_t x = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+		return (x >> ((uint32_t)(a & 3u) * 8u)) & 0xffu;
+	}
+};
+
 // Visits stream bytes [a, a + n) in order; the stream ends at sorted position jend whose
 // piece is truncated to cend bytes.  fn(byte) returns false to stop.  Returns bytes visited.
 template <typename Fn>
@@ -942,8 +965,9 @@ __device__ uint32_t stream_visit(const Dev& d, const Walk& w, uint32_t jend, uin
 	uint32_t pos = 0, done = 0;
 	const uint32_t b = a + n;
 	if (w.clen) {
+		ByteWin cb(w.cb);
 		for (uint32_t k = a; k < b && k < w.clen; k++) {
-			if (!fn(w.cb[k]))
+			if (!fn((uint8_t)cb(k)))
 				return done;
 			done++;
 		}
@@ -957,9 +981,9 @@ __device__ uint32_t stream_visit(const Dev& d, const Walk& w, uint32_t jend, uin
 			continue;
 		const uint32_t lo = a > pos ? a : pos, hi = b < pos + pl ? b : pos + pl;
 		if (lo < hi) {
-			const uint8_t* src = d.payload + d.off[slow_event(d, j)] + (lo - pos);
+			ByteWin src(d.payload + d.off[slow_event(d, j)] + (lo - pos));
 			for (uint32_t k = 0; k < hi - lo; k++) {
-				if (!fn(src[k]))
+				if (!fn((uint8_t)src(k)))
 					return done;
 				done++;
 			}
@@ -1057,12 +1081,11 @@ enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
 // Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
 // session's state in S.  Returns the LRU operation it implies; an insert (saveSession,
 // Discovery.cpp:148-150) is left to the caller, which may have to evict first.
-__device__ uint32_t session_event(const Dev& d, SessState& S, uint32_t jj) {
+__device__ uint32_t session_event(const Dev& d, const KeyTrie* trie, SessState& S, uint32_t jj) {
 	const uint32_t i = slow_event(d, jj);
 	const EventRec& ev = d.ev[i];
 	const uint8_t flags = ev.flags;
 	const uint32_t L = d.len[i];
-	const KeyTrie* trie = d.trie;
 	ebd_event_result r;
 	r.consumed = 0;
 	r.status = EBD_STATUS_NONE;
@@ -1072,8 +1095,7 @@ __device__ uint32_t session_event(const Dev& d, SessState& S, uint32_t jj) {
 	atomicAdd(&d.ctr[CTR_SESSION_EVENTS], 1ull);
 	uint32_t op = OP_NONE;
 	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
-		const uint8_t* buf = d.payload + d.off[i];
-		auto at = [buf](uint32_t k) { return (uint32_t)buf[k]; };
+		ByteWin at(d.payload + d.off[i]);
 		if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
 			S.stamp = d.seq_base + i;
 			r.info |= EBD_INFO_EXISTING;
@@ -1163,18 +1185,24 @@ __device__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, 
 	});
 }
 
-// The parallel session path: one lane per session, events in order.  Exact while no LRU
-// eviction can happen (run_batch checks an upper bound of the live sessions first).
-__global__ void k_walk(Dev d, uint32_t nslow) {
-	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
+// The parallel session path: one lane per session (k_walk_heads lists them), events in
+// order.  Exact while no LRU eviction can happen (run_batch checks an upper bound of the
+// live sessions first).  The header-key trie and the byte classes sit in LDS: the walk
+// reads them once per byte.
+__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
+	__shared__ KeyTrie trie;
+	for (uint32_t k = threadIdx.x; k < (uint32_t)sizeof(KeyTrie); k += kWalkThreads)
+		((uint8_t*)&trie)[k] = ((const uint8_t*)d.trie)[k];
+	__syncthreads();
+	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
+	for (uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x; h < nh; h += gridDim.x * kWalkThreads) {
+		const uint32_t j = d.heads[h];
 		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
-		if (j > 0 && (uint32_t)(d.slow_keys[j - 1] >> 32) == slot)
-			continue;
 		SessState S;
 		session_begin(d, S, j, slot);
 		uint32_t jj = j;
 		for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
-			const uint32_t op = session_event(d, S, jj);
+			const uint32_t op = session_event(d, &trie, S, jj);
 			if (op == OP_INSERT) {
 				S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
 				S.stamp = d.seq_base + slow_event(d, jj);
@@ -1288,7 +1316,10 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 	__shared__ uint32_t nord, nlive, k_next, evict_for;
 	__shared__ unsigned long long rs[kLruThreads];
 	__shared__ uint32_t ri[kLruThreads];
+	__shared__ KeyTrie trie;
 	const uint32_t t = threadIdx.x;
+	for (uint32_t k = t; k < (uint32_t)sizeof(KeyTrie); k += kLruThreads)
+		((uint8_t*)&trie)[k] = ((const uint8_t*)d.trie)[k];
 	if (t == 0)
 		nlive = 0;
 	__syncthreads();
@@ -1343,7 +1374,7 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 				uint32_t e = kNone;
 				for (; k < nord; k++) {
 					const uint32_t jj = ord[k], h = head[jj];
-					const uint32_t op = session_event(d, S[h], jj);
+					const uint32_t op = session_event(d, &trie, S[h], jj);
 					if (op == OP_ERASE && S[h].li != kNone) {
 						live_remove(S, live, nlive, h);
 					} else if (op == OP_INSERT) {
@@ -1574,6 +1605,42 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t x, uint32_t* part, uint3
 	__syncthreads(); // part may be rewritten by the next call
 	*total = t;
 	return before + x;
+}
+
+// The batch's sessions for k_walk: the sorted position of each one's first event.  A block
+// takes tiles of kPubThreads * kHeadsPer positions, kHeadsPer consecutive ones per thread,
+// and reserves its tile's heads with one atomic.
+constexpr uint32_t kHeadsPer = 16;
+__global__ __launch_bounds__(kPubThreads) void k_walk_heads(Dev d, uint32_t nslow) {
+	__shared__ uint32_t part[kPubThreads / 64];
+	__shared__ unsigned long long base;
+	const uint64_t tile = (uint64_t)kPubThreads * kHeadsPer;
+	for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < nslow; t0 += (uint64_t)gridDim.x * tile) {
+		const uint64_t a = t0 + (uint64_t)threadIdx.x * kHeadsPer;
+		uint32_t mask = 0;
+		if (a < nslow) {
+			uint32_t prev = a == 0 ? 0xffffffffu : (uint32_t)(d.slow_keys[a - 1] >> 32);
+			for (uint32_t k = 0; k < kHeadsPer && a + k < nslow; k++) {
+				const uint32_t s = (uint32_t)(d.slow_keys[a + k] >> 32);
+				if (s != prev)
+					mask |= 1u << k;
+				prev = s;
+			}
+		}
+		const uint32_t cnt = (uint32_t)__popc(mask);
+		uint32_t total;
+		const uint32_t incl = block_scan(cnt, part, &total);
+		if (threadIdx.x == 0)
+			base = atomicAdd(&d.ctr[CTR_HEADS], (unsigned long long)total);
+		__syncthreads();
+		uint32_t at = (uint32_t)base + incl - cnt;
+		while (mask) {
+			const uint32_t k = (uint32_t)__ffs(mask) - 1u;
+			mask &= mask - 1u;
+			d.heads[at++] = (uint32_t)(a + k);
+		}
+		__syncthreads(); // base is rewritten for the next tile
+	}
 }
 
 // Pass 1: the arena bytes of each block's claims.
@@ -2093,7 +2160,8 @@ hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_
 }
 size_t sess_state_bytes() { return sizeof(SessState); }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, 64, cus * 16)), dim3(64), 0, st, d, nslow);
+	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * 4)), dim3(kWalkThreads), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {

@@ -106,6 +106,7 @@ enum : uint8_t { KT_OTHER = 0, KT_HOST = 1, KT_CLIENT0 = 2 }; // client key k ->
 
 struct KeyTrie {
 	uint8_t next[kTrieNodes][128]; // next node for a lower-cased 7-bit key byte
+	uint8_t cls[256];              // byte_class() of every byte (a table the session path keeps in LDS)
 	uint8_t type[kTrieNodes];      // KT_*
 	uint8_t nodes;
 };
@@ -151,7 +152,7 @@ EBD_HD uint8_t gp_key_type(const KeyTrie* t, uint8_t node) { return t->type[node
 
 // One byte (P:124-160 and the handlers P:162-364).  pos = request-stream position.
 EBD_HD void gp_step(GenParser& g, const KeyTrie* trie, uint32_t c, uint32_t pos) {
-	const uint8_t cls = byte_class(c);
+	const uint8_t cls = trie->cls[c & 255];
 	switch (g.state) {
 	case ST_METHOD: // P:162-188
 		if (cls & C_UPPER) {

@@ -30,7 +30,7 @@ def main():
     E, cfg = args.events, args.config
     ctx = ebd.Context(max_events=E, service_capacity=1 << max(20, int(np.ceil(np.log2(E * 0.8)))),
                       string_arena=max(256 << 20, E * 48), timing=True)
-    size = ebd.trace_size_device(ctx, cfg, cfg, 0, E, align=16)
+    E, size = ebd.trace_size_device(ctx, cfg, cfg, 0, E, align=16, with_events=True)
     ev = torch.empty(E * 36, dtype=torch.uint8, device=dev)
     ln = torch.empty(E, dtype=torch.int32, device=dev)
     of = torch.empty(E, dtype=torch.int64, device=dev)
@@ -54,6 +54,7 @@ def main():
     fr = kt["k_fresh"][1] / max(kt["k_fresh"][0], 1)
     print(json.dumps({"lib": os.path.basename(ebd.LIB_PATH), "cold": args.cold, "events": E, "step_ms": dt * 1e3, "events_per_s": E / dt,
                       "k_fresh_ms": fr, "k_fresh_alg_gbps": alg / fr / 1e6,
+                      "session_events": ctx.stats()["session_events"],
                       "kernel_ms": {k: v[1] / v[0] for k, v in kt.items() if v[0]},
                       "errors": ctx.stats()["error_names"]}))
 
