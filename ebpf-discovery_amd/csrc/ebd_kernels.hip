@@ -323,7 +323,11 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 // Logical index (s << 8) | b into the LDS image (ebd_dfa.h: byte-major, kLdsStride).
 struct LdsTable {
 	const uint8_t* t;
+#ifdef EBD_STATE_MAJOR
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
+#else
 	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i & 0xffu) * kLdsStride + (i >> 8)]; }
+#endif
 };
 
 // One 16-byte chunk as 4 little-endian words.
@@ -351,12 +355,21 @@ struct DevMem {
 	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
 };
 
-constexpr int kFreshThreads = 1024;
+#ifndef EBD_FRESH_THREADS
+#define EBD_FRESH_THREADS 1024
+#endif
+#ifndef EBD_FRESH_WGS
+#define EBD_FRESH_WGS 1 // workgroups per CU
+#endif
+constexpr int kFreshThreads = EBD_FRESH_THREADS;
 constexpr int kFreshWaves = kFreshThreads / 64;
 #ifndef EBD_SCAN_WAVES
-#define EBD_SCAN_WAVES 12
+#define EBD_SCAN_WAVES 10
 #endif
-constexpr int kScanWaves = EBD_SCAN_WAVES; // waves [0, kScanWaves) scan; the others finalize
+// waves [0, kScanWaves) scan; the others finalize.  Finalize is latency-bound (tracker words
+// and endpoint bytes past the staged 64 B come from HBM): 10 scan + 6 finalize waves beat
+// 12 + 4 (2.74 vs 2.87 ms per 20 M config-3 events) and 11 + 5 or 9 + 7.
+constexpr int kScanWaves = EBD_SCAN_WAVES;
 constexpr int kFinWaves = kFreshWaves - kScanWaves;
 constexpr uint32_t kScanLanes = kScanWaves * 64, kFinLanes = kFinWaves * 64;
 #ifndef EBD_RING
@@ -370,7 +383,11 @@ static_assert(kRing >= 128 && (kRing & (kRing - 1)) == 0, "ring: a power of two 
 
 // LDS address of entry (s, byte k of word x): v_bfe (off the state chain) + v_mad_u32_u24.
 __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t x, int k) {
+#ifdef EBD_STATE_MAJOR // entry (s, b) at s * 256 + b: one v_perm_b32 builds the index
+	return __builtin_amdgcn_perm(s, x, 0x0c0c0400u | (uint32_t)(k & 3));
+#else
 	return __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8) * kLdsStride + s;
+#endif
 }
 
 // Every byte of w in [0x20, 0x7e] (SWAR: no byte < 0x20, none >= 0x7f; exact tests).
@@ -382,11 +399,13 @@ __device__ __forceinline__ bool printable4(uint32_t w) {
 
 // 16 DFA steps over one chunk: s advances, m = the maximum next state, qs = the states at
 // the quarter starts (s0 | s4 << 8 | s8 << 16 | s12 << 24), qm = running maxima after 4, 8
-// and 12 steps (ebd_fresh.h chunk_update).  A quarter (one 4-byte word) whose start state
-// is a generic header-value state (di.vl0 / di.vl1: they step to themselves on every byte
-// in [0x20, 0x7e], checked when the table is built) and whose bytes are all in that range
-// leaves the state as it is: the lane skips its 4 table reads (exec-masked), which takes
-// the User-Agent-style padding that dominates request bytes off the LDS.
+// and 12 steps (ebd_fresh.h chunk_update).  With EBD_SKIP, a quarter (one 4-byte word)
+// whose start state is a generic header-value state (di.vl0 / di.vl1: they step to
+// themselves on every byte in [0x20, 0x7e], checked when the table is built) and whose
+// bytes are all in that range leaves the state as it is and the lane skips its 4 table
+// reads.  The skip is exec-masked: the wave still waits for the lanes that step, and the
+// test costs more issue slots than the LDS reads it saves (20 M config-3 events: 2.87 ms
+// without, 2.92 ms with), so it is off by default.
 __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t vl0, uint32_t vl1, uint32_t& s,
 		uint32_t& m, uint32_t& qs, uint32_t& qm) {
 	qs = s;
@@ -394,7 +413,7 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 #pragma unroll
 	for (int q = 0; q < 4; q++) {
 		const uint32_t x = w.w[q];
-#ifndef EBD_NO_SKIP
+#ifdef EBD_SKIP
 		const bool skip = (s == vl0 || s == vl1) && printable4(x);
 #else
 		const bool skip = false;
@@ -402,7 +421,11 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 		if (!skip) {
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
+#ifndef EBD_EXP_FAKESTEP
 				s = T[tab_index(s, x, k)];
+#else // experiment: a VALU-only step in place of the LDS table read (results are wrong)
+				s = 64u | ((s * 5u + __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8)) & 63u);
+#endif
 				m = max(m, s);
 			}
 		} else {
@@ -533,7 +556,11 @@ static_assert(R_WORDS == 16, "finalize record is 16 words");
 // reads the request line and usually the Host header from LDS instead of reloading lines
 // that left L2 while the lane scanned the rest of the buffer.  Rows are structure of
 // arrays too: word j of the row of lane (or slot) l at [j * stride + l], one row of slack.
+#ifndef EBD_NO_STAGING
 constexpr uint32_t kStage = 64, kStageWords = kStage / 4;
+#else // experiment: finalize reads every byte from the buffer (no LDS staging)
+constexpr uint32_t kStage = 0, kStageWords = 1;
+#endif
 
 // Buffer bytes for fresh_finalize: offsets [0, lim) from the staged copy (word j at
 // s[j * kFinLanes]), the rest from the buffer in global memory.
@@ -616,7 +643,11 @@ struct FreshLds {
 	FreshShared sh;
 };
 
-__global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
+__global__ __launch_bounds__(kFreshThreads)
+#if EBD_FRESH_WGS > 1
+__attribute__((amdgpu_waves_per_eu(EBD_FRESH_WGS * kFreshThreads / 256, 8)))
+#endif
+void k_fresh(Dev d) {
 	__shared__ __attribute__((aligned(16))) FreshLds lds;
 	uint8_t* T = lds.T;
 	FreshShared& sh = lds.sh;
@@ -743,9 +774,11 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 #pragma unroll
 			for (uint32_t f = 0; f < R_WORDS; f++)
 				sh.ring[f * kRing + slot] = t[f];
+#ifndef EBD_NO_STAGING
 #pragma unroll
 			for (uint32_t j = 0; j < kStageWords; j++)
 				sh.rdata[j * kRing + slot] = stg[j * kScanLanes];
+#endif
 			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
 	};
@@ -822,19 +855,28 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 		if (valid) {
 			if (w0 == 0) {
 				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
+#ifndef EBD_NO_STAGING
 #pragma unroll
 				for (int k = 0; k < 4; k++) // window 0 into the lane's staging row
 #pragma unroll
 					for (int j = 0; j < 4; j++)
 						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
+#endif
 			}
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
+#ifndef EBD_EXP_NOSCAN
 				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm);
+#else // experiment: the window stream alone, no DFA (results are wrong)
+				sx = (s ^ X[k].w[0] ^ X[k].w[1] ^ X[k].w[2] ^ X[k].w[3]) & 63u;
+				m = qs = qm = sx;
+#endif
 				if (live) {
 					const uint32_t c = 4 * w0 + k;
+#ifndef EBD_EXP_NOTRACK // experiment: no crossing trackers (results are wrong)
 					chunk_update(di, sr, c, s, qs, qm, m);
+#endif
 					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
 					s = sx;
 				}
@@ -842,7 +884,9 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 			w0++;
 			done = !live;
 		}
+#ifndef EBD_EXP_NOPUSH // experiment: no records for finalize (results are wrong)
 		push(done);
+#endif
 		if (done) {
 			e0 = e1;
 			e1 = lane_ev(d, grab(), re);
@@ -2130,7 +2174,7 @@ uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
 	const uint64_t groups = ((uint64_t)d.n + kFreshThreads * 4 - 1) / (kFreshThreads * 4);
-	const int grid = (int)(groups < (uint64_t)cus ? groups : (uint64_t)cus);
+	const int grid = (int)(groups < (uint64_t)cus * EBD_FRESH_WGS ? groups : (uint64_t)cus * EBD_FRESH_WGS);
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
