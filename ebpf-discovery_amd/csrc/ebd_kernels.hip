@@ -118,12 +118,14 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 		return kNone;
 	}
 	Slot* s = d.slots + idx;
+#ifndef EBD_EXP_AGG_NOATOMIC // experiment: probe only, no counter / first-arrival atomics
 	if (inc_int)
 		atomicAdd(&s->internal_clients, inc_int);
 	if (inc_ext)
 		atomicAdd(&s->external_clients, inc_ext);
 	if (first < seen_first)
 		atomicMin(&s->first, first);
+#endif
 	return idx;
 }
 
@@ -1530,6 +1532,11 @@ struct AggShared {
 
 __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
 		unsigned long long net) {
+#ifdef EBD_EXP_AGG_NOINSERT // experiment: classification only (results are wrong)
+	if (cls == 7)
+		atomicAdd(&sh.cn, 1u);
+	return;
+#endif
 	bool claimed;
 	const Hash128 key = d.keys[i];
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
@@ -1547,7 +1554,11 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 __device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh) {
 	ebd_event_result r = d.res[i];
 	unsigned long long net = 0;
+#ifndef EBD_EXP_AGG_NOCIP // experiment: no client-IP token parse (results are wrong)
 	const uint32_t cls = cip_classify(d, i, r, row, &net);
+#else
+	const uint32_t cls = CLS_INTERNAL;
+#endif
 	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 	d.res[i] = r;
 	agg_request(d, i, r, cls, sh, net);
