@@ -408,8 +408,15 @@ __device__ __forceinline__ bool printable4(uint32_t w) {
 // reads.  The skip is exec-masked: the wave still waits for the lanes that step, and the
 // test costs more issue slots than the LDS reads it saves (20 M config-3 events: 2.87 ms
 // without, 2.92 ms with), so it is off by default.
+#ifdef EBD_EXP_DUAL
+#define DUAL_ARG , uint32_t& g_dual
+#define DUAL_PASS , dual
+#else
+#define DUAL_ARG
+#define DUAL_PASS
+#endif
 __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t vl0, uint32_t vl1, uint32_t& s,
-		uint32_t& m, uint32_t& qs, uint32_t& qm) {
+		uint32_t& m, uint32_t& qs, uint32_t& qm DUAL_ARG) {
 	qs = s;
 	m = 0;
 #pragma unroll
@@ -423,21 +430,32 @@ __device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uin
 		if (!skip) {
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
+#ifdef EBD_EXP_DUAL // experiment: a second, independent chain over the same bytes (ILP probe)
+				g_dual = T[tab_index(g_dual, x, k)];
+#endif
 #ifndef EBD_EXP_FAKESTEP
 				s = T[tab_index(s, x, k)];
 #else // experiment: a VALU-only step in place of the LDS table read (results are wrong)
 				s = 64u | ((s * 5u + __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8)) & 63u);
 #endif
+#ifndef EBD_EXP_LEAN
 				m = max(m, s);
+#endif
 			}
 		} else {
 			m = max(m, s);
 		}
+#ifndef EBD_EXP_LEAN
 		if (q < 3) {
 			qs |= s << (8 * (q + 1));
 			qm = q == 0 ? m : (qm | (m << (8 * q)));
 		}
+#endif
 	}
+#ifdef EBD_EXP_LEAN // experiment: steps only, no chunk maximum or quarter states (results are wrong)
+	m = s;
+	qm = 0;
+#endif
 }
 
 // quad_perm DPP: the value of `v` held by quad lane P's pattern
@@ -631,6 +649,10 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+#ifdef EBD_EXP_LEAN
+		d.res[i] = fr.r;
+		return;
+#endif
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
 		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
@@ -735,6 +757,9 @@ void k_fresh(Dev d) {
 	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
 	uint32_t w0 = 0; // e0's window to scan next
 	uint32_t s = di.init, live = 0, post = 0;
+#ifdef EBD_EXP_DUAL
+	uint32_t dual = di.init + 1;
+#endif
 	ScanRec sr;
 	rec_init(di, sr);
 
@@ -869,7 +894,7 @@ void k_fresh(Dev d) {
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
 #ifndef EBD_EXP_NOSCAN
-				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm);
+				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm DUAL_PASS);
 #else // experiment: the window stream alone, no DFA (results are wrong)
 				sx = (s ^ X[k].w[0] ^ X[k].w[1] ^ X[k].w[2] ^ X[k].w[3]) & 63u;
 				m = qs = qm = sx;
@@ -877,7 +902,19 @@ void k_fresh(Dev d) {
 				if (live) {
 					const uint32_t c = 4 * w0 + k;
 #ifndef EBD_EXP_NOTRACK // experiment: no crossing trackers (results are wrong)
+#ifndef EBD_EXP_LEAN
 					chunk_update(di, sr, c, s, qs, qm, m);
+#else // one select per tracker of (chunk | start state << 16)
+					{
+						const uint32_t pk = c | (s << 16);
+						sr.url.c = st_pred<RS_URL>(di, s) ? sr.url.c : pk;
+						sr.host.c = st_pred<RS_HOST>(di, s) ? sr.host.c : pk;
+						sr.hend.c = st_pred<RS_HEND>(di, s) ? sr.hend.c : pk;
+						sr.cip.c = sr.cseen ? sr.cip.c : pk;
+						sr.cseen |= s >= di.hvc0 ? 1u : 0u;
+						sr.term.c = c;
+					}
+#endif
 #endif
 					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
 					s = sx;
@@ -895,6 +932,10 @@ void k_fresh(Dev d) {
 			resolve();
 		}
 	}
+#ifdef EBD_EXP_DUAL
+	if ((dual ^ d.n) == 0x7fffffffu) // never: keeps the second chain alive
+		set_error(d, EBD_ERR_INTERNAL);
+#endif
 	if (lane == 0)
 		atomicAdd(&sh.scan_done, 1u);
 }
@@ -1509,11 +1550,14 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
 // and events).  The client class comes from the client-IP header's front token when k_fresh
 // found one (cip_classify), else from the session's source address (Aggregator.cpp:60-66,
-// 85-88).  A block walks a contiguous range of the batch 256 events at a time.  Requests
-// with a client-IP header (~30 % in config 3) are queued in LDS and parsed kAggThreads at a
-// time, so the token parse, the longest code path, runs on full waves instead of on the
-// few lanes of each wave that have one.  Aggregation is order-free (counters, atomicMin of
-// the first-arrival word), so queueing does not change the result.
+// 85-88).  A block walks a contiguous range of the batch 256 events at a time, each wave
+// its own 64 of them, and the waves never wait for each other: every step of a wave is a
+// chain of dependent random accesses (result, key, slot probe, claim / counter atomics), and
+// a block-wide barrier per step made each step last as long as the slowest of 256 chains.
+// Requests with a client-IP header (~30 % in config 3) go to the wave's own LDS ring and are
+// parsed 64 at a time, so the token parse, the longest code path, runs on full waves instead
+// of on the few lanes of each wave that have one.  Aggregation is order-free (counters,
+// atomicMin of the first-arrival word), so queueing does not change the result.
 //
 // A service created here only claims its slot: the claim (slot, claiming event) goes to the
 // block's own stretch of the claim stage, counted in LDS, with no global atomic.  The
@@ -1521,12 +1565,12 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // a scan of the per-block counts (k_pub_count, k_pub_scan) and copy the endpoint bytes
 // (k_publish).  A single global counter serialises at ~12 ns per atomic: reserving per block
 // and step cost ~5 ms per 100 M-event batch that creates 30 M services.
-constexpr uint32_t kCipQueue = 2 * kAggThreads;
+constexpr uint32_t kAggWaves = kAggThreads / 64;
+constexpr uint32_t kCipRing = 128; // per wave: < 64 waiting + at most 64 new per step
 
 struct AggShared {
-	uint32_t q[kCipQueue]; // queued client-IP requests
-	uint32_t qn;
-	uint32_t cn;           // claims of this block
+	uint32_t q[kAggWaves][kCipRing]; // each wave's queued client-IP requests (a ring)
+	uint32_t cn;                     // claims of this block
 	unsigned long long nreq;
 };
 
@@ -1570,28 +1614,38 @@ EBD_HD uint32_t agg_steps_per_block(uint32_t n, uint32_t grid) {
 	return (steps + grid - 1) / grid;
 }
 
+// LDS words written by some lanes of a wave and then read by others: order the accesses.
+__device__ __forceinline__ void wave_sync() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
 	__shared__ AggShared sh;
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 	uint8_t* row = rows + threadIdx.x * kCipStride;
+	uint32_t* q = sh.q[wave];
 	if (threadIdx.x == 0) {
 		sh.nreq = 0;
-		sh.qn = 0;
 		sh.cn = 0;
 	}
 	__syncthreads();
 	uint32_t cnt = 0;
+	uint32_t qh = 0, qn = 0; // wave-uniform: ring head and queued requests
 	const uint32_t steps = (d.n + kAggThreads - 1) / kAggThreads;
 	const uint32_t per = agg_steps_per_block(d.n, gridDim.x);
 	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
-	for (uint32_t st = s0; st < s1; st++) { // uniform trip count: the barriers below are safe
-		const uint32_t i = st * kAggThreads + threadIdx.x;
+	for (uint32_t st = s0; st < s1; st++) {
+		const uint32_t i = st * kAggThreads + wave * 64 + lane;
+		bool queue = false;
 		if (i < d.n) {
 			ebd_event_result r = d.res[i];
 			if (r.status == EBD_STATUS_FINISHED && !(r.info & EBD_INFO_SESSION)) {
 				cnt++;
 				if (r.info & EBD_INFO_CIP) {
-					sh.q[atomicAdd(&sh.qn, 1u)] = i;
+					queue = true;
 				} else {
 					const uint8_t* evb = (const uint8_t*)(d.ev + i);
 					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
@@ -1605,25 +1659,21 @@ __global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
 				}
 			}
 		}
-		__syncthreads();
-		const uint32_t m = sh.qn; // < kCipQueue: below kAggThreads before this step, + at most kAggThreads
-		__syncthreads();          // every thread has read qn before a push or the drain changes it
-		const bool last = st + 1 == s1;
-		if (m >= kAggThreads || (last && m > 0)) { // full waves; the block's last step drains the rest
-			if (threadIdx.x < min(m, (uint32_t)kAggThreads))
-				agg_cip_one(d, sh.q[threadIdx.x], row, sh);
-			__syncthreads();
-			if (m >= kAggThreads && threadIdx.x < m - kAggThreads) // [kAggThreads, m) -> [0, m - kAggThreads)
-				sh.q[threadIdx.x] = sh.q[kAggThreads + threadIdx.x];
-			if (threadIdx.x == 0)
-				sh.qn = m >= kAggThreads ? m - kAggThreads : 0;
-			__syncthreads();
-		}
-		if (last && m > kAggThreads) { // the block's last step: what one drain left goes too
-			if (threadIdx.x < m - kAggThreads)
-				agg_cip_one(d, sh.q[threadIdx.x], row, sh);
+		const unsigned long long b = __ballot(queue);
+		if (queue)
+			q[(qh + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))) & (kCipRing - 1)] = i;
+		qn += (uint32_t)__popcll(b);
+		if (qn >= 64) { // a full wave of client-IP requests
+			wave_sync();
+			agg_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row, sh);
+			qh += 64;
+			qn -= 64;
+			wave_sync(); // the ring words just read may be rewritten by the next step
 		}
 	}
+	wave_sync();
+	if (lane < qn) // what is left in the ring
+		agg_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row, sh);
 	atomicAdd(&sh.nreq, (unsigned long long)cnt);
 	__syncthreads();
 	if (threadIdx.x == 0) {
@@ -2179,7 +2229,22 @@ static int grid_for(uint64_t items, int block, int cap) {
 		g = 1;
 	return (int)(g > (uint64_t)cap ? cap : g);
 }
-static uint32_t agg_grid(uint32_t n, int cus) { return (uint32_t)grid_for(n, kAggThreads, min(cus * 8, 2048)); } // k_pub_scan: <= 2048
+// k_agg_fast's grid: the blocks that are resident at once (more would run as a second, partial
+// round after the first; fewer leave the random-access latency exposed), at most 2048
+// (k_pub_scan scans 2 per thread).
+static uint32_t agg_blocks_per_cu() {
+	static int bpc = 0;
+	if (bpc <= 0) {
+		int nb = 0;
+		if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_agg_fast, kAggThreads, 0) != hipSuccess || nb <= 0)
+			nb = 4;
+		bpc = nb;
+	}
+	return (uint32_t)bpc;
+}
+static uint32_t agg_grid(uint32_t n, int cus) {
+	return (uint32_t)grid_for(n, kAggThreads, (int)min((uint32_t)cus * agg_blocks_per_cu(), 2048u));
+} // k_pub_scan: <= 2048
 uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n, agg_grid(n, cus)) * kAggThreads; }
 
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {

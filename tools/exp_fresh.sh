@@ -6,5 +6,5 @@ mkdir -p gpurun_out
 for v in "$@"; do
 	if [ "$v" = default ]; then unset EBD_LIB; else export EBD_LIB=$PWD/ebpf-discovery_amd/build/variants/libebd_amd_$v.so; fi
 	echo "=== $v"
-	timeout -k 10 180 python tools/perf_fresh.py --events 20000000 --reps 3 || exit $?
+	timeout -k 10 ${EXP_TIMEOUT:-90} python tools/perf_fresh.py --events 20000000 --reps 3 || exit $?
 done
