@@ -878,6 +878,10 @@ void k_fresh(Dev d) {
 			tw = nw;
 		}
 		transpose_quad(X, r);
+#ifdef EBD_EXP_XPOSE3 // experiment: two more transposes (an involution: results unchanged), to price one
+		transpose_quad(X, r);
+		transpose_quad(X, r);
+#endif
 		bool done = false;
 		if (valid) {
 			if (w0 == 0) {

@@ -66,18 +66,18 @@ __global__ __launch_bounds__(1024) void k_chain(const uint8_t* gtab, const uint3
 
 template <int LAYOUT, int ILP>
 static double run(const uint8_t* dtab, const uint32_t* dtext, uint32_t nwords, uint32_t* dout, int blocks, uint32_t iters,
-		size_t pad) {
+		size_t pad, int threads = 1024) {
 	hipEvent_t a, b;
 	(void)hipEventCreate(&a);
 	(void)hipEventCreate(&b);
-	hipLaunchKernelGGL((k_chain<LAYOUT, ILP>), dim3(blocks), dim3(1024), pad, 0, dtab, dtext, nwords, iters, dout);
+	hipLaunchKernelGGL((k_chain<LAYOUT, ILP>), dim3(blocks), dim3(threads), pad, 0, dtab, dtext, nwords, iters, dout);
 	(void)hipEventRecord(a);
-	hipLaunchKernelGGL((k_chain<LAYOUT, ILP>), dim3(blocks), dim3(1024), pad, 0, dtab, dtext, nwords, iters, dout);
+	hipLaunchKernelGGL((k_chain<LAYOUT, ILP>), dim3(blocks), dim3(threads), pad, 0, dtab, dtext, nwords, iters, dout);
 	(void)hipEventRecord(b);
 	(void)hipEventSynchronize(b);
 	float ms = 0;
 	(void)hipEventElapsedTime(&ms, a, b);
-	const double steps = (double)blocks * 1024 * ILP * iters * 16;
+	const double steps = (double)blocks * threads * ILP * iters * 16;
 	return steps / (ms * 1e-3) / 1e9; // G byte-steps / s
 }
 
@@ -127,6 +127,12 @@ int main() {
 				run<1, 1>(dtab, dtext, nwords, dout, blocks, iters, pad), run<1, 2>(dtab, dtext, nwords, dout, blocks, iters, pad),
 				run<2, 1>(dtab, dtext, nwords, dout, blocks, iters, pad), run<2, 2>(dtab, dtext, nwords, dout, blocks, iters, pad),
 				run<2, 4>(dtab, dtext, nwords, dout, blocks, iters, pad));
+	}
+	// chains per CU: scan lanes of k_fresh (640 = 10 waves) at ILP 1 and 2, one block per CU
+	for (int th : {384, 640, 1024}) {
+		const size_t pad = 40 * 1024;
+		printf("threads=%d  L2/ILP1 %.0f  L2/ILP2 %.0f  L2/ILP4 %.0f (G steps/s)\n", th, run<2, 1>(dtab, dtext, nwords, dout, cus * 8, iters, pad, th),
+				run<2, 2>(dtab, dtext, nwords, dout, cus * 8, iters, pad, th), run<2, 4>(dtab, dtext, nwords, dout, cus * 8, iters, pad, th));
 	}
 	return 0;
 }
