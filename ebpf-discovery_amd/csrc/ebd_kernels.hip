@@ -1625,7 +1625,11 @@ __device__ __forceinline__ void wave_sync() {
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(kAggThreads) void k_agg_fast(Dev d) {
+// 6 waves per SIMD: the compiler fits the kernel in 80 VGPRs without spilling (91 unbounded, 5 waves)
+#ifndef EBD_AGG_WAVES
+#define EBD_AGG_WAVES 6
+#endif
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(EBD_AGG_WAVES, 8))) void k_agg_fast(Dev d) {
 	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
 	__shared__ AggShared sh;
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
