@@ -59,7 +59,8 @@ hipError_t launch_net_clean(const Dev& d, unsigned long long now, unsigned long 
 hipError_t launch_keep_collect(const Dev& d, KeepRec* keep, unsigned long long* kbytes, unsigned long long kcap, hipStream_t st,
 		int cus);
 hipError_t launch_keep_insert(const Dev& d, const KeepRec* keep, const uint8_t* kbytes, uint32_t* remap, hipStream_t st, int cus);
-hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap, hipStream_t st, int cus);
+hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap,
+		const unsigned long long* old_v6d, hipStream_t st, int cus);
 hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus);
 } // namespace ebd
 
@@ -155,7 +156,7 @@ struct ebd_ctx {
 	NetEnt* d_nets[2] = {nullptr, nullptr};
 	int net_cur = 0;
 	uint32_t net_cap = 0;
-	unsigned long long* d_v6d = nullptr;
+	unsigned long long* d_v6d[2] = {nullptr, nullptr}; // v6 prefix dictionary, swapped with d_nets
 	uint32_t v6d_cap = 0;
 	uint64_t clock_ns = 0; // ebd_set_clock (0: CLOCK_MONOTONIC per batch)
 	KeepRec* d_keep = nullptr;
@@ -295,7 +296,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.net_on = c->net_on;
 	d.nets = c->d_nets[c->net_cur];
 	d.net_mask = c->net_cap ? c->net_cap - 1 : 0;
-	d.v6d = c->d_v6d;
+	d.v6d = c->d_v6d[c->net_cur];
 	d.v6d_mask = c->v6d_cap ? c->v6d_cap - 1 : 0;
 	d.now = 1;
 	return d;
@@ -316,7 +317,7 @@ static void ctx_free(ebd_ctx* c) {
 			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
-			c->d_v6d, c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
+			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
 	for (void* p : ptrs)
 		if (p)
 			(void)hipFree(p);
@@ -498,8 +499,10 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 			CTX_TRY(hipMalloc(&c->d_nets[k], (size_t)c->net_cap * sizeof(NetEnt)));
 			CTX_TRY(hipMemsetAsync(c->d_nets[k], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
 		}
-		CTX_TRY(hipMalloc(&c->d_v6d, (size_t)c->v6d_cap * sizeof(unsigned long long)));
-		CTX_TRY(hipMemsetAsync(c->d_v6d, 0, (size_t)c->v6d_cap * sizeof(unsigned long long), c->stream));
+		for (int k = 0; k < 2; k++) {
+			CTX_TRY(hipMalloc(&c->d_v6d[k], (size_t)c->v6d_cap * sizeof(unsigned long long)));
+			CTX_TRY(hipMemsetAsync(c->d_v6d[k], 0, (size_t)c->v6d_cap * sizeof(unsigned long long), c->stream));
+		}
 	}
 	CTX_TRY(hipStreamSynchronize(c->stream));
 #undef CTX_TRY
@@ -817,11 +820,13 @@ static int validate_batch(const ebd_ctx* c, const ebd_discovery_event* events, c
 static int stage_locked(ebd_ctx* c, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
 		const uint8_t* payload, uint64_t payload_bytes, uint32_t n, uint64_t* ticket) {
 	HIP_TRY(hipSetDevice(c->device));
-	const int s = c->next_slot;
+	// any slot not holding a staged batch (tickets may be submitted out of order), next_slot first
+	int s = c->next_slot;
+	if (c->stg[s].staged)
+		s ^= 1;
 	auto& g = c->stg[s];
 	if (g.staged)
 		return -EBUSY; // two batches are already staged and not submitted
-	c->next_slot ^= 1;
 	if (!g.ev) {
 		HIP_TRY(hipMalloc(&g.ev, (size_t)c->max_events * sizeof(EventRec)));
 		HIP_TRY(hipMalloc(&g.len, (size_t)c->max_events * sizeof(uint32_t)));
@@ -848,6 +853,7 @@ static int stage_locked(ebd_ctx* c, const ebd_discovery_event* events, const uin
 	if (int rc = upload(c, g.payload, payload, payload_bytes))
 		return rc;
 	HIP_TRY(hipEventRecord(g.up, c->cstream));
+	c->next_slot = s ^ 1; // only once the slot is staged
 	g.n = n;
 	g.staged = 1;
 	g.ticket = c->next_ticket++;
@@ -1014,6 +1020,22 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 	return 0;
 }
 
+// The live network-map entries move into the other (zeroed) table and their v6 prefixes into the
+// other (zeroed) dictionary, under the slots remap gives (nullptr: the same slots).  Erased
+// entries and dictionary slots only they used are dropped (ebd_kernels.hip k_net_remap).
+static int rebuild_nets(ebd_ctx* c, const uint32_t* remap) {
+	const int nxt = c->net_cur ^ 1;
+	HIP_TRY(hipMemsetAsync(c->d_nets[nxt], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_v6d[nxt], 0, (size_t)c->v6d_cap * sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_NETS, 0, 2 * sizeof(unsigned long long), c->stream)); // CTR_NETS, CTR_V6D
+	Dev dn = make_dev(c);
+	dn.nets = c->d_nets[nxt];
+	dn.v6d = c->d_v6d[nxt];
+	HIP_TRY(launch_net_remap(dn, c->d_nets[c->net_cur], c->net_cap - 1, remap, c->d_v6d[c->net_cur], c->stream, c->cus));
+	c->net_cur = nxt;
+	return 0;
+}
+
 // Aggregator::clear with network counters (A:138-149): the services with a non-empty map
 // survive, re-inserted into the emptied table with zeroed client counters; their map entries
 // move to a fresh table under the new slots (ebd_kernels.hip k_keep_collect .. k_net_remap).
@@ -1043,14 +1065,7 @@ static int clear_keep_nets(ebd_ctx* c) {
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_keep_insert(d, c->d_keep, (const uint8_t*)c->d_kbytes, c->d_remap, c->stream, c->cus));
-	const int nxt = c->net_cur ^ 1;
-	HIP_TRY(hipMemsetAsync(c->d_nets[nxt], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
-	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_NETS, 0, sizeof(unsigned long long), c->stream));
-	Dev dn = d;
-	dn.nets = c->d_nets[nxt];
-	HIP_TRY(launch_net_remap(dn, c->d_nets[c->net_cur], c->net_cap - 1, c->d_remap, c->stream, c->cus));
-	c->net_cur = nxt;
-	return 0;
+	return rebuild_nets(c, c->d_remap);
 }
 
 int ebd_clear(ebd_ctx* c) {
@@ -1083,7 +1098,17 @@ int ebd_network_counters_cleaning(ebd_ctx* c, uint64_t now_ns) {
 	HIP_TRY(hipSetDevice(c->device));
 	const uint64_t now = now_ns ? now_ns : ctx_now(c);
 	HIP_TRY(launch_net_clean(make_dev(c), now, 3600ull * 1000000000ull, c->stream, c->cus)); // std::chrono::hours(1)
+	// Erased entries keep their keys (a later request of the same prefix reuses them), so a
+	// daemon that cleans but never clears would fill the table and the v6 dictionary with
+	// dead keys: past half full, both are rebuilt from the live entries.
+	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	if (2 * c->h_ctr[CTR_NETS] > c->net_cap || 2 * c->h_ctr[CTR_V6D] > c->v6d_cap) {
+		const int rc = rebuild_nets(c, nullptr);
+		if (rc)
+			return rc;
+		HIP_TRY(hipStreamSynchronize(c->stream));
+	}
 	return 0;
 }
 

@@ -2026,19 +2026,30 @@ __global__ void k_keep_insert(Dev d, const KeepRec* keep, const uint8_t* kbytes,
 	}
 }
 
-// Live entries of the old table into the (zeroed) new one under their services' new slots.
-__global__ void k_net_remap(Dev d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap) {
+// Live entries of the old table into the (zeroed) new one under their services' new slots
+// (remap == nullptr: the same slots, a compaction).  Erased entries and the v6 prefixes only
+// they used are dropped: a v6 prefix is re-interned from the old dictionary into d.v6d (a
+// zeroed one), so neither table keeps more than the live map entries (Aggregator.cpp:182-209
+// erases them; the maps hold at most one retention period of prefixes).
+__global__ void k_net_remap(Dev d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap,
+		const unsigned long long* old_v6d) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k <= old_mask; k += gridDim.x * blockDim.x) {
 		const NetEnt e = old[k];
 		if (e.key == 0 || e.time == 0)
 			continue;
 		const uint32_t kind = (uint32_t)(e.key >> 62), slot = (uint32_t)(e.key >> 31) & 0x7fffffffu;
-		const uint32_t ns = remap[slot];
+		const uint32_t ns = remap ? remap[slot] : slot;
 		if (ns == kNone) { // a live entry belongs to a service with a non-empty map: kept
 			set_error(d, EBD_ERR_INTERNAL);
 			continue;
 		}
-		NetEnt* ne = net_find_or_claim(d, d.nets, d.net_mask, net_key(kind, ns, (uint32_t)(e.key & 0x7fffffffu)));
+		uint32_t v = (uint32_t)(e.key & 0x7fffffffu);
+		if (kind == NET_V6) {
+			v = v6d_index(d, old_v6d[v] & 0xffffffffffffull);
+			if (v == kNone)
+				continue;
+		}
+		NetEnt* ne = net_find_or_claim(d, d.nets, d.net_mask, net_key(kind, ns, v));
 		if (ne)
 			ne->time = e.time;
 	}
@@ -2354,8 +2365,10 @@ hipError_t launch_keep_insert(const Dev& d, const KeepRec* keep, const uint8_t* 
 	hipLaunchKernelGGL(k_keep_insert, dim3(cus * 4), dim3(256), 0, st, d, keep, kbytes, remap);
 	return hipGetLastError();
 }
-hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_net_remap, dim3(grid_for((uint64_t)old_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, old, old_mask, remap);
+hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, const uint32_t* remap,
+		const unsigned long long* old_v6d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_net_remap, dim3(grid_for((uint64_t)old_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, old, old_mask, remap,
+			old_v6d);
 	return hipGetLastError();
 }
 hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus) {

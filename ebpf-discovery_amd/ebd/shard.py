@@ -27,6 +27,7 @@ import numpy as np
 from . import SERVICE_DTYPE
 
 REC = SERVICE_DTYPE  # the exchanged record: ebd_service (include/ebpf_discovery_amd.h)
+STR_SLACK = 64  # readable bytes past received endpoint strings (k_merge copies 8-byte words)
 M32 = np.uint64(0xFFFFFFFF)
 
 
@@ -198,15 +199,18 @@ def exchange(recs, strings, counts, scounts, group=None):
     out_r = torch.empty(int(rcounts.sum()) * nrec, dtype=torch.uint8, device=dev)
     dist.all_to_all_single(out_r, recs, output_split_sizes=[int(c) * nrec for c in rcounts],
                            input_split_sizes=[int(c) * nrec for c in counts], group=group)
-    out_s = torch.empty(int(rscounts.sum()), dtype=torch.uint8, device=dev)
-    dist.all_to_all_single(out_s, strings, output_split_sizes=[int(c) for c in rscounts],
+    # STR_SLACK bytes past the received strings: the merge copies endpoints in whole 8-byte words
+    nstr = int(rscounts.sum())
+    out_s = torch.zeros(nstr + STR_SLACK, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out_s[:nstr], strings, output_split_sizes=[int(c) for c in rscounts],
                            input_split_sizes=[int(c) for c in scounts], group=group)
     if out_r.numel():  # endpoint_off (byte 16 of a record) += the source's string base
         base = np.zeros(world, np.int64)
         base[1:] = np.cumsum(rscounts)[:-1]
         src_base = torch.repeat_interleave(torch.tensor(base, device=dev), torch.tensor(rcounts, device=dev))
         words = out_r.view(torch.int64).view(-1, nrec // 8)
-        words[:, 2] += src_base
+        # ~0 = no endpoint bytes (the source's arena was full): left as it is
+        words[:, 2] = torch.where(words[:, 2] == -1, words[:, 2], words[:, 2] + src_base)
     return out_r, out_s
 
 
@@ -244,6 +248,7 @@ def device_exchange_merge(ctx, device, group=None, map_first=None):
         # the merge carries client counters only: network maps are per context
         raise ValueError("device_exchange_merge: contexts with network counters are not merged across GPUs")
     world = dist.get_world_size(group)
+    check_same_hash_key(ctx, device, group)
     recs, strs, counts, scounts = ctx.export_services_device(world, device)
     if map_first is not None and recs.numel():
         words = recs.view(torch_int64()).view(-1, REC.itemsize // 8)
@@ -252,6 +257,19 @@ def device_exchange_merge(ctx, device, group=None, map_first=None):
     ctx.clear()
     ctx.merge_services_device(out_r, out_s)
     return int(counts.sum()), out_r.numel() // REC.itemsize
+
+
+def check_same_hash_key(ctx, device, group=None):
+    """Owners are key_lo mod world: a rank keyed with another secret would send the same
+    (pid, endpoint) to another owner and the merged table would hold it twice.  Raises unless
+    every rank's context uses the same service-key secret."""
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor(np.array(ctx.hash_key, np.uint64).view(np.int64), device=device)
+    parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, mine, group=group)
+    if any(not torch.equal(p, mine) for p in parts):
+        raise ValueError("device_exchange_merge: ranks key services with different secrets (pass one hash_key)")
 
 
 def torch_int64():

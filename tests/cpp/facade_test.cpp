@@ -1,0 +1,232 @@
+// facade_test.cpp — INTEGRATION.md's C++ call sites compiled against include/ebpf_discovery_amd.hpp
+// and libebd_amd.so (built by tests/cpp/Makefile; run by tests/test_cpp_facade.py).
+//
+//   facade_test cpu   no GPU: the batch packing, and the facade's error path (ebd_ctx_create
+//                     fails, the constructor throws ebdamd::Error, Discovery.cpp:42-46 style)
+//   facade_test gpu   the Discovery poll loop over an in-memory EventSource on cuda:0:
+//                     config 1 (35-B and 31-B payloads), a saved session that
+//                     goes INVALID (bpfDiscoveryDeleteSession, Discovery.cpp:125-129), the
+//                     report and clear of outputServicesToStdout (Discovery.cpp:60-71) and the
+//                     network counters with an overridden getCurrentTime (AggregatorTest.cpp:41-46)
+// Prints "ok" and exits 0 when every check passes.
+#include "ebpf_discovery_amd.hpp"
+
+#include <cstdio>
+#include <deque>
+#include <map>
+#include <sstream>
+#include <tuple>
+
+namespace {
+
+int failures = 0;
+#define CHECK(cond)                                                          \
+	do {                                                                     \
+		if (!(cond)) {                                                       \
+			std::fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #cond); \
+			failures++;                                                      \
+		}                                                                    \
+	} while (0)
+
+ebd_discovery_event make_event(uint32_t pid, uint32_t fd, uint32_t sid, uint32_t seq, uint8_t flags, uint8_t src0 = 127,
+		uint8_t src3 = 1) {
+	ebd_discovery_event e{};
+	e.pid = pid;
+	e.fd = fd;
+	e.sessionID = sid;
+	e.bufferSeq = seq;
+	e.sourceIP[0] = src0;
+	e.sourceIP[3] = src3;
+	e.flags = flags;
+	return e;
+}
+
+// The BPF queue and savedBuffersMap in memory (DiscoveryBpf.h).
+class MemorySource : public ebdamd::EventSource {
+public:
+	using Key = std::tuple<uint32_t, uint32_t, uint32_t, uint32_t>;
+	void push(const ebd_discovery_event& e, const std::string* data) {
+		queue.push_back(e);
+		if (data)
+			saved[Key{e.pid, e.fd, e.sessionID, e.bufferSeq}] = std::vector<uint8_t>(data->begin(), data->end());
+	}
+	int popEvent(ebd_discovery_event& ev) override {
+		if (queue.empty())
+			return -ENOENT;
+		ev = queue.front();
+		queue.pop_front();
+		return 0;
+	}
+	bool takeSavedBuffer(const ebd_discovery_event& ev, std::vector<uint8_t>& data) override {
+		auto it = saved.find(Key{ev.pid, ev.fd, ev.sessionID, ev.bufferSeq});
+		if (it == saved.end())
+			return false;
+		data = std::move(it->second);
+		saved.erase(it);
+		return true;
+	}
+	void deleteTrackedSession(uint32_t pid, uint32_t fd, uint32_t sid) override { deleted.push_back(Key{pid, fd, sid, 0}); }
+
+	std::deque<ebd_discovery_event> queue;
+	std::map<Key, std::vector<uint8_t>> saved;
+	std::vector<Key> deleted;
+};
+
+constexpr uint8_t kV4New = EBD_FLAG_SESSION_IPV4 | EBD_FLAG_SESSION_UNENCRYPTED_HTTP | EBD_FLAG_EVENT_NEW_DATA;
+
+int run_cpu() {
+	ebdamd::EventBatch b;
+	const std::string req = "GET / HTTP/1.1\r\nHost: h\r\n\r\n";
+	b.add(make_event(1, 5, 1, 1, kV4New), req.data(), (uint32_t)req.size());
+	b.add(make_event(1, 5, 2, 1, kV4New), nullptr, 0);
+	b.add(make_event(1, 5, 3, 1, EBD_FLAG_EVENT_DATA_END), nullptr, 0);
+	b.add(make_event(1, 5, 4, 1, kV4New), req.data(), 10);
+	CHECK(b.size() == 4);
+	CHECK(b.lengths()[0] == req.size() && b.lengths()[1] == EBD_NO_BUFFER && b.lengths()[2] == EBD_NO_BUFFER);
+	CHECK(b.offsets()[3] == req.size() && b.lengths()[3] == 10);
+	CHECK(b.payloadBytes() == req.size() + 10);
+	CHECK(std::memcmp(b.payload() + req.size(), req.data(), 10) == 0);
+	// no GPU: the context cannot be created, and the facade throws where the reference does
+	bool threw = false;
+	try {
+		ebdamd::Aggregator agg(ebdamd::IpInterfaces{}, false);
+	} catch (const ebdamd::Error& e) {
+		threw = e.code() < 0;
+	}
+	CHECK(threw);
+	MemorySource src;
+	threw = false;
+	try {
+		ebdamd::Discovery d(src, true);
+	} catch (const ebdamd::Error&) {
+		threw = true;
+	}
+	CHECK(threw);
+	return 0;
+}
+
+class ClockedAggregator : public ebdamd::Aggregator {
+public:
+	using ebdamd::Aggregator::Aggregator;
+	uint64_t now = 1000000000000ull;
+
+protected:
+	uint64_t getCurrentTime() const override { return now; }
+};
+
+int run_gpu() {
+	// config 1: 1000 x the 35-byte GET, one connection per event
+	{
+		MemorySource src;
+		const std::string req = "GET / HTTP/1.1\r\nHost: 127.0.0.1\r\n\r\n";
+		for (uint32_t i = 0; i < 1000; i++)
+			src.push(make_event(1000, 5, i + 1, 1, kV4New), &req);
+		ebdamd::Options opt;
+		opt.maxEvents = 256; // four hand-overs in one poll cycle
+		opt.maxPayload = 1 << 20;
+		ebdamd::Discovery d(src, false, ebdamd::IpInterfaces{}, opt);
+		d.init();
+		CHECK(d.fetchAndHandleEvents() == 0);
+		const auto svc = d.aggregator().collectServices();
+		CHECK(svc.size() == 1);
+		if (svc.size() == 1) {
+			ebdamd::Service want;
+			want.pid = 1000;
+			want.endpoint = "127.0.0.1/";
+			want.domain = "127.0.0.1";
+			want.scheme = "http";
+			want.internalClientsNumber = 1000;
+			CHECK(svc[0] == want);
+		}
+		std::ostringstream out;
+		d.outputServicesToStdout(out);
+		CHECK(out.str() == "{\"service\":[{\"pid\":1000,\"endpoint\":\"127.0.0.1/\",\"domain\":\"127.0.0.1\",\"scheme\":\"http\","
+						   "\"internalClientsNumber\":1000,\"externalClientsNumber\":0}]}\n");
+		CHECK(d.aggregator().collectServices().empty()); // cleared after the report
+		std::ostringstream none;
+		d.outputServicesToStdout(none);
+		CHECK(none.str().empty());
+	}
+	// the 31-byte variant never finishes: no service, 1000 saved sessions
+	{
+		MemorySource src;
+		const std::string req = "GET / HTTP/1.1\r\nHost: 127.0.0.1";
+		for (uint32_t i = 0; i < 1000; i++)
+			src.push(make_event(1000, 5, i + 1, 1, kV4New), &req);
+		ebdamd::Discovery d(src, false);
+		CHECK(d.fetchAndHandleEvents() == 0);
+		CHECK(d.aggregator().collectServices().empty());
+		CHECK(d.aggregator().stats().live_sessions == 1000);
+	}
+	// a saved session whose next buffer is invalid: the kernel session is deleted once; a
+	// fragmented request across two poll cycles; a missing buffer and a DATA_END event
+	{
+		MemorySource src;
+		const std::string a = "GET /x HTTP/1.1\r\nHo", bad = "st\x01 h\r\n\r\n", f1 = "POST /y HTTP/1.1\r\nHost: ", f2 = "z\r\n\r\n";
+		src.push(make_event(7, 9, 1, 1, kV4New), &a);
+		src.push(make_event(7, 9, 2, 1, kV4New), &f1);
+		src.push(make_event(7, 9, 3, 1, kV4New), nullptr); // saved buffer missing
+		ebdamd::Discovery d(src, false);
+		CHECK(d.fetchAndHandleEvents() == 0);
+		CHECK(src.deleted.empty());
+		src.push(make_event(7, 9, 1, 2, kV4New), &bad);
+		src.push(make_event(7, 9, 2, 2, kV4New), &f2);
+		src.push(make_event(7, 9, 2, 2, EBD_FLAG_EVENT_DATA_END), nullptr);
+		CHECK(d.fetchAndHandleEvents() == 0);
+		CHECK(src.deleted.size() == 1 && src.deleted[0] == (MemorySource::Key{7, 9, 1, 0}));
+		const auto svc = d.aggregator().collectServices();
+		CHECK(svc.size() == 1 && svc[0].endpoint == "z/y" && svc[0].internalClientsNumber == 1);
+		CHECK(d.aggregator().stats().live_sessions == 0);
+	}
+	// network counters with the clock overridden (AggregatorMock, AggregatorTest.cpp:41-46)
+	{
+		ClockedAggregator agg(ebdamd::IpInterfaces{}, true);
+		ebdamd::EventBatch b;
+		const char* clients[] = {"8.8.8.8", "8.8.9.9", "1.2.3.4", "2001:db8:1::5"};
+		std::vector<std::string> bufs;
+		for (const char* c : clients)
+			bufs.push_back(std::string("GET /n HTTP/1.1\r\nHost: svc\r\nX-Forwarded-For: ") + c + "\r\n\r\n");
+		for (uint32_t i = 0; i < bufs.size(); i++)
+			b.add(make_event(50, 3, i + 1, 1, kV4New), bufs[i].data(), (uint32_t)bufs[i].size());
+		CHECK(agg.newEvents(b) == 0);
+		auto svc = agg.collectServices();
+		CHECK(svc.size() == 1);
+		if (svc.size() == 1) {
+			CHECK(svc[0].externalClientsNumber == 4);
+			CHECK(svc[0].externalIPv4_16ClientNets == 2 && svc[0].externalIPv4_24ClientNets == 3 &&
+					svc[0].externalIPv6ClientsNets == 1);
+		}
+		agg.now += 59ull * 60 * 1000000000ull;
+		agg.networkCountersCleaning();
+		CHECK(agg.collectServices()[0].externalIPv4_24ClientNets == 3);
+		agg.now += 60ull * 1000000000ull;
+		agg.networkCountersCleaning();
+		svc = agg.collectServices();
+		CHECK(svc.size() == 1 && svc[0].externalIPv4_16ClientNets == 0 && svc[0].externalIPv6ClientsNets == 0);
+		agg.clear();
+		CHECK(agg.collectServices().empty());
+		CHECK(agg.stats().errors == 0);
+	}
+	return 0;
+}
+
+} // namespace
+
+int main(int argc, char** argv) {
+	const std::string mode = argc > 1 ? argv[1] : "cpu";
+	try {
+		if (mode == "gpu")
+			run_gpu();
+		else
+			run_cpu();
+	} catch (const std::exception& e) {
+		std::fprintf(stderr, "exception: %s\n", e.what());
+		return 2;
+	}
+	if (failures) {
+		std::fprintf(stderr, "%d checks failed\n", failures);
+		return 1;
+	}
+	std::printf("ok\n");
+	return 0;
+}

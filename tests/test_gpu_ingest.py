@@ -106,3 +106,24 @@ def test_device_submit_returns_before_aggregation_finishes():
         ref.submit(ev, lens, offs, payload)
     assert ctx.services() == ref.services()
     assert comparable(ctx.results()) == comparable(ref.results())
+
+
+def test_tickets_submitted_out_of_order():
+    """Stage A, stage B, submit B, then stage C: the slot A still holds is skipped and C goes
+    into the free one; submitting A and C afterwards gives every batch's services."""
+    parts = [ebd.generate_host(3, 3, k * 1000, 1000) for k in range(3)]
+    ctx = ebd.Context(max_events=1000, max_payload=max(p[3].size for p in parts))
+    ta = ctx.stage(*parts[0])
+    tb = ctx.stage(*parts[1])
+    ctx.submit_staged(tb)
+    tc = ctx.stage(*parts[2])
+    ctx.submit_staged(ta)
+    ctx.submit_staged(tc)
+    ctx.sync()
+    o = O.Oracle()
+    for k in (1, 0, 2):
+        o.process(*parts[k])
+    assert ctx.stats()["errors"] == 0
+    got = [(g[0], g[1], g[4], g[5]) for g in ctx.services()]
+    want = [(w[0], w[1], w[4], w[5]) for w in o.services()]  # counters; first arrival is batch order
+    assert got == want

@@ -173,3 +173,34 @@ def test_report_json_config3_matches_oracle_without_network_counters():
     text = ctx.report_json()
     assert json_objects(text) == json_objects(o.services_json())
     assert len(json_objects(text)) == len(o.services())
+
+
+def test_v6_dictionary_does_not_fill_across_cleanings_and_clears():
+    """The IPv6 /48 prefix dictionary only holds prefixes of live map entries:
+    far more distinct external v6 prefixes than net_capacity, cycled through batches an hour
+    apart with cleanings (which rebuild the half-full tables) and clears, never fill it, and
+    every batch's maps equal the oracle's."""
+    cap = 1 << 10
+    ctx = ebd.Context(max_events=600, max_payload=1 << 16, network_counters=True, net_capacity=cap)
+    o = O.Oracle(network_counters=True)
+    for k in range(12):
+        bufs, rows = [], []
+        for j in range(300):  # 300 fresh /48 prefixes per batch, 12 x 300 > 1024 in all
+            bufs.append(http("h", f"/p{j % 3}", f"2001:db8:{k:x}{j:03x}::1"))
+            rows.append(dict(pid=100, sid=k * 1000 + j + 1, flags=ebd.FLAG_IPV6 | ebd.FLAG_UNENCRYPTED | ebd.FLAG_NEW_DATA))
+        lens, offs, payload = T.pack(bufs)
+        ev = T.events(rows)
+        now = T0 + k * 61 * MIN
+        ctx.set_clock(now)
+        o.set_time(now)
+        ctx.submit(ev, lens, offs, payload)
+        o.process(ev, lens, offs, payload)
+        assert ctx.stats()["errors"] == 0, (k, ctx.stats())
+        assert gpu_nets(ctx) == o.nets(), k
+        assert ctx.services(with_nets=True) == o.services_nets(), k
+        ctx.network_counters_cleaning(now + 60 * MIN)  # this batch's prefixes expire
+        o.network_counters_cleaning(now + 60 * MIN)
+        if k % 4 == 3:
+            ctx.clear()
+            o.clear()
+        assert gpu_nets(ctx) == o.nets(), k

@@ -133,3 +133,51 @@ def test_bench_dry_run_spawns_two_gloo_ranks():
     o = O.Oracle()
     o.process(ev, lens, offs, payload)
     assert line["services_merged"] == len(o.services())
+
+
+class _KeyOnly:
+    """Stands in for a Context where only its service-key secret matters."""
+
+    def __init__(self, key):
+        self.hash_key = key
+
+
+def _key_worker(rank, world, port, same, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    try:
+        ctx = _KeyOnly((1, 2) if same or rank == 0 else (1, 3))
+        try:
+            shard.check_same_hash_key(ctx, "cpu")
+            ok = True
+        except ValueError:
+            ok = False
+        # an exported record without endpoint bytes (endpoint_off = ~0: the source arena was
+        # full) keeps ~0 through the exchange; the others are rebased onto the received bytes
+        rec = np.zeros(2, shard.REC)
+        rec["endpoint_off"] = [np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64(0)]
+        rec["endpoint_len"] = [0, 3]
+        strings = np.frombuffer(b"ab%d" % rank, np.uint8).copy()
+        counts = np.array([1, 1], np.uint32) if rank == 0 else np.array([2, 0], np.uint32)
+        scounts = np.array([0, 3], np.uint64) if rank == 0 else np.array([3, 0], np.uint64)
+        r, s = shard.exchange(torch.from_numpy(rec.view(np.uint8).copy()), torch.from_numpy(strings), counts, scounts)
+        got = r.numpy().view(shard.REC)
+        offs = [int(x) for x in got["endpoint_off"]]
+        nb = s.numel()
+        with open(out_path % rank, "w") as f:
+            json.dump({"ok": ok, "offs": offs, "nbytes": nb}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_exchange_checks_hash_keys_and_keeps_missing_endpoints(same, tmp_path):
+    out_path = str(tmp_path / "r%d.json")
+    mp.start_processes(_key_worker, args=(2, _free_port(), same, out_path), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = (json.load(open(out_path % k)) for k in (0, 1))
+    assert r0["ok"] == r1["ok"] == same
+    # rank 0 receives its own first record (no bytes) and rank 1's two (3 bytes at rank 1's base 0)
+    assert r0["offs"] == [0xFFFFFFFFFFFFFFFF, 0xFFFFFFFFFFFFFFFF, 0]
+    assert r1["offs"] == [0]  # rank 0's second record, its 3 bytes at offset 0
+    assert r0["nbytes"] >= 3 + shard.STR_SLACK
