@@ -939,6 +939,8 @@ int ebd_fetch_results_async(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uin
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	*n = c->last_n;
+	if (!out)
+		return 0; // size query
 	if (cap < c->last_n)
 		return -ENOSPC;
 	HIP_TRY(hipSetDevice(c->device));
@@ -957,6 +959,8 @@ int ebd_fetch_results(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t*
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	*n = c->last_n;
+	if (!out)
+		return 0; // size query
 	if (cap < c->last_n)
 		return -ENOSPC;
 	HIP_TRY(hipSetDevice(c->device));
@@ -1618,16 +1622,23 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 		return -EINVAL;
 	static Interfaces ifs;
 	fill_ifs(ifs, v4, n4, v6, n6);
-	ScanRec sr;
-	const uint32_t s = fresh_scan_host(HostTab{t->next}, t->info, buf, len, HostPast{}, sr);
+	const HostMem mem{buf, len};
+	WalkRec wr;
+	const uint32_t s = fresh_walk_host(HostTab{t->next}, t->info, [&](uint32_t k) { return mem.at(k); }, len,
+			[&](uint32_t p) {
+				while (p < len && buf[p] >= 0x20 && buf[p] <= 0x7e)
+					p++;
+				return p;
+			},
+			wr);
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
 	const bool post = len > 0 && buf[0] == 'P';
-	fresh_finalize(HostTab{t->next}, t->info, sr, s, post, HostMem{buf, len}, len, HashKey{hash_key[0], hash_key[1]}, pid, flags, fr);
-	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
+	fresh_finalize(HostTab{t->next}, t->info, wr, s, post, mem, len, HashKey{hash_key[0], hash_key[1]}, pid, flags, fr);
+	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // k_fresh's planner classifies the source address
 		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
-	if (fr.cip) { // what k_agg_fast (cip_classify) does for this event
+	if (fr.cip) { // what k_fresh's finalize does for this event
 		uint32_t tb, te;
 		uint8_t cls;
 		cip_token(ifs, [buf](uint32_t b) { return (uint32_t)buf[b]; }, fr.r.u.span.cip_off, fr.r.consumed, &tb, &te, &cls);

@@ -776,11 +776,11 @@ EBD_HD uint64_t endpoint_piece(uint32_t hl, uint32_t n, uint32_t oo, uint64_t A,
 
 // Block form over E = buffer[hs, hs + hl) + buffer[us, us + ul), reading 8-byte pieces
 // through `ld8(offset)` (any alignment; bytes beyond a span are masked off).  The loads of
-// a group of 8 pieces (64 bytes of E) are all issued before any is used, so an endpoint of
-// up to 64 bytes costs one memory round trip.
-template <typename Ld8>
+// a group of kGroup pieces are all issued before any is used: 8 pieces (64 bytes of E, one
+// memory round trip for most endpoints) from HBM, fewer from LDS, where latency is short and
+// registers are what limits the kernel.
+template <uint32_t kGroup = 8, typename Ld8>
 EBD_HD Hash128 endpoint_key(const HashKey& key, uint32_t pid, uint32_t hs, uint32_t hl, uint32_t us, uint32_t ul, Ld8 ld8) {
-	constexpr uint32_t kGroup = 8;
 	KeyHasher kh;
 	kh.init(key, pid);
 	const uint32_t n = hl + ul;

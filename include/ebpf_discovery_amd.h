@@ -277,7 +277,7 @@ typedef struct ebd_kernel_time {
 int ebd_kernel_times(ebd_ctx* ctx, ebd_kernel_time* out, uint32_t cap, uint32_t* n);
 int ebd_reset_kernel_times(ebd_ctx* ctx);
 
-/* Per-event results of the last batch (host copy), n <= cap. */
+/* Per-event results of the last batch (host copy), n <= cap; out == NULL: *n only. */
 int ebd_fetch_results(ebd_ctx* ctx, ebd_event_result* out, uint32_t cap, uint32_t* n);
 /* The same read back on the context's D2H stream once the batch is done, without blocking
  * (out should be pinned); complete after ebd_sync.  The next batch's kernels wait for it. */
