@@ -42,10 +42,15 @@ WORKLOADS = {
     2: "config2: fixed 64-B GET, single endpoint 10.0.0.1:8080/index.html",
     3: "config3: mixed 32-1024 B GET/POST (mean ~252 B), Zipf(1.1) URLs x 1e5 and hosts x 1e3, 64 pids, "
        "30% client-IP headers, ~1% invalid",
+    4: "config4: 100 M requests (config-3 content, seed 4) each cut into 2-4 recv() events, 1-8 keep-alive requests "
+       "per connection then DATA_END, 4096 connections interleaved (~322 M events, multi-buffer reassembly)",
     5: "config5: N x 125 M mixed-length requests (config-3 distribution, seed 5; 8 GPUs = the 1 B-request trace) "
        "sharded by hash(pid, fd, sessionID) across N GPUs, owner-partitioned RCCL service merge",
 }
-DEFAULT_EVENTS = {1: 1_000_000, 2: 10_000_000, 3: 100_000_000, 5: 125_000_000}
+DEFAULT_EVENTS = {1: 1_000_000, 2: 10_000_000, 3: 100_000_000, 4: 322_000_000, 5: 125_000_000}
+# config 4 is submitted as several poll cycles per step (sessions carried between them): one
+# 322 M-event cycle would need a 322 M-event context (session set, session strings)
+SUB_BATCH = {4: 81_000_000}
 GEN_CHUNK = 1 << 28  # candidate events per device generation call
 
 
@@ -58,6 +63,8 @@ def parse_args():
     ap.add_argument("--events", type=int, default=0, help="events per GPU (default: the config's size)")
     ap.add_argument("--seed", type=int, default=0, help="trace seed (default: the config number)")
     ap.add_argument("--service-capacity", type=int, default=0)
+    ap.add_argument("--sub-batch", type=int, default=0,
+                    help="events per poll cycle (default: the whole batch; config 4: 81 M); a step submits them all")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per thread count (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", choices=("cold", "warm"), default="cold",
@@ -117,7 +124,7 @@ def cpu_baseline(config, seed, budget_s):
     import oracle_py as O
     import ebd
     o = O.Oracle()
-    chunk = 250_000 if config in (3, 5) else 1_000_000
+    chunk = 250_000 if config in (3, 4, 5) else 1_000_000
     done, spent, first = 0, 0.0, 0
     gen = 3 if config == 5 else config
     while spent < budget_s:
@@ -180,8 +187,9 @@ def generate_shard(ctx, cfg, seed, E, world, rank, dev):
     shard_ = (world, rank) if cfg == 5 else (1, 0)
     cand = E * world if cfg == 5 else E
     plan, n_tot, b_tot = [], 0, 0
-    for c0 in range(0, cand, GEN_CHUNK):
-        cn = min(GEN_CHUNK, cand - c0)
+    step = cand if cfg == 4 else GEN_CHUNK  # config 4's positions interleave connections: one call
+    for c0 in range(0, cand, step):
+        cn = min(step, cand - c0)
         k, b = ebd.trace_size_device(ctx, cfg, seed, c0, cn, align=16, shard=shard_, with_events=True)
         plan.append((c0, cn, k, b, n_tot, b_tot))
         n_tot += k
@@ -229,20 +237,28 @@ def main():
         torch.distributed.broadcast(kt_, 0)
         key = kt_.cpu().numpy().view(np.uint64)
     cap = int(E * 1.15) if cfg == 5 else E
-    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(cap, 1) * 0.8)))))
-    ctx = ebd.Context(max_events=cap, device=local, service_capacity=svc_cap, string_arena=max(256 << 20, cap * 48),
-                      timing=True, hash_key=(int(key[0]), int(key[1])))
+    sub = args.sub_batch or SUB_BATCH.get(cfg, 0) or cap
+    reqs = cap / 3.2 if cfg == 4 else cap  # requests, not events, create services
+    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(reqs, 1) * 0.8)))))
+    ctx = ebd.Context(max_events=min(cap, sub), device=local, service_capacity=svc_cap,
+                      string_arena=max(256 << 20, int(reqs) * 48), timing=True, hash_key=(int(key[0]), int(key[1])))
     t0 = time.perf_counter()
     ev_t, len_t, off_t, pay_t, gidx_t, n, size = generate_shard(ctx, cfg, seed, E, world, rank, dev)
     log(f"[rank {rank}] generated {n} events, {size / 1e9:.2f} GB payload in {time.perf_counter() - t0:.1f} s")
     G = E * world if cfg == 5 else E  # trace positions per step (candidates)
 
-    def step(k, cold):
+    cuts = list(range(0, n, sub)) + [n]
+
+    def step(k, cold, each=None):
         if cold:
             ctx.clear()  # Aggregator::clear after the previous interval's report (Aggregator.cpp:136-153)
         # global trace order: step k's event i is at k * G + its position in the trace
         ctx.set_seq_base(k * G if cfg == 5 else k * world * G + rank * G)
-        ctx.submit_device(ev_t, len_t, off_t, pay_t, n)
+        for a, z in zip(cuts[:-1], cuts[1:]):  # poll cycles of the batch, sessions carried between them
+            ctx.submit_device(ev_t[a * 36:], len_t[a:], off_t[a:], pay_t, z - a)
+            if each is not None:
+                ctx.sync()
+                each(a, z)
 
     def timed_steps(k0, cold):
         if world > 1:
@@ -270,7 +286,6 @@ def main():
     elapsed = timed_steps(args.warmup, cold)
     kt = ctx.kernel_times()
     st = ctx.stats()
-    res = ctx.results()  # of the last timed batch
     # the other mode, reported beside (same batch, same number of steps)
     other_mode = "warm" if cold else "cold"
     ctx.reset_kernel_times()
@@ -278,11 +293,28 @@ def main():
     other_elapsed = timed_steps(k_other, not cold)
     other_kt = ctx.kernel_times()
 
-    # algorithmic bytes of one batch: sum(consumed + 40) per data event
-    data_events = int((res["status"] != ebd.STATUS_NONE).sum())
-    alg_bytes = int(res["consumed"].astype(np.uint64).sum()) + 40 * data_events
-    fresh_launches, fresh_ms = kt["k_fresh"]
-    fresh_avg_ms = fresh_ms / max(fresh_launches, 1)
+    # algorithmic bytes of one batch: consumed + 40 B per data event (36-B
+    # DiscoveryEvent + 4-B length), 36 B per close-only event; one more step, untimed, reads the
+    # results of every poll cycle
+    acc = {"consumed": 0, "data": 0, "close": 0}
+    flags_all = ev_t[:n * 36].view(-1, 36)[:, 32].cpu().numpy()
+
+    def tally(a, z):
+        r = ctx.results()
+        acc["consumed"] += int(r["consumed"].astype(np.uint64).sum())
+        f = flags_all[a:z]
+        acc["data"] += int(((f & ebd.FLAG_NEW_DATA) != 0).sum())
+        acc["close"] += int(((f & ebd.FLAG_NEW_DATA) == 0).sum())
+
+    step(k_other + args.steps, cold, each=tally)
+    ctx.sync()
+    alg_bytes = acc["consumed"] + 40 * acc["data"] + 36 * acc["close"]
+    # the roofline's kernel: k_fresh (configs 1-3, 5), or for config 4 the kernel with the most
+    # time per step (the session walk), timed over all its launches in one step
+    per_step = {k: v[1] / args.steps for k, v in kt.items() if v[0]}
+    top = max(per_step, key=per_step.get) if cfg == 4 else "k_fresh"
+    fresh_launches, fresh_ms = kt[top]
+    fresh_avg_ms = per_step[top] if cfg == 4 else fresh_ms / max(fresh_launches, 1)
     achieved = alg_bytes / (fresh_avg_ms / 1e3) / 1e9
     traffic = None
     if world == 1 and os.path.exists(args.pmc):
@@ -344,13 +376,16 @@ def main():
         "dtype": "u8",
         "data": "synthetic: Philox-seeded trace generated in HBM (bit-identical to the host generator)",
         "config": {"workload": WORKLOADS[cfg], "config": cfg, "events_per_gpu": n, "seed": seed,
-                   "payload_bytes_per_gpu": size, "step_mode": args.mode,
+                   "payload_bytes_per_gpu": size, "step_mode": args.mode, "poll_cycles_per_step": len(cuts) - 1,
                    "parallelism": (f"{world} shards by hash(pid, fd, sessionID), RCCL owner merge" if world > 1
                                    else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_fresh", "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes,
-                     "alg_bytes_def": "sum(consumed) + 40 B per data event (36-B DiscoveryEvent + 4-B length)"},
+                     "kernel": top, "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_def": "sum(consumed) + 40 B per data event (36-B DiscoveryEvent + 4-B length) + 36 B per "
+                                      "close-only event" + (" (kernel time: all its launches in one step of %d poll "
+                                                             "cycles)" % (len(cuts) - 1) if cfg == 4 else "")},
+        "step_roofline_frac": alg_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
         "cpu_baseline": cpu,
         "step_gbps_alg": alg_bytes * world * args.steps / elapsed / 1e9,
         "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items() if v[0]},

@@ -1205,6 +1205,13 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_service* recs, uint32_t n, c
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
+	if (n > c->verify_cap) { // every merged record may race a claim: room to verify each
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		HIP_TRY(hipFree(c->d_verify));
+		c->d_verify = nullptr;
+		HIP_TRY(hipMalloc(&c->d_verify, (size_t)n * sizeof(VerifyRec)));
+		c->verify_cap = n;
+	}
 	Dev d = make_dev(c);
 	d.n = 0;
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));

@@ -343,10 +343,19 @@ constexpr int kLoadWaves = EBD_FRESH_LOADERS;
 constexpr int kWalkWaves = EBD_FRESH_WALKERS;
 constexpr int kFinWaves = kFreshWaves - 1 - kLoadWaves - kWalkWaves;
 static_assert(kFinWaves >= 1, "k_fresh: at least one finalize wave");
-constexpr uint32_t kTile = 16384;  // payload bytes per slot
-constexpr uint32_t kTilePad = 64;  // word / 8-byte reads past a buffer's end stay inside the slot
-constexpr uint32_t kSlots = 6;
-constexpr uint32_t kTileEvents = 128;
+#ifndef EBD_TILE
+#define EBD_TILE 16384
+#endif
+#ifndef EBD_SLOTS
+#define EBD_SLOTS 6
+#endif
+constexpr uint32_t kTile = EBD_TILE; // payload bytes per slot
+constexpr uint32_t kTilePad = 64;    // word / 8-byte reads past a buffer's end stay inside the slot
+constexpr uint32_t kSlots = EBD_SLOTS;
+#ifndef EBD_TILE_EVENTS
+#define EBD_TILE_EVENTS 128
+#endif
+constexpr uint32_t kTileEvents = EBD_TILE_EVENTS;
 constexpr uint32_t kFinRing = 256; // finalize records in flight
 static_assert((kFinRing & (kFinRing - 1)) == 0 && kFinRing >= 128, "ring: a power of two >= 2 x 64");
 // slot state: code | (tile + kSlots) << 2; code 0: free after that tile, 1: planned, 2: ready
@@ -707,7 +716,11 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 						lds_store_rel(&sh.freed[rs], pos + 1); // the ring slot may be written again
 						if (q[R_POS] != pos + 1)
 							set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
+#ifndef EBD_EXP_NOFIN // experiment: records taken, not finalized (results are wrong)
 						else if (finalize_rec(d, sh, q, rb))
+#else
+						else
+#endif
 							tile_event_done(sh, q[R_SLOT] & 0xffu);
 						todo = false;
 					}
@@ -809,10 +822,18 @@ __global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
 					s = di.init;
 					walk_init(di, wr);
 					post = sh.tile[slot][T0] == 'P' ? 1u : 0u;
+#ifdef EBD_EXP_NOWALK // experiment: the tile stream without walks (results are wrong)
+					p = L;
+#endif
 				}
 			}
 		}
 		bool fin = false;
+#ifdef EBD_EXP_NOWALK
+		if (ev != kNone && rdy && p >= L) {
+			fin = true;
+		} else
+#endif
 		if (ev != kNone && rdy) {
 			worked = true;
 			const uint8_t* b = sh.tile[slot] + T0;

@@ -306,19 +306,41 @@ class Oracle:
 
 
 def _throughput_worker(args):
-    config, seed, first, n, budget_s = args
+    config, seed, first, n, budget_s, shard = args
     import ebd
+    from ebd import shard as sh
     o = Oracle()
     done, spent, at = 0, 0.0, first
     chunk = 100_000
     while spent < budget_s:
         ev, lens, offs, payload = ebd.generate_host(config, seed, at, chunk)
+        if shard is not None:  # config 4: this worker's connections (they interleave in the trace)
+            keep = sh.shard_indices(ev, shard[0])[shard[1]].astype(np.int64)
+            ev, lens, offs = ev[keep], lens[keep], offs[keep]
         t = time.perf_counter()
         o.process(ev, lens, offs, payload)
         spent += time.perf_counter() - t
-        done += chunk
+        done += len(ev)
         at += chunk
     return done, spent
+
+
+def host_cpu():
+    """nproc, this process's affinity share and the CPU model of the host."""
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count() or 1, "affinity_share": share, "cpu_model": model}
 
 
 def parallel_throughput(config, seed, budget_s, threads=None):
@@ -329,18 +351,22 @@ def parallel_throughput(config, seed, budget_s, threads=None):
     the slowest worker's busy time.  The per-worker tables would be merged as the GPUs'
     are; the merge is not timed here."""
     import multiprocessing as mp
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    threads = threads or min(16, share)
+    host = host_cpu()
+    threads = threads or min(16, host["affinity_share"])
     if threads < 2:
         return None
     slice_ = 50_000_000
+    if config == 4:  # connections interleave: every worker walks the same trace, keeping its connections
+        jobs = [(config, seed, 0, slice_, budget_s, (threads, k)) for k in range(threads)]
+        how = "its own connections (hash(pid, fd, sessionID) mod workers) of"
+    else:  # one event per connection: index slices are connection shards
+        jobs = [(config, seed, k * slice_, slice_, budget_s, None) for k in range(threads)]
+        how = "its own connection slice of"
     with mp.get_context("fork").Pool(threads) as pool:
-        res = pool.map(_throughput_worker, [(config, seed, k * slice_, slice_, budget_s) for k in range(threads)])
+        res = pool.map(_throughput_worker, jobs)
     done = sum(r[0] for r in res)
     busy = max(r[1] for r in res)
-    return dict(value=done / busy, unit="events/s", cores=threads, kind="port",
-                sample=f"{threads} processes x ~{budget_s:.0f} s, each on its own connection slice of the config-{config} "
-                       f"trace (seed {seed}), {done} events in all")
+    return dict(value=done / busy, unit="events/s", cores=threads, kind="port", host=host,
+                sample=f"{threads} processes x ~{budget_s:.0f} s, each on {how} the config-{config} "
+                       f"trace (seed {seed}), {done} events in all; cores = min(16, affinity share): the GPU box gives "
+                       f"one GPU's job 16 cores")
