@@ -341,17 +341,18 @@ def main():
         torch.distributed.barrier()
         torch.cuda.synchronize()
         tm = time.perf_counter()
-        sent, got = shard.device_exchange_merge(ctx, dev, map_first=map_first)
+        x = shard.device_exchange_merge(ctx, dev, map_first=map_first)
         ctx.sync()
         torch.distributed.barrier()
         merge_ms = (time.perf_counter() - tm) * 1e3
         owned = ctx.stats()["services"]
-        tot = torch.tensor([n, owned, sent, got], dtype=torch.int64, device=dev)
+        tot = torch.tensor([n, owned, x["sent"], x["record_bytes"], x["string_bytes"]], dtype=torch.int64, device=dev)
         torch.distributed.all_reduce(tot)
         mt = torch.tensor([merge_ms], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(mt, op=torch.distributed.ReduceOp.MAX)
         n_all = int(tot[0])
         merge = {"merge_ms": float(mt.item()), "services_merged": int(tot[1]), "records_exchanged": int(tot[2]),
+                 "record_bytes": int(tot[3]), "string_bytes": int(tot[4]), "record_size": shard.REC.itemsize,
                  "table_state": "the last timed step's interval (cold) or all steps (warm)"}
         if rank != 0:
             torch.distributed.destroy_process_group()

@@ -36,7 +36,8 @@ hipError_t launch_publish(const Dev& d, hipStream_t st, int cus);
 uint32_t agg_stage_per_block(uint32_t n, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
 hipError_t launch_collect(const Dev& d, ebd_service* out, hipStream_t st, int cus);
-hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus);
+hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, uint32_t slot_cap,
+		hipStream_t st, int cus);
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
 		uint32_t count, uint32_t index, unsigned long long* alen, uint32_t* keep, hipStream_t st);
 hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n,
@@ -45,10 +46,13 @@ hipError_t launch_gen_write(const GenTables* T, uint32_t config, uint64_t seed, 
 void build_gen_tables(GenTables* T);
 hipError_t launch_owner_count(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cnt,
 		unsigned long long* bytes, hipStream_t st, int cus);
-hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
-		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
-		hipStream_t st, int cus);
-hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
+hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cur,
+		ebd_wire_service* out, unsigned long long* srcoff, hipStream_t st, int cus);
+hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb, hipStream_t st, int cus);
+hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
+		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus);
+hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
+		const unsigned long long* offs, hipStream_t st, int cus);
 hipError_t launch_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt, hipStream_t st);
 hipError_t launch_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
 		const uint32_t* stt, unsigned long long* alen, hipStream_t st);
@@ -216,6 +220,7 @@ static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collec
 		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used"};
 enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_PUBLISH, KT_SSET_CLEAR, KT_VERIFY,
 	KT_CLEAR, KT_N };
+static_assert(KT_N <= 16, "kernel timing slots");
 
 static hipEvent_t take_event(ebd_ctx* c) {
 	if (!c->free_events.empty()) {
@@ -1065,7 +1070,7 @@ static int clear_keep_nets(ebd_ctx* c) {
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_KEEP, 0, 2 * sizeof(unsigned long long), c->stream));
 	Dev d = make_dev(c);
 	HIP_TRY(launch_keep_collect(d, c->d_keep, c->d_kbytes, c->kbytes_cap, c->stream, c->cus));
-	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_keep_insert(d, c->d_keep, (const uint8_t*)c->d_kbytes, c->d_remap, c->stream, c->cus));
@@ -1079,7 +1084,7 @@ int ebd_clear(ebd_ctx* c) {
 	HIP_TRY(hipSetDevice(c->device));
 	if (c->net_on)
 		return clear_keep_nets(c);
-	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	return 0;
@@ -1157,7 +1162,24 @@ int ebd_report_json(ebd_ctx* c, char* out, uint64_t cap, uint64_t* len) {
 	return ebd_format_services_json(svc.data(), n, str.data(), sl, out, cap, len);
 }
 
-int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
+// The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
+// are n entries, the scan's scratch is allocated on the stream.
+static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, unsigned long long* nb, unsigned long long* offs) {
+	hipError_t e = launch_wire_bytes(recs, n, nb, c->stream, c->cus);
+	if (e != hipSuccess)
+		return e;
+	size_t tb = 0;
+	if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nb, offs, (int)n, c->stream)) != hipSuccess)
+		return e;
+	void* tmp = nullptr;
+	if ((e = hipMallocAsync(&tmp, tb + 16, c->stream)) != hipSuccess)
+		return e;
+	e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nb, offs, (int)n, c->stream);
+	const hipError_t f = hipFreeAsync(tmp, c->stream);
+	return e != hipSuccess ? e : f;
+}
+
+int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
 		uint32_t* counts, uint64_t* str_counts) {
 	if (!c || world == 0 || world > 64 || !counts || !str_counts)
 		return -EINVAL;
@@ -1165,32 +1187,36 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, ui
 	HIP_TRY(hipSetDevice(c->device));
 	if (!c->d_collect)
 		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-	unsigned long long* own = nullptr; // cnt, bytes, cur, scur, sbase: world each
-	HIP_TRY(hipMallocAsync((void**)&own, 5 * 64 * sizeof(unsigned long long), c->stream));
+	unsigned long long* own = nullptr; // cnt, bytes, cur: world each
+	HIP_TRY(hipMallocAsync((void**)&own, 3 * 64 * sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(own, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
 	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, own, own + 64, c->stream, c->cus));
-	unsigned long long h[5 * 64];
+	unsigned long long h[3 * 64];
 	HIP_TRY(hipMemcpyAsync(h, own, 2 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	uint64_t total = 0, stotal = 0;
 	for (uint32_t w = 0; w < world; w++) {
 		counts[w] = (uint32_t)h[w];
 		str_counts[w] = h[64 + w];
-		h[128 + w] = total;  // cur
-		h[192 + w] = stotal; // scur
-		h[256 + w] = stotal; // sbase
+		h[128 + w] = total; // cur: the owner's first record
 		total += h[w];
 		stotal += h[64 + w];
 	}
 	int rc = 0;
-	if (recs) {
+	if (recs && total) {
 		if (total > cap || stotal > strcap || !strings) {
 			rc = -ENOSPC;
 		} else {
-			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 3 * 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
-			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, c->d_sarena, own + 128, own + 192, own + 256, recs, strings,
-					c->stream, c->cus));
+			// records by owner, then their bytes at the scan of their sizes: owner w's bytes are
+			// the str_counts[w] after the earlier owners', in its records' order
+			unsigned long long* tmp = nullptr; // srcoff, nb, offs: total each
+			HIP_TRY(hipMallocAsync((void**)&tmp, 3 * total * sizeof(unsigned long long), c->stream));
+			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
+			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, own + 128, recs, tmp, c->stream, c->cus));
+			HIP_TRY(wire_offsets(c, recs, (uint32_t)total, tmp + total, tmp + 2 * total));
+			HIP_TRY(launch_wire_copy(recs, (uint32_t)total, tmp + 2 * total, tmp, c->d_sarena, strings, c->stream, c->cus));
+			HIP_TRY(hipFreeAsync(tmp, c->stream));
 		}
 	}
 	HIP_TRY(hipFreeAsync(own, c->stream));
@@ -1198,7 +1224,7 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_service* recs, ui
 	return rc;
 }
 
-int ebd_merge_services_device(ebd_ctx* c, const ebd_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen) {
+int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen) {
 	if (!c || (n && (!recs || (!strings && strlen))))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
@@ -1214,10 +1240,14 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_service* recs, uint32_t n, c
 	}
 	Dev d = make_dev(c);
 	d.n = 0;
+	unsigned long long* tmp = nullptr; // nb, offs
+	HIP_TRY(hipMallocAsync((void**)&tmp, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_EVICTIONS, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(launch_merge(d, recs, n, strings, c->stream, c->cus));
+	HIP_TRY(launch_merge(d, recs, n, strings, strlen, tmp + n, c->stream, c->cus));
 	HIP_TRY(launch_verify(d, c->stream, c->cus));
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
@@ -1629,23 +1659,16 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 		return -EINVAL;
 	static Interfaces ifs;
 	fill_ifs(ifs, v4, n4, v6, n6);
-	const HostMem mem{buf, len};
-	WalkRec wr;
-	const uint32_t s = fresh_walk_host(HostTab{t->next}, t->info, [&](uint32_t k) { return mem.at(k); }, len,
-			[&](uint32_t p) {
-				while (p < len && buf[p] >= 0x20 && buf[p] <= 0x7e)
-					p++;
-				return p;
-			},
-			wr);
+	ScanRec sr;
+	const uint32_t s = fresh_scan_host(HostTab{t->next}, t->info, buf, len, HostPast{}, sr);
 	FreshResult fr;
 	std::memset(&fr, 0, sizeof(fr));
 	uint8_t zero[16] = {0};
 	const bool post = len > 0 && buf[0] == 'P';
-	fresh_finalize(HostTab{t->next}, t->info, wr, s, post, mem, len, HashKey{hash_key[0], hash_key[1]}, pid, flags, fr);
-	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // k_fresh's planner classifies the source address
+	fresh_finalize(HostTab{t->next}, t->info, sr, s, post, HostMem{buf, len}, len, HashKey{hash_key[0], hash_key[1]}, pid, flags, fr);
+	if (fr.r.status == EBD_STATUS_FINISHED && !fr.cip) // what k_agg_fast does for this event
 		fr.r.info = (uint8_t)(fr.r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
-	if (fr.cip) { // what k_fresh's finalize does for this event
+	if (fr.cip) { // what k_agg_fast (cip_classify) does for this event
 		uint32_t tb, te;
 		uint8_t cls;
 		cip_token(ifs, [buf](uint32_t b) { return (uint32_t)buf[b]; }, fr.r.u.span.cip_off, fr.r.consumed, &tb, &te, &cls);

@@ -136,8 +136,12 @@ GenParser represent(const KeyTrie* t, const AState& a, int variant) {
 void build_lds_image(const DfaTable* t, uint8_t* out) {
 	std::memset(out, 0, kLdsTableBytes);
 	for (uint32_t st = 0; st < kLdsRows; st++)
-		for (uint32_t b = 0; b < kLdsBytes; b++)
+		for (uint32_t b = 0; b < 256; b++)
+#ifdef EBD_STATE_MAJOR
+			out[st * 256 + b] = t->next[st * 256 + b];
+#else
 			out[b * kLdsStride + st] = t->next[st * 256 + b];
+#endif
 }
 
 int build_dfa(const KeyTrie* trie, DfaTable* out) {
@@ -307,11 +311,6 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 	}
 	if (nvl > 2)
 		return -6;
-	// the kernel keeps rows 0..127 and steps every byte >= 0x80 like 0x7f
-	for (uint32_t st = 0; st < in.nstates; st++)
-		for (int b = 0x80; b < 256; b++)
-			if (out->next[st * 256 + b] != out->next[st * 256 + 0x7f])
-				return -7;
 	return 0;
 }
 

@@ -37,17 +37,14 @@ struct DfaTable {
 	uint8_t next[256 * 256]; // next[s * 256 + byte]
 };
 
-// The table as the kernel keeps it in LDS: byte-major, entry (s, b) at b * kLdsStride + s,
-// rows for the bytes 0..127 only.  Every byte >= 0x80 steps like 0x7f (both are outside every
-// byte class, so they lead to INVALID from every live state; ebd_build_dfa checks that the
-// rows agree) and the kernel clamps them to 0x7f.  A step's address is one
-// v_mad_u32_u24(b, kLdsStride, s).  kLdsStride = 196 bytes = 49 dwords, an odd count, so the
-// bank of (s, b) is (17 b + s / 4) mod 32: lanes reading different bytes in one state spread
-// over the banks, and so do lanes in different states on one byte.
+// The table as the kernel keeps it in LDS: byte-major, entry (s, b) at b * kLdsStride + s.
+// A step's address is then one v_mad_u32_u24(b, kLdsStride, s) on the byte as loaded, with
+// no per-byte remapping.  kLdsStride = 196 bytes = 49 dwords, an odd count, so the bank of
+// (s, b) is (17 b + s / 4) mod 32: lanes reading different bytes in one state spread over the
+// banks, and so do lanes in different states on one byte.
 constexpr uint32_t kLdsStride = 196;
 constexpr uint32_t kLdsRows = kLdsStride; // >= nstates (ebd_build_dfa checks)
-constexpr uint32_t kLdsBytes = 128;       // byte rows kept
-constexpr uint32_t kLdsTableBytes = kLdsBytes * kLdsStride;
+constexpr uint32_t kLdsTableBytes = 256 * kLdsStride;
 void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes
 
 void build_key_trie(KeyTrie* t);

@@ -1,31 +1,24 @@
 // ebd_fresh.h — fast path for one event parsed by a fresh parser (Discovery.cpp:141-159
-// handleNewSession), written once for the GPU kernel (k_fresh) and its host emulation.
+// handleNewSession), written once for the GPU kernel and its host emulation.
 //
-// The walk runs the projected DFA (ebd_dfa.h) over the buffer one 4-byte word at a time,
-// word w = bytes [4w, 4w + 4).  The last word may run past the buffer; the walk steps over
-// those bytes too, which only changes states at positions >= L, so a terminal position >= L
-// is an unfinished parse and every other tracked position is < L.
-//
-// Jumps.  In a generic header-value state (vl0 / vl1: the value of a header that is neither
-// Host nor a client-IP key; they step to themselves on every byte in [0x20, 0x7e], checked
-// when the table is built) the parser only waits for the first byte outside [0x20, 0x7e]:
-// the CR that ends the value, or an invalid byte (HttpRequestParser.cpp:304-330).  So when a
-// word starts in such a state, the walk jumps to the word holding the next non-printable
-// byte (the kernel finds it in a bitmap of the tile), or to L when there is none.  No
-// predicate below changes inside a skipped stretch, so every flip still lies in a walked word.
-//
-// Per walked word the walk keeps the word's maximum next state (a state >= hvc0 is a
-// client-IP value state).  Along a fresh parse these predicates of the state are monotone
-// (false ... false, true ... true; ebd_dfa.h phase groups):
+// The byte scan runs the projected DFA (ebd_dfa.h) over the buffer in 16-byte chunks,
+// chunk c = bytes [16c, 16c + 16) of the buffer.  The last chunk may run past the buffer;
+// the scan steps over those bytes too, which only changes states at positions >= L, so a
+// terminal position >= L is an unfinished parse and every other tracked position is < L.
+// Per byte the scan only does the table step and keeps the chunk's maximum next state (a
+// state >= hvc0 is a client-IP value state).  Along a fresh parse these predicates of the
+// state are monotone (false ... false, true ... true; ebd_dfa.h phase groups):
 //   URL   s > url_id                        the URL has ended
 //   HOST  Host seen                          the first Host value byte was consumed
 //   HEND  Host seen and s != HV(host)        the Host value has ended
 //   TERM  FINISHED / INVALID                 parse() returns
-// A tracker keeps the last walked word whose start state still fails its predicate, with that
-// start state; so it names the word in which the predicate flips.  The client-IP value start
-// (first byte whose next state is >= hvc0) is tracked the same way, until a word has reached
-// such a state.  Finalize re-runs the DFA over the tracker's 4 bytes from the stored state:
-// the steps before the flip give the exact position.
+// A tracker keeps the last chunk whose start state still fails its predicate, so it ends
+// up naming the chunk in which the predicate flips, together with the states at the
+// starts of that chunk's four 4-byte quarters.  The client-IP value start (first byte
+// whose next state is >= hvc0) is tracked the same way, with the running maxima after 4, 8
+// and 12 steps, until a chunk has seen such a state.  Finalize picks the quarter in which
+// the predicate flips from those states and re-runs the DFA over its 4 bytes: the steps
+// before the flip give the exact position.
 #pragma once
 
 #include "../../include/ebpf_discovery_amd.h"
@@ -36,14 +29,16 @@ namespace ebd {
 
 constexpr uint32_t kNone = 0xffffffffu;
 
-// A walked word and the state at its start, packed: w | s0 << 16 (w < 2^14: L <= 8192).
-EBD_HD uint32_t wtrk(uint32_t w, uint32_t s0) { return w | (s0 << 16); }
-EBD_HD uint32_t wtrk_w(uint32_t t) { return t & 0xffffu; }
-EBD_HD uint32_t wtrk_s(uint32_t t) { return t >> 16; }
+// The chunk in which a predicate flips, and the states at the starts of its quarters
+// (qs = s0 | s4 << 8 | s8 << 16 | s12 << 24).
+struct Trk {
+	uint32_t c, qs;
+};
 
-struct WalkRec {
-	uint32_t url, host, hend, cip, term; // wtrk; term: the last walked word
-	uint32_t cseen;                      // a client-IP value state was reached (the cip tracker is frozen)
+struct ScanRec {
+	Trk url, host, hend, cip, term; // term: the last chunk scanned
+	uint32_t cqm;                   // cip chunk: running max next state after 4, 8, 12 steps (bytes 0..2)
+	uint32_t cseen;                 // a client-IP value state was reached (the cip tracker is frozen)
 };
 
 enum { RS_URL, RS_HOST, RS_HEND, RS_TERM, RS_CIP };
@@ -62,28 +57,39 @@ EBD_HD bool st_pred(const DfaInfo& di, uint32_t s) {
 		return st_host_seen(di, s) && s != di.hvh;
 	return st_terminal(di, s);
 }
-// a word starting in this state may be jumped over up to the next non-printable byte
-EBD_HD bool st_skips(const DfaInfo& di, uint32_t s) { return s == di.vl0 || s == di.vl1; }
 
-EBD_HD void walk_init(const DfaInfo& di, WalkRec& r) {
-	const uint32_t t = wtrk(0, di.init);
+EBD_HD void rec_init(const DfaInfo& di, ScanRec& r) {
+	const Trk t{0, di.init * 0x01010101u};
 	r.url = r.host = r.hend = r.cip = r.term = t;
+	r.cqm = 0;
 	r.cseen = 0;
 }
 
-// After walked word w with start state s0 and maximum next state m.
-EBD_HD void word_update(const DfaInfo& di, WalkRec& r, uint32_t w, uint32_t s0, uint32_t m) {
-	const uint32_t t = wtrk(w, s0);
+// After chunk c: s0 = its start state, qs = its quarter-start states, qm = running maxima
+// after 4/8/12 steps, m = the chunk's maximum next state.
+EBD_HD void chunk_update(const DfaInfo& di, ScanRec& r, uint32_t c, uint32_t s0, uint32_t qs, uint32_t qm, uint32_t m) {
+	const Trk t{c, qs};
 	r.url = st_pred<RS_URL>(di, s0) ? r.url : t;
 	r.host = st_pred<RS_HOST>(di, s0) ? r.host : t;
 	r.hend = st_pred<RS_HEND>(di, s0) ? r.hend : t;
-	r.cip = r.cseen ? r.cip : t;
+	const bool open = r.cseen == 0;
+	r.cip = open ? t : r.cip;
+	r.cqm = open ? qm : r.cqm;
 	r.cseen |= m >= di.hvc0 ? 1u : 0u;
 	r.term = t;
 }
 
 // Byte k of a packed word.
 EBD_HD uint32_t byte_of(uint32_t w, uint32_t k) { return (w >> (8 * k)) & 0xffu; }
+
+// Quarter of the tracker's chunk in which W's predicate flips (3 when no quarter start
+// after the first satisfies it).
+template <int W>
+EBD_HD uint32_t flip_quarter(const DfaInfo& di, const Trk& t, uint32_t cqm) {
+	if (W == RS_CIP)
+		return byte_of(cqm, 0) >= di.hvc0 ? 0u : byte_of(cqm, 1) >= di.hvc0 ? 1u : byte_of(cqm, 2) >= di.hvc0 ? 2u : 3u;
+	return st_pred<W>(di, byte_of(t.qs, 1)) ? 0u : st_pred<W>(di, byte_of(t.qs, 2)) ? 1u : st_pred<W>(di, byte_of(t.qs, 3)) ? 2u : 3u;
+}
 
 // Steps over the 4 bytes of `w` from state s before W's predicate holds (RS_CIP: before the
 // first step whose next state is >= hvc0); 4 if it never does.
@@ -100,34 +106,34 @@ EBD_HD uint32_t rescan4(const Tab& T, const DfaInfo& di, uint32_t s, uint32_t w)
 	return before;
 }
 
-// Position (in the buffer) of the first byte after which W's predicate holds; word4 = the
-// tracker word's 4 bytes.
+// Position (in the buffer) of the first byte after which W's predicate holds.
 template <int W, typename Tab>
-EBD_HD uint32_t flip_pos(const Tab& T, const DfaInfo& di, uint32_t t, uint32_t word4) {
-	return 4 * wtrk_w(t) + rescan4<W>(T, di, wtrk_s(t), word4);
+EBD_HD uint32_t flip_pos(const Tab& T, const DfaInfo& di, const Trk& t, uint32_t q, uint32_t w4) {
+	return 16 * t.c + 4 * q + rescan4<W>(T, di, byte_of(t.qs, q), w4);
 }
 
-// Host emulation of the device walk.  byte(k): buffer byte k for any k (past L: whatever
-// follows the buffer); next_np(p): the first byte >= p below L outside [0x20, 0x7e], or L.
-template <typename Tab, typename Byte, typename NextNp>
-inline uint32_t fresh_walk_host(const Tab& T, const DfaInfo& di, Byte byte, uint32_t L, NextNp next_np, WalkRec& r) {
-	walk_init(di, r);
-	uint32_t s = di.init, p = 0;
-	while (p < L && !st_terminal(di, s)) {
-		if (st_skips(di, s)) {
-			const uint32_t q = next_np(p);
-			if (q >= L)
-				break; // printable to the end: still waiting for the CR, unfinished
-			p = q & ~3u;
-		}
+// Host emulation of the device scan: the same chunks, and bytes past the buffer taken from
+// `past(k)` (the device reads whatever follows the buffer).
+template <typename Tab, typename Past>
+inline uint32_t fresh_scan_host(const Tab& T, const DfaInfo& di, const uint8_t* p, uint32_t L, Past past, ScanRec& r) {
+	rec_init(di, r);
+	uint32_t s = di.init;
+	const uint32_t nch = (L + 15) / 16;
+	for (uint32_t c = 0; c < nch; c++) {
 		const uint32_t s0 = s;
-		uint32_t m = 0;
-		for (uint32_t k = 0; k < 4; k++) {
-			s = T[(s << 8) | byte(p + k)];
+		uint32_t m = 0, qs = s0, qm = 0;
+		for (uint32_t k = 0; k < 16; k++) {
+			const uint32_t pos = c * 16 + k;
+			s = T[(s << 8) | (pos < L ? p[pos] : past(pos - L))];
 			m = m > s ? m : s;
+			if (k == 3 || k == 7 || k == 11) {
+				qs |= s << (8 * ((k + 1) / 4));
+				qm |= m << (8 * (k / 4));
+			}
 		}
-		word_update(di, r, p >> 2, s0, m);
-		p += 4;
+		chunk_update(di, r, c, s0, qs, qm, m);
+		if (st_terminal(di, s))
+			break;
 	}
 	return s;
 }
@@ -135,31 +141,38 @@ inline uint32_t fresh_walk_host(const Tab& T, const DfaInfo& di, Byte byte, uint
 struct FreshResult {
 	ebd_event_result r;
 	Hash128 key;
-	bool cip;  // client class pending: decided from the client-IP front token (cip_token)
+	bool cip;  // client class pending: decided from the client-IP token (k_agg_fast, cip_classify)
 	bool keyed; // FINISHED: the key over (pid, host + url) is still to be computed
 };
 
-// The 4 buffer bytes each tracker's rescan needs.
+// The flip quarter of every tracker and the 4 buffer bytes a rescan of it needs.
 struct FinLoads {
+	uint32_t qt, qu, qh, qe, qc;
 	uint32_t wt, wu, wh, we, wc;
 };
 
-// Mem supplies ld4(off) (4 bytes at buffer offset off, any alignment) and ld8(off).
+// Mem supplies ld4(off) (4 bytes at buffer offset off, any alignment) and ld8(off); every
+// load is issued before any is used.
 template <typename Mem>
-EBD_HD void fresh_loads(const WalkRec& r, const Mem& mem, FinLoads& f) {
-	f.wt = mem.ld4(4 * wtrk_w(r.term));
-	f.wu = mem.ld4(4 * wtrk_w(r.url));
-	f.wh = mem.ld4(4 * wtrk_w(r.host));
-	f.we = mem.ld4(4 * wtrk_w(r.hend));
-	f.wc = mem.ld4(4 * wtrk_w(r.cip));
+EBD_HD void fresh_loads(const DfaInfo& di, const ScanRec& sr, const Mem& mem, FinLoads& f) {
+	f.qt = flip_quarter<RS_TERM>(di, sr.term, 0);
+	f.qu = flip_quarter<RS_URL>(di, sr.url, 0);
+	f.qh = flip_quarter<RS_HOST>(di, sr.host, 0);
+	f.qe = flip_quarter<RS_HEND>(di, sr.hend, 0);
+	f.qc = flip_quarter<RS_CIP>(di, sr.cip, sr.cqm);
+	f.wt = mem.ld4(16 * sr.term.c + 4 * f.qt);
+	f.wu = mem.ld4(16 * sr.url.c + 4 * f.qu);
+	f.wh = mem.ld4(16 * sr.host.c + 4 * f.qh);
+	f.we = mem.ld4(16 * sr.hend.c + 4 * f.qe);
+	f.wc = mem.ld4(16 * sr.cip.c + 4 * f.qc);
 }
 
-// Turns a walk into the per-event result (the client class is decided after: the client-IP
-// front token if there is one, else the source address).  `post`: the buffer's first byte is
-// 'P'.  flags come from the DiscoveryEvent (Discovery.cpp:136, 157).  A FINISHED result leaves
-// out.keyed set: the key is endpoint_key over its spans; out.cip: cip_off is the raw value start.
+// Turns a scan into the per-event result (the client class is decided later by k_agg_fast:
+// the client-IP front token if there is one, else the source address).  `post`: the
+// buffer's first byte is 'P'.  flags come from the DiscoveryEvent (Discovery.cpp:136, 157).
+// A FINISHED result leaves out.keyed set: the key is endpoint_key over its spans.
 template <typename Tab>
-EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const WalkRec& wr, uint32_t s_final, bool post, const FinLoads& f,
+EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, bool post, const FinLoads& f,
 		uint32_t L, uint8_t flags, FreshResult& out) {
 	ebd_event_result& r = out.r;
 	r.info = 0;
@@ -167,7 +180,7 @@ EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const WalkRec& wr, uint
 	out.key.lo = out.key.hi = 0;
 	out.cip = false;
 	out.keyed = false;
-	const uint32_t consumed = flip_pos<RS_TERM>(T, di, wr.term, f.wt) + 1;
+	const uint32_t consumed = flip_pos<RS_TERM>(T, di, sr.term, f.qt, f.wt) + 1;
 	if (!st_terminal(di, s_final) || consumed > L) {
 		// not terminal, or terminal only past the buffer's last byte: parse() stops at L
 		// (HttpRequestParser.cpp:85-106), unfinished
@@ -176,25 +189,26 @@ EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const WalkRec& wr, uint
 		return;
 	}
 	r.consumed = (uint16_t)consumed;
-	const bool fin = s_final != di.inv, host = s_final == di.fin1, cip = fin && wr.cseen;
+	const bool fin = s_final != di.inv, host = s_final == di.fin1, cip = fin && sr.cseen;
 	if (!fin) {
 		r.status = EBD_STATUS_INVALID;
 		return;
 	}
 	r.status = EBD_STATUS_FINISHED;
 	const uint32_t url_start = post ? 5 : 4;
-	const uint32_t url_len = flip_pos<RS_URL>(T, di, wr.url, f.wu) - url_start;
+	const uint32_t url_len = flip_pos<RS_URL>(T, di, sr.url, f.qu, f.wu) - url_start;
 	uint32_t host_start = 0, host_len = 0;
 	if (host) {
-		host_start = flip_pos<RS_HOST>(T, di, wr.host, f.wh);
-		host_len = flip_pos<RS_HEND>(T, di, wr.hend, f.we) - host_start;
+		host_start = flip_pos<RS_HOST>(T, di, sr.host, f.qh, f.wh);
+		host_len = flip_pos<RS_HEND>(T, di, sr.hend, f.qe, f.we) - host_start;
 	}
 	uint8_t info = (uint8_t)((post ? EBD_INFO_POST : 0) | ((flags & 16) ? EBD_INFO_HTTPS : 0));
 	if (cip) {
-		r.u.span.cip_off = (uint16_t)flip_pos<RS_CIP>(T, di, wr.cip, f.wc); // raw value start
+		// raw value start of the first client-IP header; token and class: k_agg_fast
+		r.u.span.cip_off = (uint16_t)flip_pos<RS_CIP>(T, di, sr.cip, f.qc, f.wc);
 		info |= EBD_INFO_CIP;
 		out.cip = true;
-	} // else the class comes from the source address
+	} // else the class comes from the source address (k_agg_fast reads the event)
 	r.info = info;
 	r.u.span.url_off = (uint16_t)url_start;
 	r.u.span.url_len = (uint16_t)url_len;
@@ -203,17 +217,17 @@ EBD_HD void fresh_spans(const Tab& T, const DfaInfo& di, const WalkRec& wr, uint
 	out.keyed = true;
 }
 
-// The whole finalize for one event but the client class.  pid: the DiscoveryEvent's
-// (Discovery.cpp:136, 157).
+// The whole finalize for one event (the host twin; the device interleaves the steps of
+// several events).  pid: the DiscoveryEvent's (Discovery.cpp:136, 157).
 template <typename Tab, typename Mem>
-EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const WalkRec& wr, uint32_t s_final, bool post, const Mem& mem,
+EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, uint32_t s_final, bool post, const Mem& mem,
 		uint32_t L, const HashKey& key, uint32_t pid, uint8_t flags, FreshResult& out) {
 	FinLoads f;
-	fresh_loads(wr, mem, f);
-	fresh_spans(T, di, wr, s_final, post, f, L, flags, out);
+	fresh_loads(di, sr, mem, f);
+	fresh_spans(T, di, sr, s_final, post, f, L, flags, out);
 	if (out.keyed) {
 		const auto& sp = out.r.u.span;
-		out.key = endpoint_key<2>(key, pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
+		out.key = endpoint_key(key, pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len, [&](uint32_t o) { return mem.ld8(o); });
 	}
 }
 

@@ -300,149 +300,245 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 }
 
 // ---------------------------------------------------------------------------------
-// k_fresh: every NEW_DATA buffer through a fresh parser (Discovery.cpp:141-159
-// handleNewSession): the walk of ebd_fresh.h, the client class and the 128-bit service key.
+// k_fresh: one lane per event, DFA table in LDS, events pulled from a workgroup queue.
 //
-// One workgroup per CU owns a contiguous range of the batch.  The payload of consecutive
-// events is (almost always) one contiguous byte range in HBM, so the workgroup streams it in
-// tiles: a tile is a run of consecutive events whose buffers lie in one 16-KiB window of the
-// payload, copied into an LDS slot by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
-// instruction, fully coalesced, no VGPRs in flight).  The lane-per-event window loads of the
-// previous design capped the stream at ~2.3 TB/s (tools/ubench_mem2.hip) however little
-// work the lanes did; a tile stream has no such cap.  Every later access to the bytes is an
-// LDS access: the walk, the span rescans, the key, the client-IP token.  Waves have roles:
-//   planner (wave 0)   reads len / off / the event records 64 events per round, 4 rounds
-//                      ahead, classifies each source address (Aggregator.cpp:60-66, 85-88),
-//                      cuts the events into tiles and writes each tile's event table
-//   loaders            DMA a planned tile into its slot, then build the slot's bitmap of
-//                      bytes outside [0x20, 0x7e] (SWAR, 16 bytes per lane)
-//   walkers            one lane per event: the DFA over 4-byte words from LDS, jumping over
-//                      generic header values to the next non-printable byte (the bitmap)
-//   finalizers         64 finished walks at a time: spans, key, client-IP token and class,
-//                      results; the last finalized event of a tile frees its slot
-// A slot's life: FREE -> PLANNED (planner) -> READY (loader) -> FREE (when every event of the
-// tile is finished).  Its state word carries the tile number, so a walker whose event lies
-// in a later tile can tell "not loaded yet" from "already done and recycled".
+// Memory layout decides this kernel's speed (tools/ubench_mem2.hip): buffers read a 64-B
+// window at a time, the four lanes of a quad loading 64 contiguous bytes of one member's
+// window per instruction (4 instructions = one window for each member), then a 4x4 block
+// transpose inside the quad (DPP) hands every lane its own window.  Each workgroup owns a
+// contiguous range of the batch and its lanes take the next event from an LDS counter when
+// they finish one, so the chip streams the payload roughly in memory order and no lane waits
+// for a longer neighbour.  The next window is loaded while the current one is scanned; it is
+// predicted as "the same buffer's next window, or the lane's next event's first window", and
+// a buffer that terminates early (POST body, invalid byte) costs one idle window.
+//
+// Chunks are event-relative (chunk c = bytes [16c, 16c + 16) of the buffer, unaligned loads):
+// there is no leading skip.  The last chunk may extend past the buffer; the DFA steps over
+// those bytes too, which can only change states at positions >= L: a terminal position >= L
+// is an unfinished parse (fresh_finalize), and every other tracked position is < L.
+//
+// Per byte: one table step (v_mad_u32_u24 + ds_read_u8) and a running maximum; per chunk:
+// the branch-free crossing trackers of ebd_fresh.h.  A lane that finishes a buffer appends
+// its scan record to the wave's queue in LDS; 64 records are finalized together (rescans,
+// spans, key), so the finalize code always runs on a full wave.
 // ---------------------------------------------------------------------------------
-// The table as k_fresh keeps it in LDS: byte-major rows for bytes 0..127 (a byte >= 0x80 steps
-// like 0x7f: both are invalid everywhere, ebd_dfa.cpp checks it).  Logical index (s << 8) | b.
+// Logical index (s << 8) | b into the LDS image (ebd_dfa.h: byte-major, kLdsStride).
 struct LdsTable {
 	const uint8_t* t;
-	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[min(i & 0xffu, 127u) * kLdsStride + (i >> 8)]; }
+#ifdef EBD_STATE_MAJOR
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
+#else
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i & 0xffu) * kLdsStride + (i >> 8)]; }
+#endif
 };
 
-#ifndef EBD_FRESH_WALKERS
-#define EBD_FRESH_WALKERS 6
+// One 16-byte chunk as 4 little-endian words.
+struct Chunk {
+	uint32_t w[4];
+};
+
+// 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
+__device__ __forceinline__ Chunk gload16(uintptr_t a) {
+	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
+	Chunk c;
+	c.w[0] = v.x;
+	c.w[1] = v.y;
+	c.w[2] = v.z;
+	c.w[3] = v.w;
+	return c;
+}
+
+// Buffer access for fresh_finalize on the device: 4 and 8 bytes at any buffer offset.  Every
+// offset it reads lies within the buffer's last 16-byte chunk, and the payload stays
+// readable EBD_PAYLOAD_PAD bytes past each buffer (ebd_api.hip pads it).
+struct DevMem {
+	const uint8_t* p;
+	__device__ __forceinline__ uint32_t ld4(uint32_t o) const { return *(const __attribute__((address_space(1))) u32a1*)(p + o); }
+	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const { return gload8u(p + o); }
+};
+
+#ifndef EBD_FRESH_THREADS
+#define EBD_FRESH_THREADS 1024
 #endif
-#ifndef EBD_FRESH_LOADERS
-#define EBD_FRESH_LOADERS 2
+#ifndef EBD_FRESH_WGS
+#define EBD_FRESH_WGS 1 // workgroups per CU
 #endif
-constexpr int kFreshThreads = 768; // 12 waves: 3 per SIMD leave 168 VGPRs to the heaviest role (finalize)
+constexpr int kFreshThreads = EBD_FRESH_THREADS;
 constexpr int kFreshWaves = kFreshThreads / 64;
-constexpr int kLoadWaves = EBD_FRESH_LOADERS;
-constexpr int kWalkWaves = EBD_FRESH_WALKERS;
-constexpr int kFinWaves = kFreshWaves - 1 - kLoadWaves - kWalkWaves;
-static_assert(kFinWaves >= 1, "k_fresh: at least one finalize wave");
-#ifndef EBD_TILE
-#define EBD_TILE 16384
+#ifndef EBD_SCAN_WAVES
+#define EBD_SCAN_WAVES 10
 #endif
-#ifndef EBD_SLOTS
-#define EBD_SLOTS 6
+// waves [0, kScanWaves) scan; the others finalize.  Finalize is latency-bound (tracker words
+// and endpoint bytes past the staged 64 B come from HBM): 10 scan + 6 finalize waves beat
+// 12 + 4 (2.74 vs 2.87 ms per 20 M config-3 events) and 11 + 5 or 9 + 7.
+constexpr int kScanWaves = EBD_SCAN_WAVES;
+#ifdef EBD_PREFETCH
+// one wave streams the workgroup's payload into L2 / the Infinity Cache ahead of the scan front
+constexpr int kPfWaves = 1;
+#ifndef EBD_PF_BYTES
+#define EBD_PF_BYTES 65536
 #endif
-constexpr uint32_t kTile = EBD_TILE; // payload bytes per slot
-constexpr uint32_t kTilePad = 64;    // word / 8-byte reads past a buffer's end stay inside the slot
-constexpr uint32_t kSlots = EBD_SLOTS;
-#ifndef EBD_TILE_EVENTS
-#define EBD_TILE_EVENTS 128
+constexpr uint64_t kPfBytes = EBD_PF_BYTES; // distance ahead of the scan front
+#else
+constexpr int kPfWaves = 0;
 #endif
-constexpr uint32_t kTileEvents = EBD_TILE_EVENTS;
-constexpr uint32_t kFinRing = 256; // finalize records in flight
-static_assert((kFinRing & (kFinRing - 1)) == 0 && kFinRing >= 128, "ring: a power of two >= 2 x 64");
-// slot state: code | (tile + kSlots) << 2; code 0: free after that tile, 1: planned, 2: ready
-enum : uint32_t { SL_FREE = 0, SL_PLANNED = 1, SL_READY = 2 };
-__device__ __forceinline__ uint32_t sl_enc(uint32_t code, uint32_t tile) { return code | ((tile + kSlots) << 2); }
-__device__ __forceinline__ int sl_tile(uint32_t st) { return (int)(st >> 2) - (int)kSlots; }
+constexpr int kFinWaves = kFreshWaves - kScanWaves - kPfWaves;
+constexpr uint32_t kScanLanes = kScanWaves * 64, kFinLanes = kFinWaves * 64;
+#ifndef EBD_RING
+#define EBD_RING 128
+#endif
+constexpr uint32_t kRing = EBD_RING; // finalize records in flight per workgroup
+// A push covers up to 64 consecutive positions and a finalize wave frees its 64 only when
+// all are ready: a ring of fewer than 2 x 64 slots can leave a push waiting on a slot whose
+// finalize wave waits on that same push.  Slots are pos & (kRing - 1).
+static_assert(kRing >= 128 && (kRing & (kRing - 1)) == 0, "ring: a power of two of at least 128 slots");
 
-// event kinds in a tile's event table
-enum : uint32_t { EK_PARSE = 0, EK_SKIP = 1, EK_BAD = 2, EK_EMPTY = 3 };
-
-// finalize record: structure of arrays in the ring (a wave's 64 lanes touch 64 consecutive words)
-enum : uint32_t {
-	R_SLOT,  // slot | index in the tile << 8
-	R_EV,    // event (range-relative)
-	R_SF,    // final state | cseen << 8 | post << 9
-	R_URL, R_HOST, R_HEND, R_CIP, R_TERM, // trackers (wtrk)
-	R_POS,   // ring position + 1 (checked by finalize)
-	R_WORDS
-};
-
-struct FreshLds {
-	uint8_t T[kLdsTableBytes]; // first: LDS address = table index
-	uint8_t tile[kSlots][kTile + kTilePad];
-	unsigned long long bm[kSlots][kTile / 64]; // bit b of word j: tile byte 64 j + b is outside [0x20, 0x7e]
-	uint4 evt[kSlots][kTileEvents];            // x: buffer offset in the tile | L << 16, y: pid, z: flags | kind << 8 | class << 12
-	uint32_t ring[R_WORDS * kFinRing];
-	uint32_t ready[kFinRing]; // position + 1 once the slot's record is written
-	uint32_t freed[kFinRing]; // position + 1 once the slot's record is taken
-	unsigned long long sbase[kSlots]; // payload offset of the tile's first byte (16-aligned)
-	uint32_t sst[kSlots], sfirst[kSlots], scnt[kSlots], sspan[kSlots], sdone[kSlots];
-	uint32_t load_next, walk_next, ntiles, plan_done, tail, claim, walk_done;
-	uint32_t abort; // a wait that cannot end: every role leaves (EBD_ERR_INTERNAL), none hangs
-};
-// Every wait in k_fresh is bounded: ~2^22 sleeps (far longer than any batch) end the kernel
-// with EBD_ERR_INTERNAL instead of hanging the GPU on a protocol fault.
-constexpr uint32_t kSpinMax = 1u << 22;
-static_assert(sizeof(FreshLds) <= 160 * 1024, "k_fresh LDS fits one CU");
-static_assert(offsetof(FreshLds, tile) % 16 == 0 && (kTile + kTilePad) % 16 == 0, "tile rows are 16-byte aligned");
-
-__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
-	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
-	__hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+// LDS address of entry (s, byte k of word x): v_bfe (off the state chain) + v_mad_u32_u24.
+__device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t x, int k) {
+#ifdef EBD_STATE_MAJOR // entry (s, b) at s * 256 + b: one v_perm_b32 builds the index
+	return __builtin_amdgcn_perm(s, x, 0x0c0c0400u | (uint32_t)(k & 3));
+#else
+	return __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8) * kLdsStride + s;
+#endif
 }
 
-// One more turn of a wait: false once the wait has lasted too long or another wave gave up.
-__device__ __forceinline__ bool keep_waiting(const Dev& d, FreshLds& sh, uint32_t& spins) {
-	if (++spins > kSpinMax) {
-		set_error(d, EBD_ERR_INTERNAL);
-		lds_store_rel(&sh.abort, 1u);
-		return false;
-	}
-	if (lds_load_acq(&sh.abort))
-		return false;
-	__builtin_amdgcn_s_sleep(2);
-	return true;
-}
-
-// Bytes of w outside [0x20, 0x7e] as 4 bits.  The borrows and carries of the SWAR tests can
-// flag a byte above a flagged one, never below: the lowest flag is always exact, and the walk
-// only ever asks for the first non-printable byte.
-__device__ __forceinline__ uint32_t nonprint4(uint32_t w) {
+// Every byte of w in [0x20, 0x7e] (SWAR: no byte < 0x20, none >= 0x7f; exact tests).
+__device__ __forceinline__ bool printable4(uint32_t w) {
 	const uint32_t lt = (w - 0x20202020u) & ~w & 0x80808080u;
 	const uint32_t ge = ((w + 0x01010101u) | w) & 0x80808080u;
-	return ((((lt | ge) >> 7) * 0x204081u) >> 21) & 0xfu;
+	return (lt | ge) == 0;
 }
 
-// A byte >= 0x80 becomes 0x7f (the table's last row).
-__device__ __forceinline__ uint32_t clamp7f(uint32_t x) {
-	const uint32_t m = x & 0x80808080u;
-	return (x & 0x7f7f7f7fu) | (m - (m >> 7));
+// 16 DFA steps over one chunk: s advances, m = the maximum next state, qs = the states at
+// the quarter starts (s0 | s4 << 8 | s8 << 16 | s12 << 24), qm = running maxima after 4, 8
+// and 12 steps (ebd_fresh.h chunk_update).  With EBD_SKIP, a quarter (one 4-byte word)
+// whose start state is a generic header-value state (di.vl0 / di.vl1: they step to
+// themselves on every byte in [0x20, 0x7e], checked when the table is built) and whose
+// bytes are all in that range leaves the state as it is and the lane skips its 4 table
+// reads.  The skip is exec-masked: the wave still waits for the lanes that step, and the
+// test costs more issue slots than the LDS reads it saves (20 M config-3 events: 2.87 ms
+// without, 2.92 ms with), so it is off by default.
+#ifdef EBD_EXP_DUAL
+#define DUAL_ARG , uint32_t& g_dual
+#define DUAL_PASS , dual
+#else
+#define DUAL_ARG
+#define DUAL_PASS
+#endif
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t vl0, uint32_t vl1, uint32_t& s,
+		uint32_t& m, uint32_t& qs, uint32_t& qm DUAL_ARG) {
+	qs = s;
+	m = 0;
+#pragma unroll
+	for (int q = 0; q < 4; q++) {
+		const uint32_t x = w.w[q];
+#ifdef EBD_SKIP
+		const bool skip = (s == vl0 || s == vl1) && printable4(x);
+#else
+		const bool skip = false;
+#endif
+		if (!skip) {
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+#ifdef EBD_EXP_DUAL // experiment: a second, independent chain over the same bytes (ILP probe)
+				g_dual = T[tab_index(g_dual, x, k)];
+#endif
+#ifndef EBD_EXP_FAKESTEP
+				s = T[tab_index(s, x, k)];
+#else // experiment: a VALU-only step in place of the LDS table read (results are wrong)
+				s = 64u | ((s * 5u + __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8)) & 63u);
+#endif
+#ifndef EBD_EXP_LEAN
+				m = max(m, s);
+#endif
+			}
+		} else {
+			m = max(m, s);
+		}
+#ifndef EBD_EXP_LEAN
+		if (q < 3) {
+			qs |= s << (8 * (q + 1));
+			qm = q == 0 ? m : (qm | (m << (8 * q)));
+		}
+#endif
+	}
+#ifdef EBD_EXP_LEAN // experiment: steps only, no chunk maximum or quarter states (results are wrong)
+	m = s;
+	qm = 0;
+#endif
 }
 
-// An event's bytes in its tile: 4 and 8 bytes at any buffer offset (LDS, no alignment needed).
-struct TileMem {
-	const uint8_t* b; // the buffer's first byte in the slot
-	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
-		const uintptr_t a = (uintptr_t)(b + o);
-		const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-		return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)a & 3u);
-	}
-	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const {
-		return (unsigned long long)ld4(o) | ((unsigned long long)ld4(o + 4) << 32);
-	}
-	__device__ __forceinline__ uint32_t at(uint32_t o) const { return b[o]; }
+// quad_perm DPP: the value of `v` held by quad lane P's pattern
+template <int P>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, P, 0xf, 0xf, true); }
+constexpr int kQX2 = 2 | (3 << 2) | (0 << 4) | (1 << 6); // lane r takes lane r ^ 2
+constexpr int kQX1 = 1 | (0 << 2) | (3 << 4) | (2 << 6); // lane r takes lane r ^ 1
+template <int K>
+__device__ __forceinline__ uint32_t qbcast(uint32_t v) { return qperm<K | (K << 2) | (K << 4) | (K << 6)>(v); }
+template <int K>
+__device__ __forceinline__ unsigned long long qbcast64(unsigned long long v) {
+	return (unsigned long long)qbcast<K>((uint32_t)v) | ((unsigned long long)qbcast<K>((uint32_t)(v >> 32)) << 32);
+}
+
+// 4x4 transpose of 16-B blocks among the 4 lanes of a quad: lane r holds X[k] = piece r of
+// member k's window; afterwards it holds piece k of its own window.
+__device__ __forceinline__ void transpose_quad(Chunk (&X)[4], uint32_t r) {
+	const bool lo2 = r < 2, lo1 = (r & 1) == 0;
+#pragma unroll
+	for (int k = 0; k < 2; k++)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t recv = qperm<kQX2>(lo2 ? X[k + 2].w[d] : X[k].w[d]);
+			X[k + 2].w[d] = lo2 ? recv : X[k + 2].w[d];
+			X[k].w[d] = lo2 ? X[k].w[d] : recv;
+		}
+#pragma unroll
+	for (int k = 0; k < 4; k += 2)
+#pragma unroll
+		for (int d = 0; d < 4; d++) {
+			const uint32_t recv = qperm<kQX1>(lo1 ? X[k + 1].w[d] : X[k].w[d]);
+			X[k + 1].w[d] = lo1 ? recv : X[k + 1].w[d];
+			X[k].w[d] = lo1 ? X[k].w[d] : recv;
+		}
+}
+
+// An event as a lane holds it.  kind: EK_PARSE (a buffer to scan), EK_SKIP (no parse:
+// not NEW_DATA or the saved buffer is missing, Discovery.cpp:99-110), EK_BAD (length or
+// offset out of range), EK_NONE (the workgroup's range is exhausted).
+enum : uint32_t { EK_PARSE = 0, EK_SKIP = 1, EK_BAD = 2, EK_NONE = 3 };
+struct LaneEv {
+	uint32_t idx;
+	uint32_t L;       // buffer length (0 unless EK_PARSE)
+	uint32_t kind;
+	uint32_t pf;      // pid (the DiscoveryEvent's, Discovery.cpp:136, 157)
+	uint32_t flags;
+	const uint8_t* p; // buffer (a harmless valid address unless EK_PARSE)
+	v4u src;          // the session's source address (DiscoverySockSourceIP), classified by finalize
 };
+
+__device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end) {
+	LaneEv e;
+	e.idx = i;
+	if (i >= end) {
+		e.kind = EK_NONE;
+		e.L = 0;
+		e.pf = e.flags = 0;
+		e.p = d.payload;
+		e.src = v4u{0u, 0u, 0u, 0u};
+		return e;
+	}
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint32_t flags = evb[32];
+	e.pf = *(const uint32_t*)evb;
+	e.src = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // 4-byte aligned, beside pid and flags
+	e.flags = flags;
+	const uint32_t L = d.len[i];
+	const uint64_t off = d.off[i];
+	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 40) ? EK_BAD : EK_PARSE;
+	e.L = e.kind == EK_PARSE ? L : 0;
+	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
+	return e;
+}
 
 __device__ __forceinline__ void write_none(const Dev& d, uint32_t i) {
 	ebd_event_result r;
@@ -468,474 +564,479 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 }
 
-// One more event of the slot's tile is finished; the last one frees the slot.
-__device__ __forceinline__ void tile_event_done(FreshLds& sh, uint32_t slot) {
-	const uint32_t st = sh.sst[slot]; // READY(t): stable until this slot's events are all done
-	if (atomicAdd(&sh.sdone[slot], 1u) + 1u == sh.scnt[slot])
-		lds_store_rel(&sh.sst[slot], sl_enc(SL_FREE, (uint32_t)sl_tile(st)));
-}
+// A finished scan waiting for fresh_finalize: 16 words, kept in the ring as 16 arrays of
+// kRing words (structure of arrays), so the 64 lanes of a push or of a finalize wave, which
+// hold consecutive ring positions, touch consecutive words: no LDS bank conflicts (a 64-B
+// record per lane made every access 16-way conflicted).
+enum : uint32_t {
+	R_PLO,  // buffer address bits 0..31
+	R_PHI,  // buffer address bits 32..47 | L << 16
+	R_IDX,  // event index
+	R_PID,
+	R_SF,   // final state | flags << 8 | cseen << 16 | post << 17
+	R_CQM,
+	R_C01,  // url.c | host.c << 16
+	R_C23,  // hend.c | cip.c << 16
+	R_C4,   // term.c
+	R_QS,   // qs[0..4] (url, host, hend, cip, term)
+	R_LIM = R_QS + 5, // staged leading bytes that are valid
+	R_SRC,  // the source address (4 words): finalize classifies it (Aggregator.cpp:60-66, 85-88)
+	R_POS = R_SRC + 4, // ring position + 1 (checked by finalize)
+	R_WORDS
+};
+static_assert(R_WORDS == 20, "finalize record is 20 words");
 
-// The client-IP front token of a finished request and its class, from the value's bytes in
-// LDS (kept out of line: it is the longest code path, and inlined into the finalize it pushed
-// the kernel past 128 VGPRs).
-__device__ __noinline__ uint32_t tile_cip(const Interfaces& ifs, const uint8_t* b, uint32_t cs, uint32_t consumed, uint32_t* tb,
-		uint32_t* te) {
-	uint8_t c8;
-	cip_token(ifs, [b](uint32_t k) { return (uint32_t)b[k]; }, cs, consumed, tb, te, &c8);
-	return c8;
-}
+// Leading buffer bytes a scan lane stages (window 0), carried to finalize in LDS so that it
+// reads the request line and usually the Host header from LDS instead of reloading lines
+// that left L2 while the lane scanned the rest of the buffer.  Rows are structure of
+// arrays too: word j of the row of lane (or slot) l at [j * stride + l], one row of slack.
+#ifndef EBD_NO_STAGING
+constexpr uint32_t kStage = 64, kStageWords = kStage / 4;
+#else // experiment: finalize reads every byte from the buffer (no LDS staging)
+constexpr uint32_t kStage = 0, kStageWords = 1;
+#endif
 
-// The finalize of one walked event (fresh_finalize + the client class), from LDS only.
-__device__ __forceinline__ bool finalize_rec(const Dev& d, FreshLds& sh, const uint32_t (&q)[R_WORDS], uint32_t rb) {
-	const uint32_t slot = q[R_SLOT] & 0xffu, j = q[R_SLOT] >> 8;
-	if (slot >= kSlots || j >= kTileEvents || rb + q[R_EV] >= d.n) {
-		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
-		return false;
+// Buffer bytes for fresh_finalize: offsets [0, lim) from the staged copy (word j at
+// s[j * kFinLanes]), the rest from the buffer in global memory.
+struct StagedMem {
+	const uint8_t* p;
+	const uint32_t* s;
+	uint32_t lim;
+	__device__ __forceinline__ uint32_t lds4(uint32_t o) const {
+		return __builtin_amdgcn_alignbyte(s[((o >> 2) + 1) * kFinLanes], s[(o >> 2) * kFinLanes], o & 3u);
 	}
-	const uint4 e = sh.evt[slot][j];
-	const uint32_t T0 = e.x & 0xffffu, L = e.x >> 16, pid = e.y, flags = e.z & 0xffu, scls = (e.z >> 12) & 3u;
-	const uint32_t i = rb + q[R_EV];
-	const TileMem mem{sh.tile[slot] + T0};
-	WalkRec wr;
-	wr.url = q[R_URL];
-	wr.host = q[R_HOST];
-	wr.hend = q[R_HEND];
-	wr.cip = q[R_CIP];
-	wr.term = q[R_TERM];
-	wr.cseen = (q[R_SF] >> 8) & 1u;
+	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
+		if (o + 4 <= lim)
+			return lds4(o);
+		return *(const __attribute__((address_space(1))) u32a1*)(p + o);
+	}
+	__device__ __forceinline__ unsigned long long ld8(uint32_t o) const {
+		if (o + 8 <= lim)
+			return (unsigned long long)lds4(o) | ((unsigned long long)lds4(o + 4) << 32);
+		return gload8u(p + o);
+	}
+};
+
+__device__ __forceinline__ uint32_t lds_load_acq(const uint32_t* p) {
+	return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(uint32_t* p, uint32_t v) {
+	__hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Workgroup state shared by the scan and finalize waves.
+struct FreshShared {
+	uint32_t ring[R_WORDS * kRing];
+	uint32_t ready[kRing]; // position + 1 once the slot's record is written
+	uint32_t freed[kRing]; // position + 1 once the slot's record is taken
+	uint32_t rdata[(kStageWords + 1) * kRing];      // staged bytes of each slot's record
+	uint32_t stage[kStageWords * kScanLanes];       // a scan lane's current buffer, as scanned
+	uint32_t fstage[(kStageWords + 1) * kFinLanes]; // a finalize lane's record's bytes
+	uint32_t next_ev;   // next event of the workgroup's range
+	uint32_t tail;      // positions handed out to scan lanes
+	uint32_t claim;     // positions handed out to finalize waves
+	uint32_t scan_done; // scan waves that finished
+};
+static_assert(sizeof(FreshShared) + kLdsTableBytes <= 160 * 1024, "k_fresh LDS fits one CU");
+
+// fresh_finalize (ebd_fresh.h) for the record in the lane's registers; the lane's staged
+// bytes are at fs (word j at fs[j * kFinLanes]).
+__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const uint32_t (&q)[R_WORDS], const uint32_t* fs) {
+	const uint8_t* p = (const uint8_t*)(uintptr_t)((unsigned long long)q[R_PLO] | ((unsigned long long)(q[R_PHI] & 0xffffu) << 32));
+	const uint32_t L = q[R_PHI] >> 16;
+	const uint32_t i = q[R_IDX];
+	if (i >= d.n || L > EBD_BUFFER_MAX_DATA_SIZE || (unsigned long long)(p - d.payload) >> 40) {
+		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
+		return;
+	}
+	ScanRec sr;
+	sr.url = Trk{q[R_C01] & 0xffffu, q[R_QS + 0]};
+	sr.host = Trk{q[R_C01] >> 16, q[R_QS + 1]};
+	sr.hend = Trk{q[R_C23] & 0xffffu, q[R_QS + 2]};
+	sr.cip = Trk{q[R_C23] >> 16, q[R_QS + 3]};
+	sr.term = Trk{q[R_C4], q[R_QS + 4]};
+	sr.cqm = q[R_CQM];
+	sr.cseen = (q[R_SF] >> 16) & 1u;
 	FreshResult fr;
-	fresh_finalize(LdsTable{sh.T}, d.di, wr, q[R_SF] & 0xffu, ((q[R_SF] >> 9) & 1u) != 0, mem, L, d.hkey, pid, (uint8_t)flags, fr);
-	ebd_event_result& r = fr.r;
-	if (r.status == EBD_STATUS_FINISHED) {
-		uint32_t cls = scls;
-		if (fr.cip) { // the first client-IP value's front token decides (Aggregator.cpp:50-74)
-			uint32_t tb, te;
-			cls = tile_cip(*d.ifs, mem.b, r.u.span.cip_off, r.consumed, &tb, &te);
-			r.u.span.cip_off = (uint16_t)tb;
-			r.u.span.cip_len = (uint16_t)(te - tb);
-		}
-		r.info = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT));
+	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM]}, L, d.hkey,
+			q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
+	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
-	} else if (r.status == EBD_STATUS_UNFINISHED) {
+		if (!fr.cip) { // the client is the session's source address; a client-IP token is k_agg_fast's
+			uint8_t src[16];
+			__builtin_memcpy(src, &q[R_SRC], 16);
+			fr.r.info = (uint8_t)(fr.r.info | (classify_source(*d.ifs, (uint8_t)(q[R_SF] >> 8), src) << EBD_INFO_CLASS_SHIFT));
+		}
+	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
+#ifdef EBD_EXP_LEAN
+		d.res[i] = fr.r;
+		return;
+#endif
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
 		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
 		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 	}
-	d.res[i] = r;
-	return true;
+	d.res[i] = fr.r;
 }
 
-__global__ __launch_bounds__(kFreshThreads) void k_fresh(Dev d) {
-	__shared__ __attribute__((aligned(16))) FreshLds sh;
-	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// The table first: LDS address = table index, so a step's read needs no base add.
+struct FreshLds {
+	uint8_t T[kLdsTableBytes];
+	FreshShared sh;
+};
+
+__global__ __launch_bounds__(kFreshThreads)
+#if EBD_FRESH_WGS > 1
+__attribute__((amdgpu_waves_per_eu(EBD_FRESH_WGS * kFreshThreads / 256, 8)))
+#endif
+void k_fresh(Dev d) {
+	__shared__ __attribute__((aligned(16))) FreshLds lds;
+	uint8_t* T = lds.T;
+	FreshShared& sh = lds.sh;
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 3;
 	// this workgroup's contiguous share of the batch
 	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
-	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per), nr = re - rb;
+	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per);
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kFreshThreads * 16u)
-		*(uint4*)(sh.T + k) = *(const uint4*)(d.dfa + k);
-	for (uint32_t k = threadIdx.x; k < kFinRing; k += kFreshThreads)
+		*(uint4*)(T + k) = *(const uint4*)(d.dfa + k);
+	for (uint32_t k = threadIdx.x; k < kRing; k += kFreshThreads)
 		sh.ready[k] = sh.freed[k] = 0;
-	if (threadIdx.x < kSlots)
-		sh.sst[threadIdx.x] = sl_enc(SL_FREE, threadIdx.x - kSlots); // "tile slot - kSlots is done"
-	if (threadIdx.x == 0)
-		sh.load_next = sh.walk_next = sh.ntiles = sh.plan_done = sh.tail = sh.claim = sh.walk_done = sh.abort = 0;
+	if (threadIdx.x == 0) {
+		sh.next_ev = rb + kScanLanes * 2;
+		sh.tail = sh.claim = sh.scan_done = 0;
+	}
 	__syncthreads();
 	const DfaInfo& di = d.di;
 
-	if (wave == 0) {
-		// ---- planner ----
-		constexpr uint32_t kAhead = 4; // rounds of 64 events whose metadata is in flight
-		uint32_t mL[kAhead], mPid[kAhead], mFl[kAhead];
-		unsigned long long mOff[kAhead];
-		v4u mSrc[kAhead];
-		auto fetch = [&](uint32_t r, uint32_t k) {
-			const uint32_t i = rb + r * 64 + lane;
-			if (i < re) {
-				const uint8_t* evb = (const uint8_t*)(d.ev + i);
-				mL[k] = d.len[i];
-				mOff[k] = d.off[i];
-				mPid[k] = *(const uint32_t*)evb;
-				mSrc[k] = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // 4-byte aligned
-				mFl[k] = *(const uint32_t*)(evb + 32);
-			}
-		};
-		const uint32_t rounds = (nr + 63) / 64;
-#pragma unroll
-		for (uint32_t k = 0; k < kAhead; k++)
-			fetch(k, k);
-		uint32_t tnum = 0, slot = 0, cnt = 0, first = 0, maxend = 0;
-		bool open = false, has_base = false;
-		unsigned long long A = 0;
-		auto close = [&]() {
-			if (lane == 0) {
-				sh.sbase[slot] = A;
-				sh.sspan[slot] = (maxend + 15u) & ~15u;
-				sh.sfirst[slot] = first;
-				sh.scnt[slot] = cnt;
-				sh.sdone[slot] = 0;
-				lds_store_rel(&sh.sst[slot], sl_enc(SL_PLANNED, tnum));
-			}
-			tnum++;
-			open = false;
-		};
-		for (uint32_t r0 = 0; r0 < rounds; r0 += kAhead) {
-#pragma unroll
-			for (uint32_t k = 0; k < kAhead; k++) {
-				const uint32_t r = r0 + k;
-				if (r >= rounds)
-					break;
-				const uint32_t i = rb + r * 64 + lane;
-				const bool valid = i < re;
-				const uint32_t L = mL[k], flags = mFl[k] & 0xffu;
-				const unsigned long long off = mOff[k];
-				const uint32_t kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP
-						: (L > EBD_BUFFER_MAX_DATA_SIZE || (off >> 40)) ? EK_BAD : L == 0 ? EK_EMPTY : EK_PARSE;
-				const bool hasb = valid && kind == EK_PARSE;
-				uint8_t src[16];
-				__builtin_memcpy(src, &mSrc[k], 16);
-				const uint32_t cls = hasb ? classify_source(*d.ifs, (uint8_t)flags, src) : 0u;
-				const uint32_t nvalid = min(64u, re - (rb + r * 64));
-				const uint4 ent = make_uint4(0u, mPid[k], flags | (kind << 8) | (cls << 12), 0u);
-				if (r + kAhead < rounds)
-					fetch(r + kAhead, k);
-				uint32_t j0 = 0;
-				while (j0 < nvalid) {
-					if (!open) {
-						slot = tnum % kSlots;
-						uint32_t spins = 0;
-						while (lds_load_acq(&sh.sst[slot]) != sl_enc(SL_FREE, tnum - kSlots))
-							if (!keep_waiting(d, sh, spins))
-								return;
-						open = true;
-						has_base = false;
-						cnt = 0;
-						maxend = 0;
-						first = r * 64 + j0;
-					}
-					if (!has_base) {
-						const unsigned long long pb = __ballot(hasb && lane >= j0);
-						if (pb) {
-							A = __shfl(off, __builtin_ctzll(pb), 64) & ~15ull;
-							has_base = true;
-						}
-					}
-					// the longest run of events from j0 that fits the tile
-					const bool fit = !hasb || (has_base && off >= A && off + L + 15ull <= A + kTile);
-					const unsigned long long nf = __ballot(lane >= j0 && lane < nvalid && !fit);
-					uint32_t stop = nf ? (uint32_t)__builtin_ctzll(nf) : nvalid;
-					stop = min(stop, j0 + (kTileEvents - cnt));
-					if (lane >= j0 && lane < stop) {
-						uint4 x = ent;
-						x.x = hasb ? (uint32_t)(off - A) | (L << 16) : 0u;
-						sh.evt[slot][cnt + lane - j0] = x;
-					}
-					uint32_t end = (lane >= j0 && lane < stop && hasb) ? (uint32_t)(off + L - A) : 0u;
-					for (int o = 32; o > 0; o >>= 1)
-						end = max(end, (uint32_t)__shfl_xor((int)end, o, 64));
-					maxend = max(maxend, end);
-					cnt += stop - j0;
-					j0 = stop;
-					if (j0 < nvalid || cnt == kTileEvents)
-						close();
-				}
-			}
-		}
-		if (open && cnt)
-			close();
-		if (lane == 0) {
-			sh.ntiles = tnum;
-			lds_store_rel(&sh.plan_done, 1u);
-		}
-		return;
-	}
-
-	if (wave <= (uint32_t)kLoadWaves) {
-		// ---- loaders ----
-		for (;;) {
-			uint32_t t = 0;
-			if (lane == 0)
-				t = atomicAdd(&sh.load_next, 1u);
-			t = __builtin_amdgcn_readfirstlane(t);
-			const uint32_t slot = t % kSlots;
-			bool have = false;
-			uint32_t spins = 0;
-			for (;;) {
-				if (lds_load_acq(&sh.sst[slot]) == sl_enc(SL_PLANNED, t)) {
-					have = true;
-					break;
-				}
-				if (lds_load_acq(&sh.plan_done) && t >= sh.ntiles)
-					break;
-				if (!keep_waiting(d, sh, spins))
-					break;
-			}
-			if (!have)
+#ifdef EBD_PREFETCH
+	if (wave == kFreshWaves - 1) {
+		// ---- prefetcher: touches every 128-B line of the payload up to kPfBytes past the scan
+		// front (the buffer of the next event the scan lanes will take), 64 lines per load
+		// instruction, 8 instructions per round, so the lanes' window loads hit in L2 / MALL ----
+		const unsigned long long lo = rb < re ? d.off[rb] & ~127ull : 0, hi = rb < re ? d.off[re - 1] + d.len[re - 1] : 0;
+		unsigned long long upto = lo;
+		uint32_t sink = 0;
+		while (upto < hi) {
+			if (lds_load_acq(&sh.scan_done) == (uint32_t)kScanWaves)
 				break;
-			const unsigned long long A = sh.sbase[slot];
-			const uint32_t span = sh.sspan[slot];
-			uint8_t* dst = sh.tile[slot];
-			for (uint32_t k = 0; k * 1024u < span; k++) {
-				const uint32_t o = k * 1024u + lane * 16u;
-				if (o < span)
-					__builtin_amdgcn_global_load_lds((const void*)(d.payload + A + o),
-							(__attribute__((address_space(3))) void*)(dst + k * 1024u), 16, 0, 0);
+			const uint32_t front = min(lds_load_acq(&sh.next_ev), re - 1);
+			const unsigned long long want = min(hi, d.off[front] + kPfBytes);
+			if (upto >= want) {
+				__builtin_amdgcn_s_sleep(8);
+				continue;
 			}
-			asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-			uint16_t* bm16 = (uint16_t*)sh.bm[slot];
-			for (uint32_t j = lane; j * 16u < span; j += 64u) {
-				const uint4 v = *(const uint4*)(dst + 16u * j);
-				bm16[j] = (uint16_t)(nonprint4(v.x) | (nonprint4(v.y) << 4) | (nonprint4(v.z) << 8) | (nonprint4(v.w) << 12));
+			uint32_t acc = 0;
+#pragma unroll
+			for (uint32_t k = 0; k < 8; k++) {
+				const unsigned long long o = upto + k * 8192ull + lane * 128ull;
+				if (o < want)
+					acc ^= *(const volatile uint32_t*)(d.payload + o);
 			}
-			lds_store_rel(&sh.sst[slot], sl_enc(SL_READY, t));
+			sink ^= acc;
+			upto = min(want, upto + 8 * 8192ull);
 		}
+		if (sink == 0x9e3779b9u && d.n == 0xffffffffu) // never: keeps the loads
+			set_error(d, EBD_ERR_INTERNAL);
 		return;
 	}
+#endif
 
-	if (wave >= (uint32_t)(1 + kLoadWaves + kWalkWaves)) {
-		// ---- finalizers: 64 consecutive ring positions per wave, each record as it arrives ----
-		// A wave cannot wait for all 64: the records that would complete its batch may belong
-		// to tiles that are only planned once the slots its own pending records hold are freed.
+	if (wave >= kScanWaves) {
+		// ---- finalize waves: 64 records at a time, in position order ----
+		const uint32_t fl = (wave - kScanWaves) * 64 + lane; // finalize lane
+		uint32_t* fs = sh.fstage + fl;
 		for (;;) {
 			uint32_t c = 0;
 			if (lane == 0)
 				c = atomicAdd(&sh.claim, 64u);
 			c = __builtin_amdgcn_readfirstlane(c);
-			const uint32_t pos = c + lane, rs = pos & (kFinRing - 1);
-			bool todo = true; // this lane's position is still to be finalized (or ruled out)
-			bool any_rec = false;
-			uint32_t spins = 0;
+			const uint32_t pos = c + lane, slot = pos & (kRing - 1);
+			// 0: waiting, 1: the record is ready, 2: the scan ended before this position.
+			// The wave polls as a whole (a uniform loop): one conflict-free LDS read per lane
+			// and one lane reading the scan counters, then a sleep.
+			uint32_t st = 0;
 			for (;;) {
-				const bool rd = todo && lds_load_acq(&sh.ready[rs]) == pos + 1;
-				if (__any(rd)) {
-					if (rd) {
-						uint32_t q[R_WORDS];
-#pragma unroll
-						for (uint32_t f = 0; f < R_WORDS; f++)
-							q[f] = sh.ring[f * kFinRing + rs];
-						lds_store_rel(&sh.freed[rs], pos + 1); // the ring slot may be written again
-						if (q[R_POS] != pos + 1)
-							set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
-#ifndef EBD_EXP_NOFIN // experiment: records taken, not finalized (results are wrong)
-						else if (finalize_rec(d, sh, q, rb))
-#else
-						else
-#endif
-							tile_event_done(sh, q[R_SLOT] & 0xffu);
-						todo = false;
-					}
-					any_rec = true;
-					spins = 0;
-					continue;
-				}
-				if (!__any(todo))
+				if (st == 0 && lds_load_acq(&sh.ready[slot]) == pos + 1)
+					st = 1;
+				if (__all(st != 0))
 					break;
 				uint32_t done = 0, tail = 0;
 				if (lane == 0) {
-					done = lds_load_acq(&sh.walk_done);
+					done = lds_load_acq(&sh.scan_done);
 					tail = lds_load_acq(&sh.tail);
 				}
 				done = __builtin_amdgcn_readfirstlane(done);
 				tail = __builtin_amdgcn_readfirstlane(tail);
-				if (done == (uint32_t)kWalkWaves) { // every position below tail was pushed
-					if (todo && pos >= tail && lds_load_acq(&sh.ready[rs]) != pos + 1)
-						todo = false;
-					if (!__any(todo))
+				if (done == (uint32_t)kScanWaves) { // every position below tail was pushed
+					if (st == 0 && pos >= tail)
+						st = 2;
+					if (__all(st != 0))
 						break;
 				}
-				if (!keep_waiting(d, sh, spins))
-					break;
+				__builtin_amdgcn_s_sleep(4);
 			}
-			if (!any_rec || lds_load_acq(&sh.abort)) // the batch began past the last record
+			if (!__any(st == 1))
 				break;
+			uint32_t q[R_WORDS];
+			if (st == 1) {
+#pragma unroll
+				for (uint32_t f = 0; f < R_WORDS; f++)
+					q[f] = sh.ring[f * kRing + slot];
+#pragma unroll
+				for (uint32_t j = 0; j < kStageWords; j++) // the staged bytes move to this lane's row
+					fs[j * kFinLanes] = sh.rdata[j * kRing + slot];
+				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
+			}
+#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
+			if (st == 1) {
+				if (q[R_POS] != pos + 1)
+					set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
+				else
+					finalize_rec(d, T, q, fs);
+			}
+#endif
 		}
 		return;
 	}
 
-	// ---- walkers: one lane per event ----
-	uint32_t ev = kNone, wt = 0, slot = 0, T0 = 0, L = 0, p = 0, s = di.init, post = 0, j = 0;
-	bool over = false, rdy = false;
-	uint32_t idle = 0;
-	WalkRec wr;
-	walk_init(di, wr);
-	for (;;) {
-		// events for the lanes without one, one LDS atomic per wave
-		const bool need = !over && ev == kNone;
-		const unsigned long long nb = __ballot(need);
-		if (nb) {
-			uint32_t base = 0;
-			if (lane == 0)
-				base = atomicAdd(&sh.walk_next, (uint32_t)__popcll(nb));
-			base = __builtin_amdgcn_readfirstlane(base);
-			if (need) {
-				const uint32_t e = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(nb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nb, 0));
-				if (e < nr) {
-					ev = e;
-					rdy = false;
-				} else {
-					over = true;
-				}
-			}
-		}
-		if (__all(over))
-			break;
-		bool worked = false;
-		// find the event's tile: tiles are numbered in event order
-		if (ev != kNone && !rdy) {
-			for (;;) {
-				slot = wt % kSlots;
-				const uint32_t st = lds_load_acq(&sh.sst[slot]);
-				const int tt = sl_tile(st);
-				if (tt > (int)wt || (tt == (int)wt && (st & 3u) == SL_FREE)) { // tile wt is done: ev is later
-					wt++;
-					continue;
-				}
-				if (tt == (int)wt && (st & 3u) == SL_READY) {
-					if (ev >= sh.sfirst[slot] + sh.scnt[slot]) {
-						wt++;
-						continue;
-					}
-					rdy = true;
-				}
-				break; // rdy, or tile wt is not loaded yet
-			}
-			if (rdy) {
-				worked = true;
-				j = ev - sh.sfirst[slot];
-				const uint4 e = sh.evt[slot][j];
-				const uint32_t kind = (e.z >> 8) & 3u;
-				if (kind != EK_PARSE) {
-					const uint32_t i = rb + ev;
-					if (kind == EK_BAD)
-						set_error(d, EBD_ERR_BAD_INPUT);
-					if (kind == EK_EMPTY)
-						write_empty(d, i);
-					else
-						write_none(d, i);
-					tile_event_done(sh, slot);
-					ev = kNone;
-					rdy = false;
-				} else {
-					T0 = e.x & 0xffffu;
-					L = e.x >> 16;
-					p = 0;
-					s = di.init;
-					walk_init(di, wr);
-					post = sh.tile[slot][T0] == 'P' ? 1u : 0u;
-#ifdef EBD_EXP_NOWALK // experiment: the tile stream without walks (results are wrong)
-					p = L;
+	// ---- scan waves ----
+	const uint32_t sl = wave * 64 + lane; // scan lane
+	uint32_t* stg = sh.stage + sl;        // this lane's staging row (word j at stg[j * kScanLanes])
+	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
+	// the lane's current event (e0) and the next one (e1, whose record arrives early)
+	LaneEv e0 = lane_ev(d, rb + sl, re);
+	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
+	uint32_t w0 = 0; // e0's window to scan next
+	uint32_t s = di.init, live = 0, post = 0;
+#ifdef EBD_EXP_DUAL
+	uint32_t dual = di.init + 1;
 #endif
-				}
-			}
-		}
-		bool fin = false;
-#ifdef EBD_EXP_NOWALK
-		if (ev != kNone && rdy && p >= L) {
-			fin = true;
-		} else
-#endif
-		if (ev != kNone && rdy) {
-			worked = true;
-			const uint8_t* b = sh.tile[slot] + T0;
-			if (st_skips(di, s)) {
-				// jump to the word of the next byte outside [0x20, 0x7e] (none: unfinished at L)
-				const uint32_t x0 = T0 + p, xe = T0 + L;
-				uint32_t J = x0 >> 6;
-				unsigned long long w = sh.bm[slot][J] & (~0ull << (x0 & 63u));
-				while (w == 0 && 64u * (J + 1) < xe)
-					w = sh.bm[slot][++J];
-				const uint32_t qx = w ? 64u * J + (uint32_t)__builtin_ctzll(w) : xe;
-				if (qx >= xe) {
-					p = L;
-					fin = true;
-				} else {
-					p = (qx - T0) & ~3u;
-				}
-			}
-			if (!fin) {
-				const uint32_t x = clamp7f(TileMem{b}.ld4(p));
-				const uint32_t s0 = s;
-				s = sh.T[__builtin_amdgcn_ubfe(x, 0, 8) * kLdsStride + s];
-				uint32_t m = s;
-				s = sh.T[__builtin_amdgcn_ubfe(x, 8, 8) * kLdsStride + s];
-				m = max(m, s);
-				s = sh.T[__builtin_amdgcn_ubfe(x, 16, 8) * kLdsStride + s];
-				m = max(m, s);
-				s = sh.T[(x >> 24) * kLdsStride + s];
-				m = max(m, s);
-				word_update(di, wr, p >> 2, s0, m);
-				p += 4;
-				fin = st_terminal(di, s) || p >= L;
-			}
-		}
-		// hand finished walks to the finalizers
-		const unsigned long long fb = __ballot(fin);
-		if (fb) {
-			uint32_t base = 0;
-			if (lane == 0)
-				base = atomicAdd(&sh.tail, (uint32_t)__popcll(fb));
-			base = __builtin_amdgcn_readfirstlane(base);
-			if (fin) {
-				const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0));
-				const uint32_t rs = pos & (kFinRing - 1);
-				uint32_t spins = 0;
-				if (pos >= kFinRing) // the slot's previous record must have been taken
-					while (lds_load_acq(&sh.freed[rs]) != pos - kFinRing + 1)
-						if (!keep_waiting(d, sh, spins))
-							break;
-				uint32_t t[R_WORDS];
-				t[R_SLOT] = slot | (j << 8);
-				t[R_EV] = ev;
-				t[R_SF] = s | (wr.cseen << 8) | (post << 9);
-				t[R_URL] = wr.url;
-				t[R_HOST] = wr.host;
-				t[R_HEND] = wr.hend;
-				t[R_CIP] = wr.cip;
-				t[R_TERM] = wr.term;
-				t[R_POS] = pos + 1;
+	ScanRec sr;
+	rec_init(di, sr);
+
+	// Hands e0's scan record to the finalize waves when `done`.
+	auto push = [&](bool done) {
+		const unsigned long long b = __ballot(done);
+		if (b == 0)
+			return;
+		uint32_t base = 0;
+		if (lane == 0)
+			base = atomicAdd(&sh.tail, (uint32_t)__popcll(b));
+		base = __builtin_amdgcn_readfirstlane(base);
+		if (done) {
+			const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+			const uint32_t slot = pos & (kRing - 1);
+			if (pos >= kRing) // the slot's previous record must have been taken
+				while (lds_load_acq(&sh.freed[slot]) != pos - kRing + 1)
+					__builtin_amdgcn_s_sleep(1);
+			// staged bytes equal the buffer's up to the scanned windows and the last chunk's end
+			const uint32_t scanned = min(64u * w0, kStage), chunks_end = (e0.L + 15u) & ~15u;
+			const unsigned long long a = (unsigned long long)(uintptr_t)e0.p;
+			uint32_t t[R_WORDS];
+			t[R_PLO] = (uint32_t)a;
+			t[R_PHI] = ((uint32_t)(a >> 32) & 0xffffu) | (e0.L << 16);
+			t[R_IDX] = e0.idx;
+			t[R_PID] = e0.pf;
+			t[R_SF] = s | (e0.flags << 8) | (sr.cseen << 16) | (post << 17);
+			t[R_CQM] = sr.cqm;
+			t[R_C01] = sr.url.c | (sr.host.c << 16);
+			t[R_C23] = sr.hend.c | (sr.cip.c << 16);
+			t[R_C4] = sr.term.c;
+			t[R_QS + 0] = sr.url.qs;
+			t[R_QS + 1] = sr.host.qs;
+			t[R_QS + 2] = sr.hend.qs;
+			t[R_QS + 3] = sr.cip.qs;
+			t[R_QS + 4] = sr.term.qs;
+			t[R_LIM] = min(scanned, chunks_end);
+			t[R_SRC + 0] = e0.src.x;
+			t[R_SRC + 1] = e0.src.y;
+			t[R_SRC + 2] = e0.src.z;
+			t[R_SRC + 3] = e0.src.w;
+			t[R_POS] = pos + 1;
 #pragma unroll
-				for (uint32_t f = 0; f < R_WORDS; f++)
-					sh.ring[f * kFinRing + rs] = t[f];
-				lds_store_rel(&sh.ready[rs], pos + 1);
-				ev = kNone;
-				rdy = false;
-			}
+			for (uint32_t f = 0; f < R_WORDS; f++)
+				sh.ring[f * kRing + slot] = t[f];
+#ifndef EBD_NO_STAGING
+#pragma unroll
+			for (uint32_t j = 0; j < kStageWords; j++)
+				sh.rdata[j * kRing + slot] = stg[j * kScanLanes];
+#endif
+			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
-		if (!__any(worked)) {
-			if (!keep_waiting(d, sh, idle))
+	};
+	// Moves on while e0 needs no scan: such events are resolved here.
+	auto resolve = [&]() {
+		for (;;) {
+			if (e0.kind == EK_SKIP) {
+				write_none(d, e0.idx);
+			} else if (e0.kind == EK_BAD) {
+				set_error(d, EBD_ERR_BAD_INPUT);
+				write_none(d, e0.idx);
+			} else if (e0.kind == EK_PARSE && e0.L == 0) {
+				write_empty(d, e0.idx);
+			} else {
 				break;
-		} else {
-			idle = 0;
+			}
+			e0 = e1;
+			e1 = lane_ev(d, grab(), re);
+		}
+		w0 = 0;
+		s = di.init;
+		post = 0;
+		rec_init(di, sr);
+		live = e0.kind == EK_PARSE ? 1u : 0u;
+	};
+	resolve();
+
+	// The window in flight: (tidx, tw) names what W holds for this lane.
+	auto nwin = [](uint32_t L) { return (L + 63) >> 6; };
+	Chunk W[4];
+	uint32_t tidx, tw;
+	auto issue = [&](const uint8_t* p, uint32_t L, uint32_t w) {
+		// member k's window: pieces p + 16 * min(4w + j, last), j = 0..3; this lane loads piece r
+		const uint32_t last = L ? (L - 1) >> 4 : 0;
+		const unsigned long long a = (unsigned long long)(uintptr_t)p;
+		const uint32_t pc = (w << 2) | (last << 16); // window's first chunk | last chunk
+		unsigned long long ak[4];
+		uint32_t pk[4];
+		ak[0] = qbcast64<0>(a), pk[0] = qbcast<0>(pc);
+		ak[1] = qbcast64<1>(a), pk[1] = qbcast<1>(pc);
+		ak[2] = qbcast64<2>(a), pk[2] = qbcast<2>(pc);
+		ak[3] = qbcast64<3>(a), pk[3] = qbcast<3>(pc);
+#pragma unroll
+		for (int k = 0; k < 4; k++) {
+			const uint32_t c = min((pk[k] & 0xffffu) + r, pk[k] >> 16);
+			W[k] = gload16((uintptr_t)(ak[k] + 16ull * c));
+		}
+	};
+	tidx = e0.idx;
+	tw = 0;
+	issue(e0.p, e0.L, 0);
+
+	while (__any(e0.kind != EK_NONE)) {
+		// is the window in flight the one e0 needs?
+		const bool valid = e0.kind == EK_PARSE && tidx == e0.idx && tw == w0;
+		Chunk X[4] = {W[0], W[1], W[2], W[3]};
+		// predict and load the next window
+		{
+			const uint8_t* np;
+			uint32_t nL, ni, nw;
+			if (!valid) {
+				np = e0.p, nL = e0.L, ni = e0.idx, nw = w0;
+			} else if (w0 + 1 < nwin(e0.L)) {
+				np = e0.p, nL = e0.L, ni = e0.idx, nw = w0 + 1;
+			} else {
+				np = e1.p, nL = e1.L, ni = e1.idx, nw = 0;
+			}
+			issue(np, nL, nw);
+			tidx = ni;
+			tw = nw;
+		}
+		transpose_quad(X, r);
+#ifdef EBD_EXP_XPOSE3 // experiment: two more transposes (an involution: results unchanged), to price one
+		transpose_quad(X, r);
+		transpose_quad(X, r);
+#endif
+		bool done = false;
+		if (valid) {
+			if (w0 == 0) {
+				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
+#ifndef EBD_NO_STAGING
+#pragma unroll
+				for (int k = 0; k < 4; k++) // window 0 into the lane's staging row
+#pragma unroll
+					for (int j = 0; j < 4; j++)
+						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
+#endif
+			}
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				uint32_t sx = s, m, qs, qm;
+#ifndef EBD_EXP_NOSCAN
+				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm DUAL_PASS);
+#else // experiment: the window stream alone, no DFA (results are wrong)
+				sx = (s ^ X[k].w[0] ^ X[k].w[1] ^ X[k].w[2] ^ X[k].w[3]) & 63u;
+				m = qs = qm = sx;
+#endif
+				if (live) {
+					const uint32_t c = 4 * w0 + k;
+#ifndef EBD_EXP_NOTRACK // experiment: no crossing trackers (results are wrong)
+#ifndef EBD_EXP_LEAN
+					chunk_update(di, sr, c, s, qs, qm, m);
+#else // one select per tracker of (chunk | start state << 16)
+					{
+						const uint32_t pk = c | (s << 16);
+						sr.url.c = st_pred<RS_URL>(di, s) ? sr.url.c : pk;
+						sr.host.c = st_pred<RS_HOST>(di, s) ? sr.host.c : pk;
+						sr.hend.c = st_pred<RS_HEND>(di, s) ? sr.hend.c : pk;
+						sr.cip.c = sr.cseen ? sr.cip.c : pk;
+						sr.cseen |= s >= di.hvc0 ? 1u : 0u;
+						sr.term.c = c;
+					}
+#endif
+#endif
+					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
+					s = sx;
+				}
+			}
+			w0++;
+			done = !live;
+		}
+#ifndef EBD_EXP_NOPUSH // experiment: no records for finalize (results are wrong)
+		push(done);
+#endif
+		if (done) {
+			e0 = e1;
+			e1 = lane_ev(d, grab(), re);
+			resolve();
 		}
 	}
+#ifdef EBD_EXP_DUAL
+	if ((dual ^ d.n) == 0x7fffffffu) // never: keeps the second chain alive
+		set_error(d, EBD_ERR_INTERNAL);
+#endif
 	if (lane == 0)
-		atomicAdd(&sh.walk_done, 1u);
+		atomicAdd(&sh.scan_done, 1u);
 }
 
 // ---------------------------------------------------------------------------------
-// The network of an external fast-path client (EBD_CFG_NETWORK_COUNTERS, Aggregator.cpp:89-106):
-// k_fresh already chose the client and its class (the client-IP front token, or the source
-// address); the maps need the address itself, parsed again here from the token's bytes.
+// Client-IP token and class of a fast-path request that carries a client-IP header
+// (HttpRequestParser.cpp:370-407 on the first client-IP value, Aggregator.cpp:50-74 on its
+// front token).  k_fresh found where the value starts; the lane copies the value's first
+// kCipRaw bytes into its LDS row with 8-byte loads and parses the token there.
 // ---------------------------------------------------------------------------------
 constexpr int kAggThreads = 256;
+constexpr int kCipRaw = 64;
+constexpr int kCipStride = kCipRaw + 8; // rows 72 B apart: lanes spread over the banks
 
-__device__ unsigned long long request_net(const Dev& d, uint32_t i, const ebd_event_result& r) {
-	unsigned long long net = 0;
-	if (r.info & EBD_INFO_CIP) {
-		const uint8_t* t = d.payload + d.off[i] + r.u.span.cip_off;
-		struct View {
-			const uint8_t* t;
-			__device__ uint8_t operator[](uint32_t k) const { return t[k]; }
-		};
-		classify_token(*d.ifs, View{t}, r.u.span.cip_len, &net);
-	} else {
-		const uint8_t* evb = (const uint8_t*)(d.ev + i);
-		const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
-		uint8_t src[16];
-		__builtin_memcpy(src, &sv, 16);
-		classify_source(*d.ifs, evb[32], src, &net);
+__device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_event_result& r, uint8_t* row,
+		unsigned long long* net) {
+	const uint8_t* p = d.payload + d.off[i];
+	const uint32_t cs = r.u.span.cip_off, lim = r.consumed; // the value ends before the final CRLF
+	unsigned long long v[kCipRaw / 8];
+#pragma unroll
+	for (int h = 0; h < kCipRaw / 8; h++) // past the request: re-read its last byte (stays in the buffer)
+		v[h] = gload8u(p + min(cs + 8 * h, lim - 1));
+#pragma unroll
+	for (int h = 0; h < kCipRaw / 8; h++)
+		*(unsigned long long*)(row + 8 * h) = v[h];
+	uint32_t tb, te;
+	uint8_t cls;
+	const uint32_t avail = lim - cs < (uint32_t)kCipRaw ? lim - cs : (uint32_t)kCipRaw; // valid bytes in the row
+	uint32_t e = 0;
+	while (e < avail && row[e] != ',' && row[e] != '\r')
+		e++;
+	if (e < avail || avail == lim - cs) {
+		cip_token(*d.ifs, [row](uint32_t b) { return (uint32_t)row[b]; }, 0, e, &tb, &te, &cls, net);
+	} else { // a value longer than the copy without ',' or CR in it: parse from the buffer
+		cip_token(*d.ifs, [p](uint32_t b) { return (uint32_t)p[b]; }, cs, lim, &tb, &te, &cls, net);
+		tb -= cs;
+		te -= cs;
 	}
-	return net;
+	r.u.span.cip_off = (uint16_t)(cs + tb);
+	r.u.span.cip_len = (uint16_t)(te - tb);
+	return cls;
 }
 
 __global__ void k_carry_insert(Dev d) {
@@ -1506,12 +1607,17 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 	}
 }
 
-// Aggregator::newRequest for the fast-path requests: coalesced reads of the results and keys
-// k_fresh wrote (the client class is already in each result, Aggregator.cpp:50-88), one slot
-// probe per request.  A block walks a contiguous range of the batch 256 events at a time, each
-// wave its own 64 of them, and the waves never wait for each other: every step of a wave is a
-// chain of dependent random accesses (slot probe, claim / counter atomics), and a block-wide
-// barrier per step made each step last as long as the slowest of 256 chains.
+// Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
+// and events).  The client class comes from the client-IP header's front token when k_fresh
+// found one (cip_classify), else from the session's source address (Aggregator.cpp:60-66,
+// 85-88).  A block walks a contiguous range of the batch 256 events at a time, each wave
+// its own 64 of them, and the waves never wait for each other: every step of a wave is a
+// chain of dependent random accesses (result, key, slot probe, claim / counter atomics), and
+// a block-wide barrier per step made each step last as long as the slowest of 256 chains.
+// Requests with a client-IP header (~30 % in config 3) go to the wave's own LDS ring and are
+// parsed 64 at a time, so the token parse, the longest code path, runs on full waves instead
+// of on the few lanes of each wave that have one.  Aggregation is order-free (counters,
+// atomicMin of the first-arrival word), so queueing does not change the result.
 //
 // A service created here only claims its slot: the claim (slot, claiming event) goes to the
 // block's own stretch of the claim stage, counted in LDS, with no global atomic.  The
@@ -1519,13 +1625,22 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // a scan of the per-block counts (k_pub_count, k_pub_scan) and copy the endpoint bytes
 // (k_publish).  A single global counter serialises at ~12 ns per atomic: reserving per block
 // and step cost ~5 ms per 100 M-event batch that creates 30 M services.
+constexpr uint32_t kAggWaves = kAggThreads / 64;
+constexpr uint32_t kCipRing = 128; // per wave: < 64 waiting + at most 64 new per step
+
 struct AggShared {
-	uint32_t cn; // claims of this block
+	uint32_t q[kAggWaves][kCipRing]; // each wave's queued client-IP requests (a ring)
+	uint32_t cn;                     // claims of this block
 	unsigned long long nreq;
 };
 
 __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
 		unsigned long long net) {
+#ifdef EBD_EXP_AGG_NOINSERT // experiment: classification only (results are wrong)
+	if (cls == 7)
+		atomicAdd(&sh.cn, 1u);
+	return;
+#endif
 	bool claimed;
 	const Hash128 key = d.keys[i];
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
@@ -1538,6 +1653,19 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 		d.cstage_slot[at] = slot;
 		d.cstage_ev[at] = i;
 	}
+}
+
+__device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh) {
+	ebd_event_result r = d.res[i];
+	unsigned long long net = 0;
+#ifndef EBD_EXP_AGG_NOCIP // experiment: no client-IP token parse (results are wrong)
+	const uint32_t cls = cip_classify(d, i, r, row, &net);
+#else
+	const uint32_t cls = CLS_INTERNAL;
+#endif
+	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+	d.res[i] = r;
+	agg_request(d, i, r, cls, sh, net);
 }
 
 // Steps (of kAggThreads events) per block; the claim stage holds per * kAggThreads per block.
@@ -1553,31 +1681,63 @@ __device__ __forceinline__ void wave_sync() {
 	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// 6 waves per SIMD: the compiler fits the kernel in 80 VGPRs without spilling (91 unbounded, 5 waves)
 #ifndef EBD_AGG_WAVES
-#define EBD_AGG_WAVES 8
+#define EBD_AGG_WAVES 6
 #endif
 __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(EBD_AGG_WAVES, 8))) void k_agg_fast(Dev d) {
+	__shared__ __attribute__((aligned(8))) uint8_t rows[kAggThreads * kCipStride];
 	__shared__ AggShared sh;
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	uint8_t* row = rows + threadIdx.x * kCipStride;
+	uint32_t* q = sh.q[wave];
 	if (threadIdx.x == 0) {
 		sh.nreq = 0;
 		sh.cn = 0;
 	}
 	__syncthreads();
 	uint32_t cnt = 0;
+	uint32_t qh = 0, qn = 0; // wave-uniform: ring head and queued requests
 	const uint32_t steps = (d.n + kAggThreads - 1) / kAggThreads;
 	const uint32_t per = agg_steps_per_block(d.n, gridDim.x);
 	const uint32_t s0 = min(steps, blockIdx.x * per), s1 = min(steps, s0 + per);
 	for (uint32_t st = s0; st < s1; st++) {
-		const uint32_t i = st * kAggThreads + threadIdx.x;
+		const uint32_t i = st * kAggThreads + wave * 64 + lane;
+		bool queue = false;
 		if (i < d.n) {
-			const ebd_event_result r = d.res[i];
+			ebd_event_result r = d.res[i];
 			if (r.status == EBD_STATUS_FINISHED && !(r.info & EBD_INFO_SESSION)) {
 				cnt++;
-				const uint32_t cls = (r.info >> EBD_INFO_CLASS_SHIFT) & 3u;
-				agg_request(d, i, r, cls, sh, d.net_on && cls == CLS_EXTERNAL ? request_net(d, i, r) : 0ull);
+				if (r.info & EBD_INFO_CIP) {
+					queue = true;
+				} else if (!d.net_on) { // k_fresh classified the source address
+					agg_request(d, i, r, (r.info >> EBD_INFO_CLASS_SHIFT) & 3u, sh, 0);
+				} else { // the network maps need the address itself
+					const uint8_t* evb = (const uint8_t*)(d.ev + i);
+					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
+					uint8_t src[16];
+					__builtin_memcpy(src, &sv, 16);
+					unsigned long long net = 0;
+					const uint32_t cls = classify_source(*d.ifs, evb[32], src, &net);
+					agg_request(d, i, r, cls, sh, net);
+				}
 			}
 		}
+		const unsigned long long b = __ballot(queue);
+		if (queue)
+			q[(qh + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))) & (kCipRing - 1)] = i;
+		qn += (uint32_t)__popcll(b);
+		if (qn >= 64) { // a full wave of client-IP requests
+			wave_sync();
+			agg_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row, sh);
+			qh += 64;
+			qn -= 64;
+			wave_sync(); // the ring words just read may be rewritten by the next step
+		}
 	}
+	wave_sync();
+	if (lane < qn) // what is left in the ring
+		agg_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row, sh);
 	atomicAdd(&sh.nreq, (unsigned long long)cnt);
 	__syncthreads();
 	if (threadIdx.x == 0) {
@@ -1780,10 +1940,21 @@ __device__ __forceinline__ Slot empty_slot() {
 }
 
 // Aggregator::clear (Aggregator.cpp:136-153): every claimed slot back to empty.
-__global__ void k_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots) {
+// Aggregator::clear's table reset.  Few services: their slots only, from the claimed-slot list
+// (random 64-B writes).  At least a quarter of the slots used: the whole table as a stream of
+// 16-B stores instead, which moves 4x the bytes at several times the rate of random writes
+// (30 M services in 2^26 slots: 1.8 ms the sparse way).
+__global__ void k_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, uint32_t slot_cap) {
 	const unsigned long long n = ctr[CTR_SERVICES];
-	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
-		slots[used[k]] = empty_slot();
+	const unsigned long long t0 = blockIdx.x * blockDim.x + threadIdx.x, nt = (unsigned long long)gridDim.x * blockDim.x;
+	if (4 * n < slot_cap) {
+		for (unsigned long long k = t0; k < n; k += nt)
+			slots[used[k]] = empty_slot();
+	} else {
+		uint4* w = (uint4*)slots; // a slot is 4 pieces; empty: first (piece 1, low half) = ~0, the rest 0
+		for (unsigned long long k = t0; k < 4ull * slot_cap; k += nt)
+			w[k] = (k & 3) == 1 ? make_uint4(~0u, ~0u, 0u, 0u) : make_uint4(0u, 0u, 0u, 0u);
+	}
 }
 
 __global__ void k_sset_clear(Dev d) {
@@ -1993,7 +2164,7 @@ __global__ void k_owner_count(const ebd_service* rec, const unsigned long long* 
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
 		const uint32_t w = (uint32_t)(rec[k].key_lo % world);
 		atomicAdd(&hc[w], 1ull);
-		atomicAdd(&hb[w], (unsigned long long)((rec[k].endpoint_len + 7u) & ~7u));
+		atomicAdd(&hb[w], rec[k].endpoint_off == ~0ull ? 0ull : (unsigned long long)((rec[k].endpoint_len + 7u) & ~7u));
 	}
 	__syncthreads();
 	for (uint32_t w = threadIdx.x; w < world; w += blockDim.x) {
@@ -2004,40 +2175,72 @@ __global__ void k_owner_count(const ebd_service* rec, const unsigned long long* 
 	}
 }
 
-// cur[w] / scur[w]: the next record / string byte of owner w (initialised to the owners'
-// segment starts); records land in arbitrary order inside their owner's segment.
-__global__ void k_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
-		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings) {
+// Records to their owners' segments (cur[w]: the next record of owner w, initialised to the
+// segment starts; arbitrary order inside a segment), as wire records; srcoff[at] keeps the
+// endpoint's arena offset for k_wire_copy.
+__global__ void k_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cur,
+		ebd_wire_service* out, unsigned long long* srcoff) {
 	const unsigned long long n = ctr[CTR_SERVICES];
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		ebd_service v = rec[k];
+		const ebd_service v = rec[k];
 		const uint32_t w = (uint32_t)(v.key_lo % world);
-		const uint32_t nb = (v.endpoint_len + 7u) & ~7u;
 		const unsigned long long at = atomicAdd(&cur[w], 1ull);
-		const unsigned long long sat = atomicAdd(&scur[w], (unsigned long long)nb);
-		if (v.endpoint_off != ~0ull) {
-			const unsigned long long* src = (const unsigned long long*)(arena + v.endpoint_off);
-			unsigned long long* dst = (unsigned long long*)(strings + sat);
-			for (uint32_t b = 0; b < nb / 8; b++)
-				dst[b] = src[b];
-			v.endpoint_off = sat - sbase[w];
-		}
-		out[at] = v;
+		ebd_wire_service o;
+		o.key_lo = v.key_lo;
+		o.key_hi = v.key_hi;
+		o.first = (v.first_seq << 16) | ((unsigned long long)(v.https & 1u) << 15) | (v.host_len & 0x7fffu);
+		o.pid = v.pid;
+		o.internal_clients = v.internal_clients;
+		o.external_clients = v.external_clients;
+		o.endpoint_len = v.endpoint_off == ~0ull ? (v.endpoint_len | EBD_WIRE_NO_BYTES) : v.endpoint_len;
+		out[at] = o;
+		srcoff[at] = v.endpoint_off;
 	}
 }
 
-__global__ void k_merge(Dev d, const ebd_service* rec, uint32_t n, const uint8_t* strings) {
+// Bytes each wire record's endpoint takes in the strings (the exclusive scan of this is its offset).
+__global__ void k_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
+		nb[k] = EBD_WIRE_BYTES(rec[k].endpoint_len);
+}
+
+// Export: each record's endpoint bytes from the arena to its scanned place in the strings.
+__global__ void k_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
+		const uint8_t* arena, uint8_t* strings) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		const ebd_service v = rec[k];
+		const uint32_t nb = EBD_WIRE_BYTES(rec[k].endpoint_len);
+		const unsigned long long* src = (const unsigned long long*)(arena + srcoff[k]);
+		unsigned long long* dst = (unsigned long long*)(strings + offs[k]);
+		for (uint32_t b = 0; b < nb / 8; b++)
+			dst[b] = src[b];
+	}
+}
+
+// Merge: received records inserted with agg_insert (counters add, the smallest first word
+// wins); the claimer publishes the endpoint from the strings (offs: the scan of k_wire_bytes).
+__global__ void k_merge(Dev d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
+		const unsigned long long* offs) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const ebd_wire_service v = rec[k];
+		const uint32_t len = v.endpoint_len & ~EBD_WIRE_NO_BYTES;
+		const unsigned long long at = offs[k];
+		if (at + EBD_WIRE_BYTES(v.endpoint_len) > strlen || len > 0xffffu) { // not what an export writes
+			set_error(d, EBD_ERR_INTERNAL);
+			continue;
+		}
 		bool claimed;
-		const unsigned long long first = (v.first_seq << 16) | ((unsigned long long)(v.https & 1u) << 15) | (v.host_len & 0x7fffu);
-		const uint32_t slot = agg_insert(d, Hash128{v.key_lo, v.key_hi}, first, v.internal_clients, v.external_clients, &claimed);
+		const uint32_t slot = agg_insert(d, Hash128{v.key_lo, v.key_hi}, v.first, v.internal_clients, v.external_clients, &claimed);
 		if (claimed) {
-			const uint8_t* ep = strings + (v.endpoint_off == ~0ull ? 0 : v.endpoint_off);
-			const uint32_t hl = min(v.host_len, v.endpoint_len);
-			claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
-					atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((v.endpoint_len + 7u) & ~7u)), v.pid, ep, hl, ep + hl,
-					v.endpoint_len - hl);
+			const uint32_t hl = min((uint32_t)(v.first & 0x7fffu), len);
+			const unsigned long long list_at = atomicAdd(&d.ctr[CTR_SERVICES], 1ull);
+			if (v.endpoint_len & EBD_WIRE_NO_BYTES) { // the source had no bytes: none here either
+				set_error(d, EBD_ERR_ARENA_FULL);
+				claim_publish(d, slot, list_at, ~0ull - len, v.pid, strings, hl, strings, len - hl);
+			} else {
+				const uint8_t* ep = strings + at;
+				claim_publish(d, slot, list_at, atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((len + 7u) & ~7u)), v.pid, ep, hl,
+						ep + hl, len - hl);
+			}
 		}
 	}
 }
@@ -2165,7 +2368,7 @@ uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
 	const uint64_t groups = ((uint64_t)d.n + kFreshThreads * 4 - 1) / (kFreshThreads * 4);
-	const int grid = (int)(groups < (uint64_t)cus ? groups : (uint64_t)cus);
+	const int grid = (int)(groups < (uint64_t)cus * EBD_FRESH_WGS ? groups : (uint64_t)cus * EBD_FRESH_WGS);
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
@@ -2230,8 +2433,9 @@ hipError_t launch_collect(const Dev& d, ebd_service* out, hipStream_t st, int cu
 	hipLaunchKernelGGL(k_collect, dim3(cus * 8), dim3(256), 0, st, d, out);
 	return hipGetLastError();
 }
-hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_clear_used, dim3(cus * 8), dim3(256), 0, st, used, ctr, slots);
+hipError_t launch_clear_used(const unsigned int* used, const unsigned long long* ctr, Slot* slots, uint32_t slot_cap,
+		hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_clear_used, dim3(cus * 16), dim3(256), 0, st, used, ctr, slots, slot_cap);
 	return hipGetLastError();
 }
 hipError_t launch_gen_len(const GenTables* T, uint32_t config, uint64_t seed, uint64_t first, uint32_t n, uint32_t align,
@@ -2294,14 +2498,23 @@ hipError_t launch_owner_count(const ebd_service* rec, const unsigned long long* 
 	hipLaunchKernelGGL(k_owner_count, dim3(cus * 4), dim3(256), 0, st, rec, ctr, world, cnt, bytes);
 	return hipGetLastError();
 }
-hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, const uint8_t* arena,
-		unsigned long long* cur, unsigned long long* scur, const unsigned long long* sbase, ebd_service* out, uint8_t* strings,
-		hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_owner_scatter, dim3(cus * 8), dim3(256), 0, st, rec, ctr, world, arena, cur, scur, sbase, out, strings);
+hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cur,
+		ebd_wire_service* out, unsigned long long* srcoff, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_owner_scatter, dim3(cus * 8), dim3(256), 0, st, rec, ctr, world, cur, out, srcoff);
 	return hipGetLastError();
 }
-hipError_t launch_merge(const Dev& d, const ebd_service* rec, uint32_t n, const uint8_t* strings, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_merge, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n, strings);
+hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_bytes, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, nb);
+	return hipGetLastError();
+}
+hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
+		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_copy, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, offs, srcoff, arena, strings);
+	return hipGetLastError();
+}
+hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
+		const unsigned long long* offs, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_merge, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n, strings, strlen, offs);
 	return hipGetLastError();
 }
 

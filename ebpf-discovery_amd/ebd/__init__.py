@@ -41,6 +41,12 @@ SERVICE_DTYPE = np.dtype([("pid", "<u4"), ("internal", "<u4"), ("external", "<u4
                           ("nets_v6", "<u4"), ("pad2", "<u4")])
 SERVICE_NET_DTYPE = np.dtype([("key_lo", "<u8"), ("key_hi", "<u8"), ("kind", "u1"), ("prefix", "u1", (6,)), ("pad", "u1"),
                               ("time_ns", "<u8")])
+# ebd_wire_service: a service on the cross-GPU wire (its endpoint bytes follow the previous
+# record's in the strings, each padded to 8 bytes; WIRE_NO_BYTES in endpoint_len: none)
+WIRE_DTYPE = np.dtype([("key_lo", "<u8"), ("key_hi", "<u8"), ("first", "<u8"), ("pid", "<u4"), ("internal", "<u4"),
+                       ("external", "<u4"), ("endpoint_len", "<u4")])
+WIRE_NO_BYTES = 0x80000000
+assert WIRE_DTYPE.itemsize == 40
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
 assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 80 and SERVICE_NET_DTYPE.itemsize == 32
 CFG_TIMING = 2
@@ -386,23 +392,24 @@ class Context:
             buf = C.create_string_buffer(ln.value)
 
     def export_services_device(self, world, device):
-        """The services grouped by owner (key_lo % world) in device tensors:
-        (records as uint8 [n * 64], strings uint8, counts[world], str_counts[world])."""
+        """The services grouped by owner (key_lo % world) in device tensors: (WIRE_DTYPE
+        records as uint8 [n * 40], their endpoint bytes uint8, counts[world], str_counts[world])."""
         import torch
         counts = np.zeros(world, np.uint32)
         scounts = np.zeros(world, np.uint64)
         _check(lib().ebd_export_services_device(self.h, world, None, 0, None, 0, _p(counts), _p(scounts)), "export")
         n, sb = int(counts.sum()), int(scounts.sum())
-        recs = torch.empty(max(n, 1) * SERVICE_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        recs = torch.empty(max(n, 1) * WIRE_DTYPE.itemsize, dtype=torch.uint8, device=device)
         strs = torch.empty(max(sb, 8), dtype=torch.uint8, device=device)
         _check(lib().ebd_export_services_device(self.h, world, C.c_void_p(recs.data_ptr()), max(n, 1),
                                                 C.c_void_p(strs.data_ptr()), strs.numel(), _p(counts), _p(scounts)),
                "ebd_export_services_device")
-        return recs[:n * SERVICE_DTYPE.itemsize], strs[:sb], counts, scounts
+        return recs[:n * WIRE_DTYPE.itemsize], strs[:sb], counts, scounts
 
     def merge_services_device(self, recs, strings):
-        """Inserts exported service records (device uint8 tensors) into this table."""
-        n = recs.numel() // SERVICE_DTYPE.itemsize
+        """Inserts wire records (device uint8 tensors; strings readable 8 bytes past their
+        bytes) into this table."""
+        n = recs.numel() // WIRE_DTYPE.itemsize
         _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
                                                C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                strings.numel()), "ebd_merge_services_device")

@@ -9,8 +9,10 @@ collective.  The one exchange is at the end, the Aggregator merge:
     GPU because the ranks share the key), its uint32 counters and the trace position of
     its first request with that request's scheme and host/url split;
   * owner = key_lo mod world.  The GPU groups its services by owner on the device
-    (ebd_export_services_device) and ONE all_to_all_single of records and one of endpoint
-    bytes ship each service to its owner, over RCCL (xGMI) on GPU tensors;
+    (ebd_export_services_device) and ONE all_to_all_single of 40-byte wire records and one
+    of endpoint bytes ship each service to its owner, over RCCL (xGMI) on GPU tensors.  A
+    record's bytes follow the previous record's (8-byte padded), so the received segments
+    concatenate into one addressable table with no offsets to rebase;
   * the owner merges on the device (ebd_merge_services_device): counters add modulo 2^32
     (Service.h:53-54 are uint32), the earliest first request fixes domain and scheme
     (Aggregator.cpp:155-168: the first request of a key creates the service, later ones
@@ -24,10 +26,11 @@ earliest event; a context's first_seq is mapped to the trace position before the
 """
 import numpy as np
 
-from . import SERVICE_DTYPE
+from . import SERVICE_DTYPE, WIRE_DTYPE, WIRE_NO_BYTES
 
-REC = SERVICE_DTYPE  # the exchanged record: ebd_service (include/ebpf_discovery_amd.h)
+REC = WIRE_DTYPE  # the exchanged record: ebd_wire_service (include/ebpf_discovery_amd.h)
 STR_SLACK = 64  # readable bytes past received endpoint strings (k_merge copies 8-byte words)
+NO_OFF = np.uint64(0xFFFFFFFFFFFFFFFF)
 M32 = np.uint64(0xFFFFFFFF)
 
 
@@ -61,7 +64,7 @@ class ServiceTable:
     """Services as ebd_service records plus the endpoint bytes they point into."""
 
     def __init__(self, rec=None, strings=None):
-        self.rec = rec if rec is not None else np.zeros(0, REC)
+        self.rec = rec if rec is not None else np.zeros(0, SERVICE_DTYPE)
         self.strings = strings if strings is not None else np.zeros(0, np.uint8)
 
     @classmethod
@@ -80,7 +83,7 @@ class ServiceTable:
     def from_rows(cls, rows, keys):
         """From (pid, endpoint, domain, scheme, internal, external, first) rows and their
         (key_lo, key_hi) keys (tests build tables from the oracle this way)."""
-        rec = np.zeros(len(rows), REC)
+        rec = np.zeros(len(rows), SERVICE_DTYPE)
         parts, off = [], 0
         for k, (row, key) in enumerate(zip(rows, keys)):
             pid, ep, dom, sch, i, e, first = row
@@ -91,6 +94,7 @@ class ServiceTable:
             r["https"] = sch in (b"https", "https")
             r["endpoint_off"], r["endpoint_len"] = off, len(ep)
             r["domain_off"], r["domain_len"] = d0, len(dom)
+            r["host_len"] = d0 + len(dom)  # a host whose domain is this one (host_domain gives it back)
             r["first_seq"], r["key_lo"], r["key_hi"] = first, key[0], key[1]
             rec[k] = r
             parts.append(ep)
@@ -136,20 +140,57 @@ class ServiceTable:
         r["endpoint_off"] = new_off.astype(np.uint64)
         return ServiceTable(r, out)
 
-    def by_owner(self, world):
-        """(records grouped by owner, strings packed per owner with endpoint_off relative to
-        the owner's segment, counts[world], str_counts[world]): ebd_export_services_device."""
+    def to_wire(self, world):
+        """(wire records grouped by owner, their endpoint bytes in record order, each padded
+        to 8, counts[world], str_counts[world]): what ebd_export_services_device returns."""
         owner = (self.rec["key_lo"] % np.uint64(world)).astype(np.int64)
         order = np.argsort(owner, kind="stable")
-        t = ServiceTable(self.rec[order], self.strings).packed()
-        owner = owner[order]
+        r, owner = self.rec[order], owner[order]
+        w = np.zeros(r.size, REC)
+        for f in ("key_lo", "key_hi", "pid", "internal", "external"):
+            w[f] = r[f]
+        w["first"] = ((r["first_seq"].astype(np.uint64) << np.uint64(16)) | (r["https"].astype(np.uint64) << np.uint64(15))
+                      | (r["host_len"].astype(np.uint64) & np.uint64(0x7FFF)))
+        has = r["endpoint_off"] != NO_OFF
+        w["endpoint_len"] = np.where(has, r["endpoint_len"], r["endpoint_len"] | np.uint32(WIRE_NO_BYTES))
+        nb = wire_bytes(w["endpoint_len"])
+        out = np.zeros(int(nb.sum()), np.uint8)
+        at = 0
+        blob = self.strings
+        for k in range(r.size):
+            if has[k]:
+                o, L = int(r["endpoint_off"][k]), int(r["endpoint_len"][k])
+                out[at:at + L] = blob[o:o + L]
+            at += int(nb[k])
         counts = np.bincount(owner, minlength=world).astype(np.uint32)
         scounts = np.zeros(world, np.uint64)
-        np.add.at(scounts, owner, t.rec["endpoint_len"].astype(np.uint64))
-        sstart = np.zeros(world, np.uint64)
-        sstart[1:] = np.cumsum(scounts)[:-1]
-        t.rec["endpoint_off"] -= sstart[owner]
-        return t.rec, t.strings, counts, scounts
+        np.add.at(scounts, owner, nb)
+        return w, out, counts, scounts
+
+    @classmethod
+    def from_wire(cls, w, strings):
+        """Received wire records (and their bytes) as a table: endpoint offsets from the scan
+        of the padded lengths, domain and scheme from the first-arrival word (k_collect)."""
+        nb = wire_bytes(w["endpoint_len"])
+        offs = np.zeros(w.size, np.uint64)
+        if w.size:
+            offs[1:] = np.cumsum(nb)[:-1]
+        r = np.zeros(w.size, SERVICE_DTYPE)
+        for f in ("key_lo", "key_hi", "pid", "internal", "external"):
+            r[f] = w[f]
+        first = w["first"].astype(np.uint64)
+        r["first_seq"] = first >> np.uint64(16)
+        r["https"] = ((first >> np.uint64(15)) & np.uint64(1)).astype(np.uint8)
+        r["host_len"] = (first & np.uint64(0x7FFF)).astype(np.uint32)
+        none = (w["endpoint_len"] & np.uint32(WIRE_NO_BYTES)) != 0
+        r["endpoint_len"] = w["endpoint_len"] & np.uint32(~WIRE_NO_BYTES & 0xFFFFFFFF)
+        r["endpoint_off"] = np.where(none, NO_OFF, offs)
+        s = strings.tobytes() if hasattr(strings, "tobytes") else bytes(strings)
+        for k in np.flatnonzero(~none):
+            o = int(offs[k])
+            hl = min(int(r["host_len"][k]), int(r["endpoint_len"][k]))
+            r["domain_off"][k], r["domain_len"][k] = host_domain(s[o:o + hl])
+        return cls(r, np.frombuffer(s, np.uint8).copy() if s else np.zeros(0, np.uint8))
 
     def rows(self):
         """[(pid, endpoint, domain, scheme, internal, external)] sorted by (pid, endpoint)."""
@@ -173,7 +214,7 @@ def concat(tables):
         recs.append(r)
         blobs.append(t.strings)
         base += t.strings.size
-    return ServiceTable(np.concatenate(recs) if recs else np.zeros(0, REC),
+    return ServiceTable(np.concatenate(recs) if recs else np.zeros(0, SERVICE_DTYPE),
                         np.concatenate(blobs) if blobs else np.zeros(0, np.uint8))
 
 
@@ -184,7 +225,7 @@ def merge_tables(tables):
 def exchange(recs, strings, counts, scounts, group=None):
     """One all_to_all_single of the owner-grouped records and one of their endpoint bytes
     (torch uint8 tensors on the group's device: RCCL on GPU tensors, gloo on CPU ones).
-    Returns (records, strings) received, endpoint_off rebased onto the received bytes."""
+    Returns (records, strings) received: segments in source order, addressable as they are."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
@@ -204,13 +245,6 @@ def exchange(recs, strings, counts, scounts, group=None):
     out_s = torch.zeros(nstr + STR_SLACK, dtype=torch.uint8, device=dev)
     dist.all_to_all_single(out_s[:nstr], strings, output_split_sizes=[int(c) for c in rscounts],
                            input_split_sizes=[int(c) for c in scounts], group=group)
-    if out_r.numel():  # endpoint_off (byte 16 of a record) += the source's string base
-        base = np.zeros(world, np.int64)
-        base[1:] = np.cumsum(rscounts)[:-1]
-        src_base = torch.repeat_interleave(torch.tensor(base, device=dev), torch.tensor(rcounts, device=dev))
-        words = out_r.view(torch.int64).view(-1, nrec // 8)
-        # ~0 = no endpoint bytes (the source's arena was full): left as it is
-        words[:, 2] = torch.where(words[:, 2] == -1, words[:, 2], words[:, 2] + src_base)
     return out_r, out_s
 
 
@@ -220,11 +254,11 @@ def exchange_merge(table, device="cpu", group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    rec, strings, counts, scounts = table.merged().by_owner(world)
+    rec, strings, counts, scounts = table.merged().to_wire(world)
     r = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(device)
     s = torch.from_numpy(strings.copy()).to(device)
     out_r, out_s = exchange(r, s, counts, scounts, group)
-    mine = ServiceTable(out_r.cpu().numpy().view(REC).copy(), out_s.cpu().numpy().copy())
+    mine = ServiceTable.from_wire(out_r.cpu().numpy().view(REC).copy(), out_s.cpu().numpy()[:out_s.numel() - STR_SLACK])
     return mine.merged().packed()
 
 
@@ -242,7 +276,8 @@ def gather_rows(table, group=None):
 def device_exchange_merge(ctx, device, group=None, map_first=None):
     """GPU path: export by owner on the device, exchange over RCCL, merge on the device into
     this rank's context (cleared first).  map_first(first_seq int64 tensor) -> trace
-    positions, applied before the exchange.  Returns (records sent, records received)."""
+    positions, applied before the exchange.  Returns {sent, received, record_bytes,
+    string_bytes}: this rank's records out and in, and the bytes it sent."""
     import torch.distributed as dist
     if getattr(ctx, "network_counters", False):
         # the merge carries client counters only: network maps are per context (DESIGN.md section 7)
@@ -250,13 +285,41 @@ def device_exchange_merge(ctx, device, group=None, map_first=None):
     world = dist.get_world_size(group)
     check_same_hash_key(ctx, device, group)
     recs, strs, counts, scounts = ctx.export_services_device(world, device)
-    if map_first is not None and recs.numel():
-        words = recs.view(torch_int64()).view(-1, REC.itemsize // 8)
-        words[:, 5] = map_first(words[:, 5])  # first_seq (byte 40)
+    if map_first is not None:
+        map_wire_first(recs, map_first)
     out_r, out_s = exchange(recs, strs, counts, scounts, group)
     ctx.clear()
     ctx.merge_services_device(out_r, out_s)
-    return int(counts.sum()), out_r.numel() // REC.itemsize
+    return {"sent": int(counts.sum()), "received": out_r.numel() // REC.itemsize,
+            "record_bytes": recs.numel(), "string_bytes": strs.numel()}
+
+
+def map_wire_first(recs, fn):
+    """In place on device wire records (uint8 tensor): the first-arrival word's sequence
+    number (bits 16..63) through fn (int64 tensor -> int64 tensor)."""
+    if recs.numel() == 0:
+        return
+    words = recs.view(torch_int64()).view(-1, REC.itemsize // 8)
+    f = words[:, 2]
+    words[:, 2] = (fn(f >> 16) << 16) | (f & 0xFFFF)
+
+
+def wire_bytes(lens):
+    """Bytes each wire record's endpoint takes in the strings (EBD_WIRE_BYTES)."""
+    lens = np.asarray(lens, np.uint32)
+    return np.where((lens & np.uint32(WIRE_NO_BYTES)) != 0, 0, (lens.astype(np.uint64) + 7) & ~np.uint64(7)).astype(np.uint64)
+
+
+def host_domain(host):
+    """(offset, length) of the domain in a Host value (ebd_spec.h host_domain,
+    Aggregator.cpp:112-130): "[...]" through the first ']' after the first '[' (empty
+    without one), else the host up to its first ':'."""
+    lb = host.find(b"[")
+    if lb >= 0:
+        rb = host.find(b"]", lb + 1)
+        return (lb, rb - lb + 1) if rb >= 0 else (0, 0)
+    c = host.find(b":")
+    return 0, (c if c >= 0 else len(host))
 
 
 def check_same_hash_key(ctx, device, group=None):

@@ -323,17 +323,34 @@ int ebd_format_services_json(const ebd_service* s, uint32_t n, const char* strin
 int ebd_report_json(ebd_ctx* ctx, char* out, uint64_t cap, uint64_t* len);
 
 /* --- cross-GPU merge of per-GPU service tables ------------------------ */
+/* A service on the wire (40 B): what the owner's merge needs.  The endpoint bytes are not
+ * addressed: record k's bytes follow record k-1's in the strings, each padded to 8 bytes, so
+ * concatenated segments (all-to-all output) stay addressable without rebasing. */
+typedef struct ebd_wire_service {
+	uint64_t key_lo, key_hi;
+	uint64_t first;            /* first-arrival word: first_seq << 16 | https << 15 | host_len */
+	uint32_t pid;
+	uint32_t internal_clients; /* uint32, add modulo 2^32 (Service.h:53-54) */
+	uint32_t external_clients;
+	uint32_t endpoint_len;     /* EBD_WIRE_NO_BYTES set: no bytes follow (the source arena was full) */
+} ebd_wire_service;
+#define EBD_WIRE_NO_BYTES 0x80000000u
+/* Bytes a wire record's endpoint takes in the strings. */
+#define EBD_WIRE_BYTES(len) (((len) & EBD_WIRE_NO_BYTES) ? 0u : (((len) + 7u) & ~7u))
+
 /* The context's services grouped by owner GPU, owner = key_lo % world, into DEVICE arrays:
- * recs[] ordered by owner (counts[w] records for owner w), strings[] the owners' endpoint
- * bytes in owner order (str_counts[w] bytes for owner w, 8-byte aligned pieces), and each
- * record's endpoint_off relative to its owner's string segment.  counts / str_counts are
- * host arrays of `world` entries.  recs == NULL: sizes only. */
-int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_service* recs, uint32_t cap, uint8_t* strings,
+ * recs[] ordered by owner (counts[w] records for owner w), strings[] their endpoint bytes in
+ * record order (str_counts[w] bytes for owner w).  counts / str_counts are host arrays of
+ * `world` entries.  recs == NULL: sizes only. */
+int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings,
 		uint64_t strcap, uint32_t* counts, uint64_t* str_counts);
-/* Merges n service records (DEVICE arrays, endpoint_off into strings) into the context's
- * table: counters add (uint32), the record with the smallest first_seq fixes scheme and
- * host/url split (Aggregator.cpp:155-168 across GPUs), the endpoint bytes are copied in. */
-int ebd_merge_services_device(ebd_ctx* ctx, const ebd_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen);
+/* Merges n wire records (DEVICE arrays; strings hold their bytes in record order, readable
+ * 8 bytes past strlen) into the context's table: counters add (uint32), the record with the
+ * smallest first word fixes scheme and host/url split (Aggregator.cpp:155-168 across GPUs),
+ * the endpoint bytes are copied in.  Records whose bytes would run past strlen are skipped
+ * and reported as EBD_ERR_INTERNAL. */
+int ebd_merge_services_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings,
+		uint64_t strlen);
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
 /* Hash of the sources this library was built from (profiles/ name the build they measured). */

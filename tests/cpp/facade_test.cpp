@@ -137,6 +137,10 @@ int run_gpu() {
 			want.scheme = "http";
 			want.internalClientsNumber = 1000;
 			CHECK(svc[0] == want);
+			if (!(svc[0] == want))
+				std::fprintf(stderr, "got pid %u endpoint '%s' domain '%s' scheme '%s' internal %u external %u\n", svc[0].pid,
+						svc[0].endpoint.c_str(), svc[0].domain.c_str(), svc[0].scheme.c_str(), svc[0].internalClientsNumber,
+						svc[0].externalClientsNumber);
 		}
 		std::ostringstream out;
 		d.outputServicesToStdout(out);

@@ -37,21 +37,16 @@ def _device_shard(ctx, cfg, seed, first, n, world, rank, dev):
 
 
 def _merge_owner_segments(segs, dev):
-    """Device merge of every owner's segments (endpoint offsets rebased onto the concatenated
-    bytes, as shard.exchange does after the all-to-all)."""
+    """Device merge of every owner's segments, concatenated as the all-to-all delivers them
+    (wire records need no rebasing), with the merge's 8 readable bytes of slack."""
     import torch
+    from ebd import shard
     rows = []
     for parts in segs:
-        base, rparts, sparts = 0, [], []
-        for r, s in parts:
-            r = r.clone()
-            if r.numel():
-                r.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)[:, 2] += base
-            rparts.append(r)
-            sparts.append(s)
-            base += s.numel()
+        recs = torch.cat([r for r, _ in parts])
+        strs = torch.cat([s for _, s in parts] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8, device=dev)])
         m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY)
-        m.merge_services_device(torch.cat(rparts), torch.cat(sparts))
+        m.merge_services_device(recs, strs)
         st = m.stats()
         assert st["errors"] == 0, st
         rows += m.services()
@@ -66,6 +61,7 @@ def test_config5_shards_device_merge_equals_oracle(world):
     its own context; export by owner and device merge give exactly the oracle's services over
     the whole unsharded trace."""
     import torch
+    from ebd import shard
     dev = torch.device("cuda:0")
     N = 1_000_000
     segs = [[] for _ in range(world)]
@@ -80,12 +76,11 @@ def test_config5_shards_device_merge_equals_oracle(world):
         assert st["errors"] == 0, st
         assert st["session_events"] == 0  # one buffer per connection: the fast path only
         recs, strs, counts, scounts = ctx.export_services_device(world, dev)
+        shard.map_wire_first(recs, lambda f: gi[f])  # first arrival: shard order -> trace position
         if recs.numel():
-            words = recs.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)
-            words[:, 5] = gi[words[:, 5]]  # first_seq: shard order -> trace position
-            owner = (words[:, 6].cpu().numpy().view(np.uint64) % np.uint64(world)).astype(np.int64)
-            assert np.all(np.diff(owner) >= 0)
-        ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))]) * ebd.SERVICE_DTYPE.itemsize
+            owner = (recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64) % np.uint64(world))
+            assert np.all(np.diff(owner.astype(np.int64)) >= 0)
+        ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))]) * ebd.WIRE_DTYPE.itemsize
         so = np.concatenate([[0], np.cumsum(scounts.astype(np.int64))])
         for w in range(world):
             segs[w].append((recs[ro[w]:ro[w + 1]], strs[so[w]:so[w + 1]]))

@@ -227,7 +227,7 @@ def test_sharded_contexts_merge_to_whole_trace():
 def _owner_segments(recs, strs, counts, scounts):
     ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
     so = np.concatenate([[0], np.cumsum(scounts.astype(np.int64))])
-    n = ebd.SERVICE_DTYPE.itemsize
+    n = ebd.WIRE_DTYPE.itemsize
     return [(recs[ro[w] * n:ro[w + 1] * n], strs[so[w]:so[w + 1]]) for w in range(len(counts))]
 
 
@@ -247,25 +247,19 @@ def test_device_export_by_owner_and_merge_equals_whole_trace():
             ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size, hash_key=ebd.TEST_HASH_KEY)
             ctx.submit(ev[idx], lens[idx], offs[idx], payload)
             recs, strs, counts, scounts = ctx.export_services_device(W, dev)
+            gpos = torch.tensor(idx.astype(np.int64), device=dev)
+            shard.map_wire_first(recs, lambda f: gpos[f])  # first arrival: shard order -> trace position
             if recs.numel():
-                words = recs.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)
-                words[:, 5] = torch.tensor(idx.astype(np.int64), device=dev)[words[:, 5]]
-                owner = (words[:, 6].cpu().numpy().view(np.uint64) % np.uint64(W)).astype(np.int64)
-                assert np.all(np.diff(owner) >= 0)  # grouped by owner
+                owner = (recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64) % np.uint64(W))
+                assert np.all(np.diff(owner.astype(np.int64)) >= 0)  # grouped by owner
             for w, seg in enumerate(_owner_segments(recs, strs, counts, scounts)):
                 segs[w].append(seg)
         rows = []
         for w in range(W):
-            base, rparts, sparts = 0, [], []
-            for r, s in segs[w]:
-                r = r.clone()
-                if r.numel():
-                    r.view(torch.int64).view(-1, ebd.SERVICE_DTYPE.itemsize // 8)[:, 2] += base
-                rparts.append(r)
-                sparts.append(s)
-                base += s.numel()
+            recs = torch.cat([r for r, _ in segs[w]])  # concatenated as the all-to-all delivers them
+            strs = torch.cat([s for _, s in segs[w]] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8, device=dev)])
             m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY)
-            m.merge_services_device(torch.cat(rparts), torch.cat(sparts))
+            m.merge_services_device(recs, strs)
             assert m.stats()["errors"] == 0
             rows += m.services()
         rows.sort(key=lambda t: (t[0], t[1]))
@@ -288,10 +282,11 @@ def test_device_exchange_merge_over_rccl_world1():
     os.environ.setdefault("MASTER_PORT", "29517")
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        sent, got = shard.device_exchange_merge(ctx, torch.device("cuda", 0), map_first=lambda f: f)
+        x = shard.device_exchange_merge(ctx, torch.device("cuda", 0), map_first=lambda f: f)
     finally:
         dist.destroy_process_group()
-    assert sent == got == len(before)
+    assert x["sent"] == x["received"] == len(before)
+    assert x["record_bytes"] == 40 * len(before)
     assert ctx.services() == before
 
 

@@ -153,20 +153,21 @@ def _key_worker(rank, world, port, same, out_path):
             ok = True
         except ValueError:
             ok = False
-        # an exported record without endpoint bytes (endpoint_off = ~0: the source arena was
-        # full) keeps ~0 through the exchange; the others are rebased onto the received bytes
+        # a wire record without endpoint bytes (WIRE_NO_BYTES: the source arena was full) takes
+        # no bytes; the others' bytes follow in record order, so the received segments
+        # concatenate into one addressable table (no rebasing)
         rec = np.zeros(2, shard.REC)
-        rec["endpoint_off"] = [np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64(0)]
-        rec["endpoint_len"] = [0, 3]
-        strings = np.frombuffer(b"ab%d" % rank, np.uint8).copy()
+        rec["endpoint_len"] = [ebd.WIRE_NO_BYTES, 3]
+        strings = np.frombuffer(b"ab%d\0\0\0\0\0" % rank, np.uint8).copy()
         counts = np.array([1, 1], np.uint32) if rank == 0 else np.array([2, 0], np.uint32)
-        scounts = np.array([0, 3], np.uint64) if rank == 0 else np.array([3, 0], np.uint64)
+        scounts = np.array([0, 8], np.uint64) if rank == 0 else np.array([8, 0], np.uint64)
         r, s = shard.exchange(torch.from_numpy(rec.view(np.uint8).copy()), torch.from_numpy(strings), counts, scounts)
-        got = r.numpy().view(shard.REC)
-        offs = [int(x) for x in got["endpoint_off"]]
+        t = shard.ServiceTable.from_wire(r.numpy().view(shard.REC).copy(), s.numpy()[:s.numel() - shard.STR_SLACK])
+        eps = [None if o == 0xFFFFFFFFFFFFFFFF else t.strings[o:o + n].tobytes().decode()
+               for o, n in zip(t.rec["endpoint_off"].tolist(), t.rec["endpoint_len"].tolist())]
         nb = s.numel()
         with open(out_path % rank, "w") as f:
-            json.dump({"ok": ok, "offs": offs, "nbytes": nb}, f)
+            json.dump({"ok": ok, "eps": eps, "nbytes": nb}, f)
     finally:
         dist.destroy_process_group()
 
@@ -177,7 +178,7 @@ def test_exchange_checks_hash_keys_and_keeps_missing_endpoints(same, tmp_path):
     mp.start_processes(_key_worker, args=(2, _free_port(), same, out_path), nprocs=2, join=True, start_method="spawn")
     r0, r1 = (json.load(open(out_path % k)) for k in (0, 1))
     assert r0["ok"] == r1["ok"] == same
-    # rank 0 receives its own first record (no bytes) and rank 1's two (3 bytes at rank 1's base 0)
-    assert r0["offs"] == [0xFFFFFFFFFFFFFFFF, 0xFFFFFFFFFFFFFFFF, 0]
-    assert r1["offs"] == [0]  # rank 0's second record, its 3 bytes at offset 0
-    assert r0["nbytes"] >= 3 + shard.STR_SLACK
+    # rank 0 receives its own first record (no bytes) and rank 1's two; rank 1 rank 0's second
+    assert r0["eps"] == [None, None, "ab1"]
+    assert r1["eps"] == ["ab0"]
+    assert r0["nbytes"] == 8 + shard.STR_SLACK
