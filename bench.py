@@ -127,7 +127,17 @@ def cpu_baseline(config, seed, budget_s):
     chunk = 250_000 if config in (3, 4, 5) else 1_000_000
     done, spent, first = 0, 0.0, 0
     gen = 3 if config == 5 else config
-    while spent < budget_s:
+    if config == 4:  # generated from position 0 only: one sample, replayed in order in chunks
+        ev, lens, offs, payload = O.config4_sample(seed, budget_s)
+        for a in range(0, len(ev), chunk):
+            if spent >= budget_s:
+                break
+            t = time.perf_counter()
+            o.process(ev[a:a + chunk], lens[a:a + chunk], offs[a:a + chunk], payload)
+            spent += time.perf_counter() - t
+            done += len(ev[a:a + chunk])
+        del ev, lens, offs, payload
+    while spent < budget_s and config != 4:
         ev, lens, offs, payload = ebd.generate_host(gen, seed, first, chunk)
         t = time.perf_counter()
         o.process(ev, lens, offs, payload)

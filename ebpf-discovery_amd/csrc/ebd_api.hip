@@ -112,7 +112,7 @@ struct ebd_ctx {
 	Slot* d_slots = nullptr;
 	uint32_t slot_cap = 0;
 	uint32_t* d_new_slots = nullptr;
-	uint32_t* d_cstage = nullptr; // claim stage: slots then events, max_events + blocks of slack each
+	ClaimRec* d_cstage = nullptr; // claim stage: max_events + blocks of slack
 	uint64_t cstage_cap = 0;
 	uint32_t* d_blk = nullptr;    // blk_cnt, blk_bytes (u32) then blk_lbase, blk_abase (u64)
 	unsigned long long* d_list_ep = nullptr;
@@ -196,6 +196,7 @@ struct ebd_ctx {
 	// session path's counters (h_end) are; batch = every kernel of the last batch finished;
 	// res = the async results read-back finished
 	hipEvent_t ev_mid = nullptr, ev_end = nullptr, ev_batch = nullptr, ev_res = nullptr;
+
 	int pending_end = 0, res_pending = 0, batch_valid = 0;
 	unsigned long long* h_end = nullptr; // pinned
 	// bookkeeping
@@ -271,8 +272,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.slots = c->d_slots;
 	d.slot_mask = c->slot_cap - 1;
 	d.new_slots = c->d_new_slots;
-	d.cstage_slot = c->d_cstage;
-	d.cstage_ev = c->d_cstage + c->cstage_cap;
+	d.cstage = c->d_cstage;
 	d.cstage_per = 0;
 	d.blk_cnt = c->d_blk;
 	d.blk_bytes = c->d_blk + kMaxAggBlocks;
@@ -459,7 +459,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	// one stretch of per-block capacity per k_agg_fast block: grid * ceil(steps / grid) steps of
 	// kAggThreads events, below (steps + grid) * kAggThreads for any batch up to max_events
 	c->cstage_cap = (((uint64_t)c->max_events + 255) / 256 + kMaxAggBlocks) * 256;
-	CTX_TRY(hipMalloc(&c->d_cstage, 2 * c->cstage_cap * sizeof(uint32_t)));
+	CTX_TRY(hipMalloc(&c->d_cstage, c->cstage_cap * sizeof(ClaimRec)));
 	CTX_TRY(hipMalloc(&c->d_blk, (size_t)kMaxAggBlocks * (2 * sizeof(uint32_t) + 2 * sizeof(unsigned long long))));
 	CTX_TRY(hipMalloc(&c->d_list_ep, (size_t)c->new_cap * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_list_pl, (size_t)c->new_cap * sizeof(unsigned long long)));

@@ -117,6 +117,16 @@ struct VerifyRec {
 	uint32_t slot, pad;
 };
 
+// A service k_agg_fast created, staged for publication (k_pub_count, k_publish): its slot and
+// everything publication needs of the claiming request, so publication reads no per-event
+// array, only the endpoint bytes.
+struct ClaimRec {
+	uint32_t slot, pid;
+	uint16_t host_off, host_len, url_off, url_len;
+	unsigned long long off; // the request's buffer in the payload
+};
+static_assert(sizeof(ClaimRec) == 24, "claim record is 24 bytes");
+
 struct Dev {
 	// immutable tables
 	const uint8_t* dfa;
@@ -143,8 +153,7 @@ struct Dev {
 	uint32_t new_cap;
 	// k_agg_fast's claims, block b's at [b * cstage_per, + blk_cnt[b]): slot and claiming event;
 	// the publication kernels' per-block byte counts and list / arena bases
-	uint32_t* cstage_slot;
-	uint32_t* cstage_ev;
+	struct ClaimRec* cstage;
 	uint32_t cstage_per;
 	uint32_t* blk_cnt;
 	uint32_t* blk_bytes;

@@ -1650,8 +1650,15 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 	if (claimed) { // at most one claim per event: the block's stretch holds them all
 		const uint32_t k = atomicAdd(&sh.cn, 1u);
 		const unsigned long long at = (unsigned long long)blockIdx.x * d.cstage_per + k;
-		d.cstage_slot[at] = slot;
-		d.cstage_ev[at] = i;
+		ClaimRec cr;
+		cr.slot = slot;
+		cr.pid = d.ev[i].pid;
+		cr.host_off = r.u.span.host_off;
+		cr.host_len = r.u.span.host_len;
+		cr.url_off = r.u.span.url_off;
+		cr.url_len = r.u.span.url_len;
+		cr.off = d.off[i];
+		d.cstage[at] = cr;
 	}
 }
 
@@ -1750,10 +1757,7 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(EBD
 // ---- publication of the services k_agg_fast created (one block per k_agg_fast block) ----
 constexpr int kPubThreads = 256, kPubClaims = kPubThreads / 4;
 
-__device__ __forceinline__ uint32_t claim_bytes(const Dev& d, uint32_t i) {
-	const ebd_event_result r = d.res[i];
-	return (r.u.span.host_len + r.u.span.url_len + 7u) & ~7u;
-}
+__device__ __forceinline__ uint32_t claim_bytes(const ClaimRec& c) { return (c.host_len + c.url_len + 7u) & ~7u; }
 
 // Inclusive prefix of x over the block (kPubThreads); `part` is LDS scratch of 4 words.
 __device__ __forceinline__ uint32_t block_scan(uint32_t x, uint32_t* part, uint32_t* total) {
@@ -1819,7 +1823,7 @@ __global__ __launch_bounds__(kPubThreads) void k_pub_count(Dev d) {
 	const unsigned long long at0 = (unsigned long long)b * d.cstage_per;
 	unsigned long long sum = 0;
 	for (uint32_t j = threadIdx.x; j < cn; j += kPubThreads)
-		sum += claim_bytes(d, d.cstage_ev[at0 + j]);
+		sum += claim_bytes(d.cstage[at0 + j]);
 	uint32_t total;
 	block_scan((uint32_t)sum, part, &total);
 	if (threadIdx.x == 0)
@@ -1872,17 +1876,18 @@ __global__ __launch_bounds__(kPubThreads) void k_publish(Dev d) {
 	unsigned long long abase = d.blk_abase[b];
 	for (uint32_t j0 = 0; j0 < cn; j0 += kPubClaims) { // uniform
 		const uint32_t j = j0 + (threadIdx.x >> 2);
-		uint32_t i = kNone, slot = 0, hl = 0, ul = 0;
+		uint32_t i = kNone, slot = 0, hl = 0, ul = 0, pid = 0;
 		const uint8_t *host = d.payload, *url = d.payload;
 		if (j < cn) {
-			i = d.cstage_ev[at0 + j];
-			slot = d.cstage_slot[at0 + j];
-			const ebd_event_result res = d.res[i];
-			const uint8_t* p = d.payload + d.off[i];
-			host = p + res.u.span.host_off;
-			hl = res.u.span.host_len;
-			url = p + res.u.span.url_off;
-			ul = res.u.span.url_len;
+			const ClaimRec cr = d.cstage[at0 + j];
+			i = 0;
+			slot = cr.slot;
+			pid = cr.pid;
+			const uint8_t* p = d.payload + cr.off;
+			host = p + cr.host_off;
+			hl = cr.host_len;
+			url = p + cr.url_off;
+			ul = cr.url_len;
 		}
 		const uint32_t n = hl + ul;
 		const uint32_t nb = (i != kNone && r == 0) ? ((n + 7u) & ~7u) : 0u; // counted once per claim
@@ -1906,7 +1911,7 @@ __global__ __launch_bounds__(kPubThreads) void k_publish(Dev d) {
 				if (listed) {
 					d.new_slots[li] = slot;
 					d.list_ep[li] = fits ? ep_at : ~0ull;
-					d.list_pl[li] = (unsigned long long)d.ev[i].pid | ((unsigned long long)n << 32);
+					d.list_pl[li] = (unsigned long long)pid | ((unsigned long long)n << 32);
 				} else {
 					set_error(d, EBD_ERR_TABLE_FULL);
 				}
