@@ -263,6 +263,7 @@ static void drain_timing(ebd_ctx* c) {
 static Dev make_dev(ebd_ctx* c) {
 	Dev d{};
 	d.dfa = c->d_dfa;
+	d.kcid = c->d_dfa + kLdsTableBytes;
 	d.di = c->dfa_host->info;
 	d.trie = c->d_trie;
 	d.ifs = c->d_ifs;
@@ -443,8 +444,9 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	}
 	std::vector<uint8_t> image(kLdsTableBytes); // the table as k_fresh keeps it in LDS
 	build_lds_image(c->dfa_host, image.data());
-	CTX_TRY(hipMalloc(&c->d_dfa, kLdsTableBytes));
-	CTX_TRY(hipMemcpy(c->d_dfa, image.data(), kLdsTableBytes, hipMemcpyHostToDevice));
+	image.insert(image.end(), c->dfa_host->kcid, c->dfa_host->kcid + 256); // dfa_parse's client ids follow the table
+	CTX_TRY(hipMalloc(&c->d_dfa, image.size()));
+	CTX_TRY(hipMemcpy(c->d_dfa, image.data(), image.size(), hipMemcpyHostToDevice));
 	CTX_TRY(hipMalloc(&c->d_trie, sizeof(KeyTrie)));
 	CTX_TRY(hipMemcpy(c->d_trie, &c->trie_host, sizeof(KeyTrie), hipMemcpyHostToDevice));
 	std::memset(&c->ifs_host, 0, sizeof(Interfaces));
@@ -1702,6 +1704,32 @@ int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t n
 	const uint32_t v[12] = {g.state, g.url_start, g.url_len, (g.f & GPF_HOST) ? g.host_start : 0,
 			(g.f & GPF_HOST) ? g.host_len : 0, g.cip_start, g.cip_len, g.f, g.cipkey, g.mcand, g.mlen,
 			(uint32_t)g.plen | ((uint32_t)g.pminor << 8)};
+	for (int k = 0; k < 12; k++)
+		out8[k] = v[k];
+	return 0;
+}
+
+// The session path's DFA walker (dfa_parse) over the same chunks: out8 as ebd_host_gp_parse's
+// (method and protocol prefix lengths are not kept by the walker: 0).
+int ebd_host_dfa_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,
+		uint32_t* consumed, uint32_t* out8) {
+	const KeyTrie* trie;
+	const DfaTable* t = host_dfa(&trie);
+	if (!t || !consumed || !out8)
+		return -EINVAL;
+	GenParser g;
+	gp_init(g);
+	uint64_t at = 0;
+	for (uint32_t k = 0; k < nchunks; k++) {
+		const uint8_t* p = data + at;
+		consumed[k] = dfa_parse(g, HostTab{t->next}, HostTab{t->kcid}, t->info, [p](uint32_t i) { return (uint32_t)p[i]; },
+				chunk_len[k], flags);
+		at += chunk_len[k];
+		if (reset_between && gp_done(g) && k + 1 < nchunks)
+			gp_reset(g);
+	}
+	const uint32_t v[12] = {g.state, g.url_start, g.url_len, (g.f & GPF_HOST) ? g.host_start : 0,
+			(g.f & GPF_HOST) ? g.host_len : 0, g.cip_start, g.cip_len, g.f, g.cipkey, g.mcand, 0, 0};
 	for (int k = 0; k < 12; k++)
 		out8[k] = v[k];
 	return 0;

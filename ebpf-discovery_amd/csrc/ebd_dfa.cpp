@@ -238,8 +238,15 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 	const int hvc_base = next_id;
 	newid[hvc_idx[0]] = hvc_base;
 	newid[hvc_idx[1]] = hvc_base + 1;
+	if (newid[0] != 0)
+		return -7; // the reset state must be id 0 (GenParser::ds after gp_init / gp_reset)
 
 	std::memset(out, 0, sizeof(*out));
+	for (int st = 0; st < 256; st++)
+		out->kcid[st] = kKcKeep;
+	for (int i = 0; i < n; i++)
+		if (states[i].state == ST_HDR_KEY)
+			out->kcid[newid[i]] = key_client_id(trie->type[states[i].key]);
 	DfaInfo& in = out->info;
 	in.nstates = (uint32_t)hvc_base + 2;
 	in.init = (uint32_t)newid[0];

@@ -35,7 +35,11 @@ struct DfaInfo {
 struct DfaTable {
 	DfaInfo info;
 	uint8_t next[256 * 256]; // next[s * 256 + byte]
+	// per state: the client-IP id (0 none, 1..5) of the header key a HEADER_KEY state has read
+	// so far (its trie node), kKcKeep for every other state (dfa_parse keeps the last id)
+	uint8_t kcid[256];
 };
+constexpr uint8_t kKcKeep = 7;
 
 // The table as the kernel keeps it in LDS: byte-major, entry (s, b) at b * kLdsStride + s.
 // A step's address is then one v_mad_u32_u24(b, kLdsStride, s) on the byte as loaded, with

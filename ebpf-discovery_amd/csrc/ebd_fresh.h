@@ -231,6 +231,117 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 	}
 }
 
+// ---------------------------------------------------------------------------------
+// The session path's parser: HttpRequestParser::parse (P:85-106) continued across the
+// buffers of a session (Discovery.cpp:123-139 handleExistingSession), as the projected DFA
+// plus the few fields the request needs.  The DFA is exact for a continued parse too: its
+// projection keeps everything that decides a future transition, whatever the sticky
+// clientIPKey (ebd_dfa.cpp checks every state against variants with it set).  What the DFA
+// forgets is which client-IP key a value belongs to, so the walker keeps the client id of
+// the last header key it read (DfaTable::kcid) and applies P:309-316 itself: the first
+// client-IP value sets clientIPKey when none is set (it stays set across reset, P:374-379),
+// and only the first header whose key equals it is the client address.
+// Spans are request-stream positions, as gp_step's.
+// ---------------------------------------------------------------------------------
+struct DfaWalk {
+	uint32_t s, kid, pos, f, cipkey, url_start, url_len, host_start, host_len, cip_start, cip_len, mcand;
+};
+
+EBD_HD void dfa_walk_load(const GenParser& g, DfaWalk& w) {
+	w.s = g.ds;
+	w.kid = g.kid;
+	w.pos = g.length;
+	w.f = g.f;
+	w.cipkey = g.cipkey;
+	w.url_start = g.url_start;
+	w.url_len = g.url_len;
+	w.host_start = g.host_start;
+	w.host_len = g.host_len;
+	w.cip_start = g.cip_start;
+	w.cip_len = g.cip_len;
+	w.mcand = g.mcand;
+}
+
+// One byte; returns true when the parse ended (FINISHED or INVALID).
+template <typename Tab, typename Kc>
+EBD_HD bool dfa_walk_step(const Tab& T, const Kc& KC, const DfaInfo& di, DfaWalk& w, uint32_t b) {
+	const uint32_t s = w.s, ns = T[(s << 8) | b], kc = KC[s];
+	w.kid = kc != kKcKeep ? kc : w.kid;
+	if (w.pos == 0)
+		w.mcand = b;
+	if (ns == di.url_id && s != di.url_id) // P:190-199: the URL starts with its '/'
+		w.url_start = w.pos;
+	if (s == di.url_id && ns != di.url_id) // P:201-213: it ends before the space
+		w.url_len = w.pos - w.url_start;
+	if (ns == di.hvh && s != di.hvh) { // P:309-310: the first Host value byte
+		w.host_start = w.pos;
+		w.f |= GPF_HOST;
+	}
+	if (s == di.hvh && ns != di.hvh)
+		w.host_len = w.pos - w.host_start;
+	if (ns >= di.hvc0 && s < di.hvc0) { // P:311-316: the first byte of a client-IP value
+		if (w.cipkey == 0)
+			w.cipkey = w.kid;
+		if (w.kid == w.cipkey && !(w.f & (GPF_CIP_FOUND | GPF_IN_CIP))) {
+			w.cip_start = w.pos;
+			w.f |= GPF_IN_CIP;
+		}
+	}
+	if (s >= di.hvc0 && ns < di.hvc0 && (w.f & GPF_IN_CIP)) { // the value's CR (P:248-257 parses it)
+		w.cip_len = w.pos - w.cip_start;
+		w.f = (w.f & ~(uint32_t)GPF_IN_CIP) | GPF_CIP_FOUND;
+	}
+	w.s = ns;
+	w.pos++;
+	return st_terminal(di, ns);
+}
+
+// The end of a parse() call: the DFA walk back into the session's GenParser.  done: the
+// parse ended (state FINISHED / INVALID as the DFA's terminal state says), with isHttps from
+// the event's flags (P:94-103, Discovery.cpp:136).
+EBD_HD void dfa_walk_store(const DfaInfo& di, const DfaWalk& w, bool done, uint8_t flags, GenParser& g) {
+	g.ds = (uint8_t)w.s;
+	g.kid = (uint8_t)w.kid;
+	g.length = w.pos;
+	g.cipkey = (uint8_t)w.cipkey;
+	g.url_start = w.url_start;
+	g.url_len = w.url_len;
+	g.host_start = w.host_start;
+	g.host_len = w.host_len;
+	g.cip_start = w.cip_start;
+	g.cip_len = w.cip_len;
+	g.mcand = (uint8_t)w.mcand;
+	uint32_t f = w.f;
+	if (done) {
+		g.state = w.s == di.inv ? ST_INVALID : ST_FINISHED;
+		f = (flags & 16) ? (f | GPF_HTTPS) : (f & ~(uint32_t)GPF_HTTPS);
+	}
+	g.f = (uint8_t)f;
+}
+
+// P:85-106 parse() of one buffer with the DFA: returns the bytes consumed (the host twin
+// of the device walker, which reads the buffer 16 bytes at a time).
+template <typename Tab, typename Kc, typename ByteAt>
+EBD_HD uint32_t dfa_parse(GenParser& g, const Tab& T, const Kc& KC, const DfaInfo& di, ByteAt at, uint32_t n, uint8_t flags) {
+	DfaWalk w;
+	dfa_walk_load(g, w);
+	uint32_t i = 0;
+	bool done = false;
+	while (i < n) {
+		if (w.pos > kMaxRequestLength) { // P:88-91
+			w.s = di.inv;
+			done = true;
+			break;
+		}
+		done = dfa_walk_step(T, KC, di, w, at(i));
+		i++;
+		if (done)
+			break;
+	}
+	dfa_walk_store(di, w, done, flags, g);
+	return i;
+}
+
 // Client-IP pass for one event (HttpRequestParser.cpp:370-407 parseClientIPValue on the
 // first client-IP header's value, Aggregator.cpp:50-74 on its front token): the raw value
 // runs from `cs` to the first ',' or the value's CR (value bytes are C-class, so a CR ends

@@ -22,6 +22,27 @@ namespace ebd {
 
 __device__ __forceinline__ void set_error(const Dev& d, unsigned long long bit) { atomicOr(&d.ctr[CTR_ERRORS], bit); }
 
+// A global counter bumped by the active lanes of a wave together: one atomic for the wave
+// instead of one per lane (a hot counter serialises its atomics at the memory side; the
+// session path bumps several per event).  Returns this lane's offset: the counter's value
+// before the wave plus the sizes of the active lanes below this one.  Works in divergent
+// code: only the lanes active at the call take part.
+__device__ __forceinline__ unsigned long long wave_add(unsigned long long* ctr, unsigned long long size) {
+	const unsigned long long act = __ballot(1);
+	const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((long long)act) - 1u;
+	unsigned long long pre = 0, tot = 0;
+	for (unsigned long long m = act; m; m &= m - 1) { // uniform: the active lanes' sizes, in lane order
+		const uint32_t l = (uint32_t)__ffsll((long long)m) - 1u;
+		const unsigned long long v = __shfl(size, (int)l);
+		pre += l < lane ? v : 0ull;
+		tot += v;
+	}
+	unsigned long long base = 0;
+	if (lane == leader)
+		base = atomicAdd(ctr, tot);
+	return __shfl(base, (int)leader) + pre;
+}
+
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -257,7 +278,7 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 			if (t == 0) {
 				s->kv = kv;
 				s->sid = sid;
-				const unsigned long long k = atomicAdd(&d.ctr[CTR_DIRTY], 1ull);
+				const unsigned long long k = wave_add(&d.ctr[CTR_DIRTY], 1ull);
 				d.dirty[k] = idx;
 				t = tag;
 			}
@@ -560,7 +581,7 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
 	d.res[i] = r;
 	const EventRec& ev = d.ev[i];
-	atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+	wave_add(&d.ctr[CTR_UNFINISHED], 1ull);
 	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 }
 
@@ -674,7 +695,7 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 #endif
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
-		atomicAdd(&d.ctr[CTR_UNFINISHED], 1ull);
+		wave_add(&d.ctr[CTR_UNFINISHED], 1ull);
 		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
 	}
 	d.res[i] = fr.r;
@@ -950,6 +971,42 @@ void k_fresh(Dev d) {
 						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
 #endif
 			}
+#if defined(EBD_EXP_SPLIT4) // experiment: every chunk its own chain (ILP probe; results are wrong)
+			{
+				uint32_t sx[4], m[4], qs[4], qm[4];
+#pragma unroll
+				for (int k = 0; k < 4; k++) {
+					sx[k] = s ^ (uint32_t)k;
+					scan_chunk(T, X[k], di.vl0, di.vl1, sx[k], m[k], qs[k], qm[k]);
+				}
+				if (live) {
+#pragma unroll
+					for (int k = 0; k < 4; k++)
+						chunk_update(di, sr, 4 * w0 + k, s ^ (uint32_t)k, qs[k], qm[k], m[k]);
+					live = !st_terminal(di, sx[3]) && 64 * (w0 + 1) < e0.L ? 1u : 0u;
+					s = sx[0] ^ sx[1] ^ sx[2] ^ sx[3];
+				}
+			}
+#elif defined(EBD_EXP_SPLIT) // experiment: chunks 0-1 and 2-3 as two independent chains (ILP probe; results are wrong)
+			{
+				uint32_t sa = s, sb = s ^ 1u, m0, qs0, qm0, m1, qs1, qm1;
+				scan_chunk(T, X[0], di.vl0, di.vl1, sa, m0, qs0, qm0);
+				scan_chunk(T, X[2], di.vl0, di.vl1, sb, m1, qs1, qm1);
+				if (live)
+					chunk_update(di, sr, 4 * w0 + 0, s, qs0, qm0, m0);
+				if (live)
+					chunk_update(di, sr, 4 * w0 + 2, s ^ 1u, qs1, qm1, m1);
+				const uint32_t sa1 = sa, sb1 = sb;
+				scan_chunk(T, X[1], di.vl0, di.vl1, sa, m0, qs0, qm0);
+				scan_chunk(T, X[3], di.vl0, di.vl1, sb, m1, qs1, qm1);
+				if (live) {
+					chunk_update(di, sr, 4 * w0 + 1, sa1, qs0, qm0, m0);
+					chunk_update(di, sr, 4 * w0 + 3, sb1, qs1, qm1, m1);
+					live = !st_terminal(di, sa) && !st_terminal(di, sb) && 64 * (w0 + 1) < e0.L ? 1u : 0u;
+					s = sa ^ sb ^ s;
+				}
+			}
+#else
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
@@ -980,11 +1037,15 @@ void k_fresh(Dev d) {
 					s = sx;
 				}
 			}
+#endif
 			w0++;
 			done = !live;
 		}
 #ifndef EBD_EXP_NOPUSH // experiment: no records for finalize (results are wrong)
 		push(done);
+#else // every result NONE, so that the kernels after k_fresh follow no span of a parse it did not finish
+		if (done)
+			write_none(d, e0.idx);
 #endif
 		if (done) {
 			e0 = e1;
@@ -1057,7 +1118,7 @@ __global__ void k_slow_collect(Dev d) {
 		if (slot >= 0) {
 			d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
 			atomicMax(&d.sset[slot].last_ev, i + 1);
-			const unsigned long long k = atomicAdd(&d.ctr[CTR_SLOW], 1ull);
+			const unsigned long long k = wave_add(&d.ctr[CTR_SLOW], 1ull);
 			d.slow_keys[k] = ((unsigned long long)(uint32_t)slot << 32) | i;
 		}
 	}
@@ -1105,6 +1166,53 @@ struct ByteWin {
 	}
 };
 
+// The session path's tables in LDS: the DFA image (byte-major, LdsTable) and the client id
+// of each header-key state (DfaTable::kcid).
+struct SessTabs {
+	const uint8_t* T;
+	const uint8_t* KC;
+};
+struct ByteTab {
+	const uint8_t* t;
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
+};
+
+// dfa_parse (ebd_fresh.h) over one buffer on the device: 16-byte aligned blocks, the next
+// one loaded while the current one is walked, 16 predicated steps per block.  The aligned
+// block holding a valid byte never leaves that byte's page, so the over-read cannot fault.
+__device__ uint32_t dfa_parse_dev(GenParser& g, const SessTabs& tb, const DfaInfo& di, const uint8_t* p, uint32_t n, uint8_t flags) {
+	DfaWalk w;
+	dfa_walk_load(g, w);
+	const LdsTable T{tb.T};
+	const ByteTab KC{tb.KC};
+	const uintptr_t a0 = (uintptr_t)p, a1 = a0 + n;
+	uintptr_t blk = a0 & ~(uintptr_t)15;
+	uint32_t i = 0;
+	bool done = false;
+	uint4 cur = n ? *(const uint4*)blk : uint4{0u, 0u, 0u, 0u};
+	while (!done && blk < a1) {
+		const uint4 nx = blk + 16 < a1 ? *(const uint4*)(blk + 16) : cur;
+		const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+#pragma unroll
+		for (int k = 0; k < 16; k++) {
+			const uintptr_t a = blk + (uintptr_t)k;
+			if (!done && a >= a0 && a < a1) {
+				if (w.pos > kMaxRequestLength) { // P:88-91
+					w.s = di.inv;
+					done = true;
+				} else {
+					done = dfa_walk_step(T, KC, di, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu);
+					i++;
+				}
+			}
+		}
+		cur = nx;
+		blk += 16;
+	}
+	dfa_walk_store(di, w, done, flags, g);
+	return i;
+}
+
 // Visits stream bytes [a, a + n) in order; the stream ends at sorted position jend whose
 // piece is truncated to cend bytes.  fn(byte) returns false to stop.  Returns bytes visited.
 template <typename Fn>
@@ -1150,7 +1258,7 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	if (g.f & GPF_CIP_FOUND) // the value up to its first ',' is the front token's source
 		raw = stream_visit(d, w, jend, cend, g.cip_start, g.cip_len, [](uint8_t c) { return c != ','; });
 	const uint32_t total = hl + ul + raw;
-	const unsigned long long at = atomicAdd(&d.ctr[CTR_SSTR], (unsigned long long)total);
+	const unsigned long long at = wave_add(&d.ctr[CTR_SSTR], (unsigned long long)total);
 	uint8_t info = (uint8_t)((g.mcand == 'P' ? EBD_INFO_POST : 0) | ((g.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0) | EBD_INFO_SESSION);
 	uint8_t cls;
 	KeyHasher kh;
@@ -1189,12 +1297,11 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 	const uint32_t slot = agg_insert(d, kh.finish(), first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl),
 			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (claimed) // a rare path: one reservation per claim
-		claim_publish(d, slot, atomicAdd(&d.ctr[CTR_SERVICES], 1ull),
-				atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
+		claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull),
+				wave_add(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
 	if (d.net_on && cls == CLS_EXTERNAL)
 		agg_nets(d, slot, net);
-	atomicAdd(&d.ctr[CTR_REQUESTS], 1ull);
-	const unsigned long long q = atomicAdd(&d.ctr[CTR_SREQ], 1ull);
+	const unsigned long long q = wave_add(&d.ctr[CTR_SREQ], 1ull); // CTR_REQUESTS: the walkers add CTR_SREQ
 	SessReq sr;
 	sr.seq = d.seq_base + i;
 	sr.pid = ev.pid;
@@ -1228,7 +1335,7 @@ enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
 // Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
 // session's state in S.  Returns the LRU operation it implies; an insert (saveSession,
 // Discovery.cpp:148-150) is left to the caller, which may have to evict first.
-__device__ uint32_t session_event(const Dev& d, const KeyTrie* trie, SessState& S, uint32_t jj) {
+__device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S, uint32_t jj) {
 	const uint32_t i = slow_event(d, jj);
 	const EventRec& ev = d.ev[i];
 	const uint8_t flags = ev.flags;
@@ -1239,14 +1346,13 @@ __device__ uint32_t session_event(const Dev& d, const KeyTrie* trie, SessState& 
 	r.info = EBD_INFO_SESSION;
 	r.u.session.index = 0xffffffffu;
 	r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
-	atomicAdd(&d.ctr[CTR_SESSION_EVENTS], 1ull);
-	uint32_t op = OP_NONE;
+	uint32_t op = OP_NONE; // CTR_SESSION_EVENTS: the walkers count the events they replay
 	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
-		ByteWin at(d.payload + d.off[i]);
+		const uint8_t* buf = d.payload + d.off[i];
 		if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
 			S.stamp = d.seq_base + i;
 			r.info |= EBD_INFO_EXISTING;
-			const uint32_t c = gp_parse(S.g, trie, at, L, flags);
+			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
 			r.consumed = (uint16_t)c;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
@@ -1264,7 +1370,7 @@ __device__ uint32_t session_event(const Dev& d, const KeyTrie* trie, SessState& 
 		} else { // handleNewSession, Discovery.cpp:141-159
 			gp_init(S.g);
 			S.w = Walk{nullptr, 0, jj};
-			const uint32_t c = gp_parse(S.g, trie, at, L, flags);
+			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
 			r.consumed = (uint16_t)c;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
@@ -1310,7 +1416,7 @@ __device__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t s
 // A session still in the LRU after the batch, with the bytes of its request in progress
 // (which ends with the session's last event jlast of the batch, fully consumed).
 __device__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, uint32_t jlast) {
-	const unsigned long long c = atomicAdd(&d.ctr[CTR_CARRY_OUT], 1ull);
+	const unsigned long long c = wave_add(&d.ctr[CTR_CARRY_OUT], 1ull);
 	if (c >= d.carry_cap) {
 		set_error(d, EBD_ERR_LRU_OVERFLOW);
 		return;
@@ -1337,10 +1443,11 @@ __device__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, 
 // live sessions first).  The header-key trie and the byte classes sit in LDS: the walk
 // reads them once per byte.
 __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
-	__shared__ KeyTrie trie;
-	for (uint32_t k = threadIdx.x; k < (uint32_t)sizeof(KeyTrie); k += kWalkThreads)
-		((uint8_t*)&trie)[k] = ((const uint8_t*)d.trie)[k];
+	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
+	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
+		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
 	__syncthreads();
+	const SessTabs tb{tabs, tabs + kLdsTableBytes};
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	for (uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x; h < nh; h += gridDim.x * kWalkThreads) {
 		const uint32_t j = d.heads[h];
@@ -1349,7 +1456,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 		session_begin(d, S, j, slot);
 		uint32_t jj = j;
 		for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
-			const uint32_t op = session_event(d, &trie, S, jj);
+			const uint32_t op = session_event(d, tb, S, jj);
 			if (op == OP_INSERT) {
 				S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
 				S.stamp = d.seq_base + slow_event(d, jj);
@@ -1359,6 +1466,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 		if (S.live)
 			session_carry_out(d, S, j, jj - 1);
 	}
+}
+
+// After a walker: every sorted session event was replayed once (Discovery::handleNewEvent)
+// and every session request counted once (the walkers bump no per-event counter).
+__global__ void k_sess_tally(Dev d) {
+	d.ctr[CTR_SESSION_EVENTS] += d.ctr[CTR_SLOW];
+	d.ctr[CTR_REQUESTS] += d.ctr[CTR_SREQ];
 }
 
 // Saved sessions with no event in this batch stay saved unchanged.
@@ -1463,10 +1577,11 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 	__shared__ uint32_t nord, nlive, k_next, evict_for;
 	__shared__ unsigned long long rs[kLruThreads];
 	__shared__ uint32_t ri[kLruThreads];
-	__shared__ KeyTrie trie;
+	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	const uint32_t t = threadIdx.x;
-	for (uint32_t k = t; k < (uint32_t)sizeof(KeyTrie); k += kLruThreads)
-		((uint8_t*)&trie)[k] = ((const uint8_t*)d.trie)[k];
+	for (uint32_t k = t * 16u; k < kLdsTableBytes + 256; k += kLruThreads * 16u)
+		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
+	const SessTabs tb{tabs, tabs + kLdsTableBytes};
 	if (t == 0)
 		nlive = 0;
 	__syncthreads();
@@ -1521,7 +1636,7 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 				uint32_t e = kNone;
 				for (; k < nord; k++) {
 					const uint32_t jj = ord[k], h = head[jj];
-					const uint32_t op = session_event(d, &trie, S[h], jj);
+					const uint32_t op = session_event(d, tb, S[h], jj);
 					if (op == OP_ERASE && S[h].li != kNone) {
 						live_remove(S, live, nlive, h);
 					} else if (op == OP_INSERT) {
@@ -2399,12 +2514,14 @@ hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_
 	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, jpos, head);
 	hipLaunchKernelGGL(k_walk_lru, dim3(1), dim3(kLruThreads), 0, st, d, nslow, (const uint32_t*)jpos, (const uint32_t*)head, S,
 			live, cap);
+	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
 	return hipGetLastError();
 }
 size_t sess_state_bytes() { return sizeof(SessState); }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
-	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * 4)), dim3(kWalkThreads), 0, st, d);
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * 3)), dim3(kWalkThreads), 0, st, d);
+	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {

@@ -127,6 +127,9 @@ struct GenParser {
 	uint8_t key;          // trie node of currentHeader.key
 	uint8_t cipkey;       // sticky result.clientIPKey: 0 none, 1..5 (P:73-80 does not clear it)
 	uint8_t f;            // GPF_*
+	uint8_t ds;           // the session path's DFA state (dfa_parse, ebd_fresh.h); 0 = reset
+	uint8_t kid;          // dfa_parse: client-IP id (0..5) of the last header key it walked
+	uint8_t pad_[2];
 	uint32_t length;      // bytes since reset (P:88-91)
 	uint32_t url_start, url_len, host_start, host_len, cip_start, cip_len;
 };
@@ -137,6 +140,9 @@ EBD_HD void gp_init(GenParser& g) {
 	g.key = kTrieRoot;
 	g.cipkey = 0;
 	g.f = 0;
+	g.ds = 0;
+	g.kid = 0;
+	g.pad_[0] = g.pad_[1] = 0;
 	g.length = 0;
 	g.url_start = g.url_len = g.host_start = g.host_len = g.cip_start = g.cip_len = 0;
 }

@@ -143,6 +143,7 @@ _SIGS = {
     "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
                                  C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ebd_host_gp_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
+    "ebd_host_dfa_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
     "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_uint32]),
     "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
@@ -518,14 +519,15 @@ def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_
     return out[0], (int(key[0]), int(key[1]))
 
 
-def host_gp_parse(chunks, flags=FLAG_UNENCRYPTED, reset_between=False):
+def host_gp_parse(chunks, flags=FLAG_UNENCRYPTED, reset_between=False, walker="gp"):
+    """The generic parser (walker "gp") or the session path's DFA walker ("dfa") over the chunks."""
     data = b"".join(chunks)
     d = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
     cl = np.array([len(c) for c in chunks], np.uint32) if chunks else np.zeros(1, np.uint32)
     cons = np.zeros(max(len(chunks), 1), np.uint32)
     o = np.zeros(12, np.uint32)
-    _check(lib().ebd_host_gp_parse(_p(d), _p(cl), len(chunks), flags, int(reset_between), _p(cons), _p(o)),
-           "ebd_host_gp_parse")
+    fn = lib().ebd_host_gp_parse if walker == "gp" else lib().ebd_host_dfa_parse
+    _check(fn(_p(d), _p(cl), len(chunks), flags, int(reset_between), _p(cons), _p(o)), "ebd_host_%s_parse" % walker)
     keys = ["state", "url_start", "url_len", "host_start", "host_len", "cip_start", "cip_len", "f", "cipkey", "mcand",
             "mlen", "proto"]
     return [int(x) for x in cons[:len(chunks)]], dict(zip(keys, (int(x) for x in o))), data

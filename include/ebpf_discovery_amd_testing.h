@@ -32,6 +32,11 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,
 		uint32_t* consumed, uint32_t* out8);
 
+/* The session path's DFA walker (dfa_parse, ebd_fresh.h) over the same chunks: out8 as
+ * ebd_host_gp_parse's, with mlen and plen 0 (the walker does not keep them). */
+int ebd_host_dfa_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,
+		uint32_t* consumed, uint32_t* out8);
+
 /* Client classification: a client-IP value token (front_token + classify_token) or,
  * with is_source, the 16 source-address bytes under `flags`.  Returns 0/1/2. */
 int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t flags, const ebd_ipv4_network* v4,

@@ -372,3 +372,76 @@ def test_word_skip_states_are_printable_self_loops():
     for v in vls:
         assert np.all(T[v, 0x20:0x7F] == v)
         assert T[v, ord("\r")] != v  # CR ends the value
+
+
+# ---------------------------------------------------------------------------------
+# The session path's DFA walker (dfa_parse) against the generic parser gp_step: the same
+# chunks, the same consumed counts and outcome, the same spans and sticky key.
+# ---------------------------------------------------------------------------------
+def _walkers_agree(chunks, flags=UNENC, reset_between=False):
+    cg, sg, data = ebd.host_gp_parse(chunks, flags, reset_between)
+    cd, sd, _ = ebd.host_gp_parse(chunks, flags, reset_between, walker="dfa")
+    assert cd == cg, (chunks, cd, cg)
+    fin = {10: 10, 11: 11}
+    assert fin.get(sd["state"], -1) == fin.get(sg["state"], -1), (chunks, sd, sg)
+    assert sd["cipkey"] == sg["cipkey"], (chunks, sd, sg)
+    if sg["state"] == 10:
+        keys = ["url_start", "url_len", "host_start", "host_len", "mcand"]
+        if sg["f"] & 2:
+            keys += ["cip_start", "cip_len"]
+        assert {k: sd[k] for k in keys} == {k: sg[k] for k in keys}, (chunks, sd, sg)
+        assert sd["f"] & (1 | 2 | 8) == sg["f"] & (1 | 2 | 8), (chunks, sd, sg)
+
+
+def test_dfa_walker_equals_generic_parser_on_vectors(vectors):
+    for case in vectors["parser_valid"] + vectors["parser_invalid"]:
+        chunks = [b(c) for c in case["chunks"]]
+        _walkers_agree(chunks, SSL if case.get("is_https") else UNENC)
+        whole = b"".join(chunks)
+        for cut in range(0, len(whole) + 1, 3):
+            _walkers_agree([whole[:cut], whole[cut:]])
+
+
+def test_dfa_walker_length_cap_and_sticky_key():
+    for total in (8193, 8194):
+        req = b"GET /" + b"a" * (total - 18) + b" HTTP/1.1\r\n\r\n"
+        _walkers_agree([req[:8192], req[8192:]])
+        _walkers_agree([req[:100], req[100:5000], req[5000:]])
+    first = b"GET / HTTP/1.1\r\nX-Forwarded-For: 1.2.3.4\r\n\r\n"
+    second = b"GET / HTTP/1.1\r\nTrue-Client-IP: 5.6.7.8\r\nx-forwarded-for: 9.9.9.9\r\n\r\n"
+    _walkers_agree([first, second], reset_between=True)
+    cons, st, data = ebd.host_gp_parse([first, second], reset_between=True, walker="dfa")
+    base = len(first)
+    assert data[base + st["cip_start"]:base + st["cip_start"] + st["cip_len"]] == b"9.9.9.9"
+
+
+def test_dfa_walker_random_sessions():
+    """Keep-alive sessions of mutated requests cut at random points: every prefix of the
+    chunk list through both walkers (reset after each finished request, as a kept session)."""
+    rng = random.Random(11)
+    keys = ["X-Forwarded-For", "true-client-ip", "X-Client-IP", "x-http-client-ip", "Rproxy_Remote_Address",
+            "rproxy_remote_addressXYZ", "X-Forwarded-Fo", "Host", "User-Agent"]
+    alphabet = b"GETPOS /:\r\n ,.[]abcXx-_0123456789\x01\x7f"
+    for it in range(600):
+        reqs = []
+        for _ in range(rng.randint(1, 4)):
+            hdrs = [b"Host: h%d.example:80" % rng.randint(0, 9)] if rng.random() < 0.8 else []
+            for _ in range(rng.randint(0, 3)):
+                k = rng.choice(keys).encode()
+                if rng.random() < 0.2:
+                    k = k.replace(b"-", b" - ", 1)
+                hdrs.append(k + b":" + b" " * rng.randint(0, 2) + rng.choice(
+                    [b"1.2.3.4", b"[2001:db8::1]:80", b"10.0.0.1, 8.8.8.8", b"x", b"fd00::1"]))
+            rng.shuffle(hdrs)
+            r = bytearray((b"POST " if rng.random() < 0.2 else b"GET ") + b"/p%d?q=1 HTTP/1.%d\r\n" % (
+                rng.randint(0, 99), rng.randint(0, 1)) + b"".join(h + b"\r\n" for h in hdrs) + b"\r\n")
+            if rng.random() < 0.3:
+                for _ in range(rng.randint(1, 2)):
+                    k = rng.randrange(len(r))
+                    r[k] = rng.choice(alphabet)
+            reqs.append(bytes(r))
+        stream = b"".join(reqs)
+        cuts = sorted(rng.sample(range(1, len(stream)), min(len(stream) - 1, rng.randint(1, 6))))
+        chunks = [stream[a:b] for a, b in zip([0] + cuts, cuts + [len(stream)])]
+        for k in range(1, len(chunks) + 1):
+            _walkers_agree(chunks[:k], SSL if it & 1 else UNENC, reset_between=True)
