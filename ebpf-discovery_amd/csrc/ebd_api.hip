@@ -263,7 +263,7 @@ static void drain_timing(ebd_ctx* c) {
 static Dev make_dev(ebd_ctx* c) {
 	Dev d{};
 	d.dfa = c->d_dfa;
-	d.kcid = c->d_dfa + kLdsTableBytes;
+	d.attr = c->d_dfa + kLdsTableBytes;
 	d.di = c->dfa_host->info;
 	d.trie = c->d_trie;
 	d.ifs = c->d_ifs;
@@ -444,7 +444,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	}
 	std::vector<uint8_t> image(kLdsTableBytes); // the table as k_fresh keeps it in LDS
 	build_lds_image(c->dfa_host, image.data());
-	image.insert(image.end(), c->dfa_host->kcid, c->dfa_host->kcid + 256); // dfa_parse's client ids follow the table
+	image.insert(image.end(), c->dfa_host->attr, c->dfa_host->attr + 256); // dfa_parse's state attributes follow the table
 	CTX_TRY(hipMalloc(&c->d_dfa, image.size()));
 	CTX_TRY(hipMemcpy(c->d_dfa, image.data(), image.size(), hipMemcpyHostToDevice));
 	CTX_TRY(hipMalloc(&c->d_trie, sizeof(KeyTrie)));
@@ -1722,7 +1722,7 @@ int ebd_host_dfa_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t 
 	uint64_t at = 0;
 	for (uint32_t k = 0; k < nchunks; k++) {
 		const uint8_t* p = data + at;
-		consumed[k] = dfa_parse(g, HostTab{t->next}, HostTab{t->kcid}, t->info, [p](uint32_t i) { return (uint32_t)p[i]; },
+		consumed[k] = dfa_parse(g, HostTab{t->next}, HostTab{t->attr}, t->info, [p](uint32_t i) { return (uint32_t)p[i]; },
 				chunk_len[k], flags);
 		at += chunk_len[k];
 		if (reset_between && gp_done(g) && k + 1 < nchunks)

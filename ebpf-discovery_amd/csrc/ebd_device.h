@@ -130,7 +130,7 @@ static_assert(sizeof(ClaimRec) == 24, "claim record is 24 bytes");
 struct Dev {
 	// immutable tables
 	const uint8_t* dfa;
-	const uint8_t* kcid; // DfaTable::kcid (the session path's dfa_parse)
+	const uint8_t* attr; // DfaTable::attr (the session path's dfa_parse)
 	DfaInfo di;
 	const KeyTrie* trie;
 	const Interfaces* ifs;

@@ -243,10 +243,10 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 
 	std::memset(out, 0, sizeof(*out));
 	for (int st = 0; st < 256; st++)
-		out->kcid[st] = kKcKeep;
+		out->attr[st] = kKcKeep;
 	for (int i = 0; i < n; i++)
 		if (states[i].state == ST_HDR_KEY)
-			out->kcid[newid[i]] = key_client_id(trie->type[states[i].key]);
+			out->attr[newid[i]] = key_client_id(trie->type[states[i].key]);
 	DfaInfo& in = out->info;
 	in.nstates = (uint32_t)hvc_base + 2;
 	in.init = (uint32_t)newid[0];
@@ -318,6 +318,14 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 	}
 	if (nvl > 2)
 		return -6;
+	for (uint32_t st = 0; st < 256; st++) {
+		uint32_t a = out->attr[st];
+		a |= st == in.url_id ? A_URL : 0u;
+		a |= st == in.hvh ? A_HVH : 0u;
+		a |= st >= in.hvc0 && st < in.nstates ? A_HVC : 0u;
+		a |= st - in.g4 < 3u ? A_TERM : 0u;
+		out->attr[st] = (uint8_t)a;
+	}
 	return 0;
 }
 

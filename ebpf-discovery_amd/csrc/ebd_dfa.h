@@ -35,11 +35,13 @@ struct DfaInfo {
 struct DfaTable {
 	DfaInfo info;
 	uint8_t next[256 * 256]; // next[s * 256 + byte]
-	// per state: the client-IP id (0 none, 1..5) of the header key a HEADER_KEY state has read
-	// so far (its trie node), kKcKeep for every other state (dfa_parse keeps the last id)
-	uint8_t kcid[256];
+	// per state, for the session path's walker (dfa_parse, ebd_fresh.h): bits 0-2 the client-IP
+	// id (0 none, 1..5) of the header key a HEADER_KEY state has read so far (its trie node),
+	// kKcKeep for every other state; then one bit per span boundary the walker records
+	uint8_t attr[256];
 };
 constexpr uint8_t kKcKeep = 7;
+enum : uint32_t { A_URL = 8, A_HVH = 16, A_HVC = 32, A_TERM = 64 }; // s == url_id, s == hvh, s >= hvc0, terminal
 
 // The table as the kernel keeps it in LDS: byte-major, entry (s, b) at b * kLdsStride + s.
 // A step's address is then one v_mad_u32_u24(b, kLdsStride, s) on the byte as loaded, with

@@ -238,108 +238,116 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 // projection keeps everything that decides a future transition, whatever the sticky
 // clientIPKey (ebd_dfa.cpp checks every state against variants with it set).  What the DFA
 // forgets is which client-IP key a value belongs to, so the walker keeps the client id of
-// the last header key it read (DfaTable::kcid) and applies P:309-316 itself: the first
-// client-IP value sets clientIPKey when none is set (it stays set across reset, P:374-379),
-// and only the first header whose key equals it is the client address.
+// the last header-key state it left (DfaTable::attr bits 0-2) and applies P:309-316 itself:
+// the first client-IP value sets clientIPKey when none is set (it stays set across reset,
+// P:374-379), and only the first header whose key equals it is the client address.
+// A step is branch-free (lanes of a wave walk different sessions): one table read, one
+// attribute read, and selects on the attribute bits that changed.  Terminal states step to
+// themselves, so bytes after the end change nothing but the position.
 // Spans are request-stream positions, as gp_step's.
 // ---------------------------------------------------------------------------------
 struct DfaWalk {
-	uint32_t s, kid, pos, f, cipkey, url_start, url_len, host_start, host_len, cip_start, cip_len, mcand;
+	uint32_t s, a, kid, pos, f, cipkey, mcand, tpos;
+	uint32_t url_start, url_end, host_start, host_end, cip_start, cip_end;
 };
 
-EBD_HD void dfa_walk_load(const GenParser& g, DfaWalk& w) {
+EBD_HD void dfa_walk_load(const GenParser& g, uint32_t attr_s, DfaWalk& w) {
 	w.s = g.ds;
+	w.a = attr_s;
 	w.kid = g.kid;
 	w.pos = g.length;
 	w.f = g.f;
 	w.cipkey = g.cipkey;
-	w.url_start = g.url_start;
-	w.url_len = g.url_len;
-	w.host_start = g.host_start;
-	w.host_len = g.host_len;
-	w.cip_start = g.cip_start;
-	w.cip_len = g.cip_len;
 	w.mcand = g.mcand;
+	w.tpos = kNone;
+	w.url_start = g.url_start;
+	w.url_end = g.url_start + g.url_len;
+	w.host_start = g.host_start;
+	w.host_end = g.host_start + g.host_len;
+	w.cip_start = g.cip_start;
+	w.cip_end = g.cip_start + g.cip_len;
 }
 
-// One byte; returns true when the parse ended (FINISHED or INVALID).
-template <typename Tab, typename Kc>
-EBD_HD bool dfa_walk_step(const Tab& T, const Kc& KC, const DfaInfo& di, DfaWalk& w, uint32_t b) {
-	const uint32_t s = w.s, ns = T[(s << 8) | b], kc = KC[s];
-	w.kid = kc != kKcKeep ? kc : w.kid;
-	if (w.pos == 0)
-		w.mcand = b;
-	if (ns == di.url_id && s != di.url_id) // P:190-199: the URL starts with its '/'
-		w.url_start = w.pos;
-	if (s == di.url_id && ns != di.url_id) // P:201-213: it ends before the space
-		w.url_len = w.pos - w.url_start;
-	if (ns == di.hvh && s != di.hvh) { // P:309-310: the first Host value byte
-		w.host_start = w.pos;
-		w.f |= GPF_HOST;
-	}
-	if (s == di.hvh && ns != di.hvh)
-		w.host_len = w.pos - w.host_start;
-	if (ns >= di.hvc0 && s < di.hvc0) { // P:311-316: the first byte of a client-IP value
-		if (w.cipkey == 0)
-			w.cipkey = w.kid;
-		if (w.kid == w.cipkey && !(w.f & (GPF_CIP_FOUND | GPF_IN_CIP))) {
-			w.cip_start = w.pos;
-			w.f |= GPF_IN_CIP;
-		}
-	}
-	if (s >= di.hvc0 && ns < di.hvc0 && (w.f & GPF_IN_CIP)) { // the value's CR (P:248-257 parses it)
-		w.cip_len = w.pos - w.cip_start;
-		w.f = (w.f & ~(uint32_t)GPF_IN_CIP) | GPF_CIP_FOUND;
-	}
+// One byte b if `valid` (otherwise nothing changes); w.tpos = the bytes of the request up
+// to and including the byte that made the state terminal.
+template <typename Tab, typename At>
+EBD_HD void dfa_walk_step(const Tab& T, const At& A, DfaWalk& w, uint32_t b, bool valid) {
+	const uint32_t ns = valid ? (uint32_t)T[(w.s << 8) | b] : w.s;
+	const uint32_t an = A[ns], ao = w.a, x = an ^ ao, en = an & x, lv = ao & x;
+	const uint32_t ko = ao & 7u, pos = w.pos;
+	w.kid = ko != kKcKeep ? ko : w.kid;
+	w.mcand = pos == 0 && valid ? b : w.mcand;
+	w.url_start = (en & A_URL) ? pos : w.url_start; // P:190-199: the URL starts with its '/'
+	w.url_end = (lv & A_URL) ? pos : w.url_end;     // P:201-213: it ends before the space
+	w.host_start = (en & A_HVH) ? pos : w.host_start; // P:309-310: the first Host value byte
+	w.host_end = (lv & A_HVH) ? pos : w.host_end;
+	w.f |= (en & A_HVH) ? (uint32_t)GPF_HOST : 0u;
+	// P:311-316: the first byte of a client-IP value; its key is the last key state's
+	const bool ce = (en & A_HVC) != 0;
+	const uint32_t ck = w.cipkey ? w.cipkey : w.kid;
+	w.cipkey = ce ? ck : w.cipkey;
+	const bool take = ce && w.kid == ck && !(w.f & (GPF_CIP_FOUND | GPF_IN_CIP));
+	w.cip_start = take ? pos : w.cip_start;
+	w.f |= take ? (uint32_t)GPF_IN_CIP : 0u;
+	const bool cl = (lv & A_HVC) && (w.f & GPF_IN_CIP); // the value's CR (P:248-257 parses it)
+	w.cip_end = cl ? pos : w.cip_end;
+	w.f = cl ? ((w.f & ~(uint32_t)GPF_IN_CIP) | GPF_CIP_FOUND) : w.f;
+	w.tpos = valid && (an & A_TERM) && w.tpos == kNone ? pos + 1 : w.tpos; // (a parse() on an ended parser takes one byte)
 	w.s = ns;
-	w.pos++;
-	return st_terminal(di, ns);
+	w.a = an;
+	w.pos = pos + (valid ? 1u : 0u);
 }
 
-// The end of a parse() call: the DFA walk back into the session's GenParser.  done: the
-// parse ended (state FINISHED / INVALID as the DFA's terminal state says), with isHttps from
-// the event's flags (P:94-103, Discovery.cpp:136).
-EBD_HD void dfa_walk_store(const DfaInfo& di, const DfaWalk& w, bool done, uint8_t flags, GenParser& g) {
+// The end of a parse() call that walked `ne` of the buffer's `n` bytes (ne < n: the request
+// reached the length cap, P:88-91): the walk back into the session's GenParser.  Returns the
+// bytes consumed.  A parse that ended takes isHttps from the event's flags (P:94-103).
+EBD_HD uint32_t dfa_walk_store(const DfaInfo& di, DfaWalk& w, uint32_t pos0, uint32_t ne, uint32_t n, uint8_t flags,
+		GenParser& g) {
+	uint32_t consumed = ne, f = w.f;
+	bool done = false;
+	if (w.tpos != kNone) {
+		consumed = w.tpos - pos0;
+		done = true;
+	} else if (ne < n) {
+		w.s = di.inv;
+		done = true;
+	}
 	g.ds = (uint8_t)w.s;
 	g.kid = (uint8_t)w.kid;
-	g.length = w.pos;
+	g.length = pos0 + consumed;
 	g.cipkey = (uint8_t)w.cipkey;
-	g.url_start = w.url_start;
-	g.url_len = w.url_len;
-	g.host_start = w.host_start;
-	g.host_len = w.host_len;
-	g.cip_start = w.cip_start;
-	g.cip_len = w.cip_len;
 	g.mcand = (uint8_t)w.mcand;
-	uint32_t f = w.f;
+	g.url_start = w.url_start;
+	g.url_len = w.url_end - w.url_start;
+	g.host_start = w.host_start;
+	g.host_len = w.host_end - w.host_start;
+	g.cip_start = w.cip_start;
+	g.cip_len = w.cip_end - w.cip_start;
 	if (done) {
 		g.state = w.s == di.inv ? ST_INVALID : ST_FINISHED;
 		f = (flags & 16) ? (f | GPF_HTTPS) : (f & ~(uint32_t)GPF_HTTPS);
 	}
 	g.f = (uint8_t)f;
+	return consumed;
+}
+
+// Bytes of this buffer the request may still take before the length cap (P:88-91: a byte
+// is refused once more than kMaxRequestLength bytes were parsed).
+EBD_HD uint32_t dfa_allow(uint32_t pos, uint32_t n) {
+	const uint32_t allow = pos <= kMaxRequestLength ? kMaxRequestLength + 1 - pos : 0;
+	return n < allow ? n : allow;
 }
 
 // P:85-106 parse() of one buffer with the DFA: returns the bytes consumed (the host twin
 // of the device walker, which reads the buffer 16 bytes at a time).
-template <typename Tab, typename Kc, typename ByteAt>
-EBD_HD uint32_t dfa_parse(GenParser& g, const Tab& T, const Kc& KC, const DfaInfo& di, ByteAt at, uint32_t n, uint8_t flags) {
+template <typename Tab, typename At, typename ByteAt>
+EBD_HD uint32_t dfa_parse(GenParser& g, const Tab& T, const At& A, const DfaInfo& di, ByteAt at, uint32_t n, uint8_t flags) {
 	DfaWalk w;
-	dfa_walk_load(g, w);
-	uint32_t i = 0;
-	bool done = false;
-	while (i < n) {
-		if (w.pos > kMaxRequestLength) { // P:88-91
-			w.s = di.inv;
-			done = true;
-			break;
-		}
-		done = dfa_walk_step(T, KC, di, w, at(i));
-		i++;
-		if (done)
-			break;
-	}
-	dfa_walk_store(di, w, done, flags, g);
-	return i;
+	dfa_walk_load(g, A[g.ds], w);
+	const uint32_t pos0 = w.pos, ne = dfa_allow(pos0, n);
+	for (uint32_t i = 0; i < ne && w.tpos == kNone; i++)
+		dfa_walk_step(T, A, w, at(i), true);
+	return dfa_walk_store(di, w, pos0, ne, n, flags, g);
 }
 
 // Client-IP pass for one event (HttpRequestParser.cpp:370-407 parseClientIPValue on the

@@ -983,7 +983,7 @@ void k_fresh(Dev d) {
 #pragma unroll
 					for (int k = 0; k < 4; k++)
 						chunk_update(di, sr, 4 * w0 + k, s ^ (uint32_t)k, qs[k], qm[k], m[k]);
-					live = !st_terminal(di, sx[3]) && 64 * (w0 + 1) < e0.L ? 1u : 0u;
+					live = 64 * (w0 + 1) < e0.L ? 1u : 0u; // every byte of the buffer (no early end on garbage states)
 					s = sx[0] ^ sx[1] ^ sx[2] ^ sx[3];
 				}
 			}
@@ -1002,7 +1002,7 @@ void k_fresh(Dev d) {
 				if (live) {
 					chunk_update(di, sr, 4 * w0 + 1, sa1, qs0, qm0, m0);
 					chunk_update(di, sr, 4 * w0 + 3, sb1, qs1, qm1, m1);
-					live = !st_terminal(di, sa) && !st_terminal(di, sb) && 64 * (w0 + 1) < e0.L ? 1u : 0u;
+					live = 64 * (w0 + 1) < e0.L ? 1u : 0u; // every byte of the buffer (no early end on garbage states)
 					s = sa ^ sb ^ s;
 				}
 			}
@@ -1033,7 +1033,11 @@ void k_fresh(Dev d) {
 					}
 #endif
 #endif
+#ifdef EBD_EXP_LENLIVE // experiment: scan every byte of the buffer (the SPLIT probes' baseline)
+					live = 16 * (c + 1) < e0.L ? 1u : 0u;
+#else
 					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
+#endif
 					s = sx;
 				}
 			}
@@ -1166,11 +1170,11 @@ struct ByteWin {
 	}
 };
 
-// The session path's tables in LDS: the DFA image (byte-major, LdsTable) and the client id
-// of each header-key state (DfaTable::kcid).
+// The session path's tables in LDS: the DFA image (byte-major, LdsTable) and the attribute
+// byte of each state (DfaTable::attr).
 struct SessTabs {
 	const uint8_t* T;
-	const uint8_t* KC;
+	const uint8_t* A;
 };
 struct ByteTab {
 	const uint8_t* t;
@@ -1178,39 +1182,31 @@ struct ByteTab {
 };
 
 // dfa_parse (ebd_fresh.h) over one buffer on the device: 16-byte aligned blocks, the next
-// one loaded while the current one is walked, 16 predicated steps per block.  The aligned
-// block holding a valid byte never leaves that byte's page, so the over-read cannot fault.
+// one loaded while the current one is walked, 16 predicated branch-free steps per block (a
+// byte is valid when its buffer offset is below the bytes the request may take).  The
+// aligned block holding a valid byte never leaves that byte's page, so the over-read cannot
+// fault.  The walk stops after the block in which the state became terminal.
 __device__ uint32_t dfa_parse_dev(GenParser& g, const SessTabs& tb, const DfaInfo& di, const uint8_t* p, uint32_t n, uint8_t flags) {
-	DfaWalk w;
-	dfa_walk_load(g, w);
 	const LdsTable T{tb.T};
-	const ByteTab KC{tb.KC};
-	const uintptr_t a0 = (uintptr_t)p, a1 = a0 + n;
-	uintptr_t blk = a0 & ~(uintptr_t)15;
-	uint32_t i = 0;
-	bool done = false;
-	uint4 cur = n ? *(const uint4*)blk : uint4{0u, 0u, 0u, 0u};
-	while (!done && blk < a1) {
-		const uint4 nx = blk + 16 < a1 ? *(const uint4*)(blk + 16) : cur;
-		const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+	const ByteTab A{tb.A};
+	DfaWalk w;
+	dfa_walk_load(g, A[g.ds], w);
+	const uint32_t pos0 = w.pos, ne = dfa_allow(pos0, n);
+	if (ne) {
+		const uintptr_t a0 = (uintptr_t)p, b0 = a0 & ~(uintptr_t)15;
+		const uint32_t k0 = (uint32_t)(a0 & 15u), nb = (k0 + ne + 15u) >> 4;
+		uint4 cur = *(const uint4*)b0;
+		for (uint32_t bi = 0; bi < nb && w.tpos == kNone; bi++) {
+			const uint4 nx = bi + 1 < nb ? *(const uint4*)(b0 + 16u * (bi + 1)) : cur;
+			const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+			const uint32_t base = 16u * bi - k0; // buffer offset of the block's byte 0 (wraps below 0)
 #pragma unroll
-		for (int k = 0; k < 16; k++) {
-			const uintptr_t a = blk + (uintptr_t)k;
-			if (!done && a >= a0 && a < a1) {
-				if (w.pos > kMaxRequestLength) { // P:88-91
-					w.s = di.inv;
-					done = true;
-				} else {
-					done = dfa_walk_step(T, KC, di, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu);
-					i++;
-				}
-			}
+			for (int k = 0; k < 16; k++)
+				dfa_walk_step(T, A, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu, base + (uint32_t)k < ne);
+			cur = nx;
 		}
-		cur = nx;
-		blk += 16;
 	}
-	dfa_walk_store(di, w, done, flags, g);
-	return i;
+	return dfa_walk_store(di, w, pos0, ne, n, flags, g);
 }
 
 // Visits stream bytes [a, a + n) in order; the stream ends at sorted position jend whose
@@ -1248,43 +1244,63 @@ __device__ uint32_t stream_visit(const Dev& d, const Walk& w, uint32_t jend, uin
 	return done;
 }
 
+// Copies stream bytes [a, a + n) to dst: 8-byte loads and stores inside each piece, byte
+// stores for a piece's last < 8 bytes (the next request's bytes follow dst's in the arena).
+__device__ void stream_copy(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, uint32_t a, uint32_t n, uint8_t* dst) {
+	const uint32_t b = a + n;
+	auto copy = [](const uint8_t* src, uint8_t* out, uint32_t len) {
+		uint32_t k = 0;
+		for (; k + 8 <= len; k += 8)
+			*(u64a1*)(out + k) = gload8u(src + k);
+		for (; k < len; k++)
+			out[k] = src[k];
+	};
+	uint32_t pos = 0;
+	if (n == 0)
+		return;
+	if (w.clen) {
+		if (a < w.clen)
+			copy(w.cb + a, dst, min(b, w.clen) - a);
+		pos = w.clen;
+	}
+	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
+		uint32_t pl = piece_len(d, j);
+		if (j == jend)
+			pl = cend;
+		if (pl == 0)
+			continue;
+		const uint32_t lo = a > pos ? a : pos, hi = b < pos + pl ? b : pos + pl;
+		if (lo < hi)
+			copy(d.payload + d.off[slow_event(d, j)] + (lo - pos), dst + (lo - a), hi - lo);
+		pos += pl;
+	}
+}
+
 // handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
 // (Discovery.cpp:161-192, 210-212) for a request finished by the session path.
 __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, const GenParser& g,
 		uint32_t i, ebd_event_result& r) {
 	const EventRec& ev = d.ev[i];
 	const uint32_t hl = (g.f & GPF_HOST) ? g.host_len : 0, ul = g.url_len;
-	uint32_t raw = 0;
-	if (g.f & GPF_CIP_FOUND) // the value up to its first ',' is the front token's source
-		raw = stream_visit(d, w, jend, cend, g.cip_start, g.cip_len, [](uint8_t c) { return c != ','; });
-	const uint32_t total = hl + ul + raw;
+	const uint32_t cl = (g.f & GPF_CIP_FOUND) ? g.cip_len : 0; // the whole first client-IP value
+	const uint32_t total = hl + ul + cl;
 	const unsigned long long at = wave_add(&d.ctr[CTR_SSTR], (unsigned long long)total);
 	uint8_t info = (uint8_t)((g.mcand == 'P' ? EBD_INFO_POST : 0) | ((g.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0) | EBD_INFO_SESSION);
 	uint8_t cls;
-	KeyHasher kh;
-	kh.init(d.hkey, ev.pid);
 	uint32_t tb = 0, te = 0;
 	if (at + total > d.sstr_cap) {
 		set_error(d, EBD_ERR_ARENA_FULL);
 		return;
 	}
 	uint8_t* dst = d.sstr + at;
-	uint32_t k = 0;
-	stream_visit(d, w, jend, cend, g.host_start, hl, [&](uint8_t c) {
-		dst[k++] = c;
-		return true;
-	});
-	stream_visit(d, w, jend, cend, g.url_start, ul, [&](uint8_t c) {
-		dst[k++] = c;
-		return true;
-	});
-	if (raw)
-		stream_visit(d, w, jend, cend, g.cip_start, raw, [&](uint8_t c) {
-			dst[k++] = c;
-			return true;
-		});
+	stream_copy(d, w, jend, cend, g.host_start, hl, dst);
+	stream_copy(d, w, jend, cend, g.url_start, ul, dst + hl);
+	stream_copy(d, w, jend, cend, g.cip_start, cl, dst + hl + ul);
 	unsigned long long net = 0;
 	if (g.f & GPF_CIP_FOUND) {
+		uint32_t raw = 0; // the value up to its first ',' is the front token's source
+		while (raw < cl && dst[hl + ul + raw] != ',')
+			raw++;
 		front_token(dst + hl + ul, raw, &tb, &te);
 		info |= EBD_INFO_CIP;
 		cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb, &net);
@@ -1292,9 +1308,10 @@ __device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend,
 		cls = classify_source(*d.ifs, ev.flags, ev.sourceIP, &net);
 	}
 	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
-	kh.bytes(dst, hl + ul);
+	// the endpoint's key in block form over its copy (the arena has 64 bytes of slack)
+	const Hash128 key = endpoint_key(d.hkey, ev.pid, 0, hl, hl, ul, [dst](uint32_t o) { return gload8u(dst + o); });
 	bool claimed;
-	const uint32_t slot = agg_insert(d, kh.finish(), first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl),
+	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl),
 			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (claimed) // a rare path: one reservation per claim
 		claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull),
@@ -1328,7 +1345,17 @@ struct SessState {
 	unsigned long long stamp;
 	uint32_t live;
 	uint32_t li; // position in the exact walker's live list
+#ifdef EBD_EXP_WALK_PROF // experiment: clock cycles in the parse and in the emission (k_walk)
+	unsigned long long tp, te;
+#endif
 };
+#ifdef EBD_EXP_WALK_PROF
+#define PROF_BEGIN const unsigned long long t0_ = clock64();
+#define PROF_END(x) S.x += clock64() - t0_;
+#else
+#define PROF_BEGIN
+#define PROF_END(x)
+#endif
 
 enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
 
@@ -1352,7 +1379,9 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 		if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
 			S.stamp = d.seq_base + i;
 			r.info |= EBD_INFO_EXISTING;
+			PROF_BEGIN
 			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
+			PROF_END(tp)
 			r.consumed = (uint16_t)c;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
@@ -1361,7 +1390,13 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 				op = OP_ERASE;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-				emit_session_request(d, S.w, jj, c, S.g, i, r);
+#ifndef EBD_EXP_WALK_NOEMIT // experiment: no request emission (results are wrong)
+				{
+					PROF_BEGIN
+					emit_session_request(d, S.w, jj, c, S.g, i, r);
+					PROF_END(te)
+				}
+#endif
 				gp_reset(S.g); // session.reset(); stays saved
 				S.w = Walk{nullptr, 0, jj + 1};
 			} else {
@@ -1370,13 +1405,21 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 		} else { // handleNewSession, Discovery.cpp:141-159
 			gp_init(S.g);
 			S.w = Walk{nullptr, 0, jj};
+			PROF_BEGIN
 			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
+			PROF_END(tp)
 			r.consumed = (uint16_t)c;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-				emit_session_request(d, S.w, jj, c, S.g, i, r);
+#ifndef EBD_EXP_WALK_NOEMIT // experiment: no request emission (results are wrong)
+				{
+					PROF_BEGIN
+					emit_session_request(d, S.w, jj, c, S.g, i, r);
+					PROF_END(te)
+				}
+#endif
 			} else {
 				r.status = EBD_STATUS_UNFINISHED;
 				if (!(flags & FLAG_END))
@@ -1449,23 +1492,44 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 	__syncthreads();
 	const SessTabs tb{tabs, tabs + kLdsTableBytes};
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
+#ifdef EBD_EXP_WALK_PROF
+	unsigned long long p_parse = 0, p_emit = 0, p_all = 0, p_sess = 0;
+#endif
 	for (uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x; h < nh; h += gridDim.x * kWalkThreads) {
+#ifdef EBD_EXP_WALK_PROF
+		const unsigned long long ts_ = clock64();
+#endif
 		const uint32_t j = d.heads[h];
 		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
 		SessState S;
 		session_begin(d, S, j, slot);
+#ifdef EBD_EXP_WALK_PROF
+		S.tp = S.te = 0;
+#endif
 		uint32_t jj = j;
 		for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
 			const uint32_t op = session_event(d, tb, S, jj);
 			if (op == OP_INSERT) {
 				S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
 				S.stamp = d.seq_base + slow_event(d, jj);
-				atomicAdd(&d.ctr[CTR_INSERTS], 1ull);
+				wave_add(&d.ctr[CTR_INSERTS], 1ull);
 			}
 		}
 		if (S.live)
 			session_carry_out(d, S, j, jj - 1);
+#ifdef EBD_EXP_WALK_PROF
+		p_parse += S.tp;
+		p_emit += S.te;
+		p_all += clock64() - ts_;
+		p_sess++;
+#endif
 	}
+#ifdef EBD_EXP_WALK_PROF // into counters no walk test reads (stats: hash_collisions, lru_evictions, kernel_deletes, live...)
+	atomicAdd(&d.ctr[CTR_COLLISIONS], p_parse);
+	atomicAdd(&d.ctr[CTR_EVICTIONS_TOTAL], p_emit);
+	atomicAdd(&d.ctr[CTR_KDELETES], p_all);
+	atomicAdd(&d.ctr[CTR_KEEP], p_sess);
+#endif
 }
 
 // After a walker: every sorted session event was replayed once (Discovery::handleNewEvent)
