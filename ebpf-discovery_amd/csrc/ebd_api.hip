@@ -22,6 +22,7 @@ hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_carry_insert(const Dev& d, hipStream_t st);
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
+hipError_t launch_emit(const Dev& d, hipStream_t st, int cus);
 struct SessState;
 hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* minus, int* scan, void* tmp, size_t tmp_bytes,
 		hipStream_t st, int cus);
@@ -129,6 +130,7 @@ struct ebd_ctx {
 	SSlot* d_sset = nullptr;
 	uint32_t sset_cap = 0;
 	uint32_t* d_dirty = nullptr;
+	uint32_t* d_evslot = nullptr;
 	unsigned long long* d_slow[2] = {nullptr, nullptr};
 	void* d_sort_tmp = nullptr;
 	size_t sort_tmp_bytes = 0;
@@ -218,9 +220,9 @@ struct ebd_ctx {
 };
 
 static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
-		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used"};
+		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used", "k_emit"};
 enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_PUBLISH, KT_SSET_CLEAR, KT_VERIFY,
-	KT_CLEAR, KT_N };
+	KT_CLEAR, KT_EMIT, KT_N };
 static_assert(KT_N <= 16, "kernel timing slots");
 
 static hipEvent_t take_event(ebd_ctx* c) {
@@ -289,6 +291,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.sset = c->d_sset;
 	d.sset_mask = c->sset_cap - 1;
 	d.dirty = c->d_dirty;
+	d.ev_slot = c->d_evslot;
 	d.slow_keys = c->d_slow[0];
 	d.carry_in = c->d_carry[c->carry_cur];
 	d.n_carry_in = c->n_carry;
@@ -320,7 +323,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
-			c->d_sset, c->d_dirty, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sset, c->d_dirty, c->d_evslot, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
@@ -479,6 +482,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMalloc(&c->d_sset, (size_t)c->sset_cap * sizeof(SSlot)));
 	CTX_TRY(hipMemsetAsync(c->d_sset, 0, (size_t)c->sset_cap * sizeof(SSlot), c->stream));
 	CTX_TRY(hipMalloc(&c->d_dirty, (n + lru) * sizeof(uint32_t)));
+	CTX_TRY(hipMalloc(&c->d_evslot, (size_t)n * sizeof(uint32_t)));
 	CTX_TRY(hipMalloc(&c->d_slow[0], n * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_slow[1], n * sizeof(unsigned long long)));
 	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
@@ -622,8 +626,8 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	const uint64_t dirty = c->h_ctr[CTR_DIRTY];
 	if (nslow > 0) {
 		c->last_slow_ran = 1;
-		int end_bit = 32;
-		while ((1ull << (end_bit - 32)) < c->sset_cap)
+		int end_bit = 32; // session groups: carried index or carry_cap + first unfinished event
+		while ((1ull << (end_bit - 32)) < (uint64_t)c->carry_cap + c->max_events)
 			end_bit++;
 		size_t bytes = c->sort_tmp_bytes;
 		HIP_TRY(timed(c, KT_SORT, [&] {
@@ -674,6 +678,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 			if (c->n_carry)
 				HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
 		}
+		HIP_TRY(timed(c, KT_EMIT, [&] { return launch_emit(d, c->stream, c->cus); }));
 	}
 	HIP_TRY(timed(c, KT_VERIFY, [&] { return launch_verify(d, c->stream, c->cus); }));
 	if (dirty)

@@ -168,7 +168,8 @@ struct Dev {
 	SSlot* sset;
 	uint32_t sset_mask;
 	uint32_t* dirty;
-	unsigned long long* slow_keys;
+	unsigned long long* slow_keys; // session group << 32 | event (k_slow_collect), sorted
+	uint32_t* ev_slot;             // per event: its session's session-set slot (session-path events only)
 	uint32_t* heads; // sorted position of each session's first event (k_walk_heads)
 	Carry* carry_in;
 	uint32_t n_carry_in;

@@ -1123,7 +1123,14 @@ __global__ void k_slow_collect(Dev d) {
 			d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
 			atomicMax(&d.sset[slot].last_ev, i + 1);
 			const unsigned long long k = wave_add(&d.ctr[CTR_SLOW], 1ull);
-			d.slow_keys[k] = ((unsigned long long)(uint32_t)slot << 32) | i;
+			// grouped by session, sessions in the order of their first UNFINISHED fresh parse
+			// (carried ones first): the lanes of a walker wave then follow sessions that started
+			// together, whose events lie close together in the batch (L2 / TLB locality), where
+			// the session-set slot order (a hash) sent them all over the batch
+			const SSlot& ss = d.sset[slot];
+			const uint32_t grp = ss.carry ? ss.carry - 1 : d.carry_cap + ~ss.first_c;
+			d.slow_keys[k] = ((unsigned long long)grp << 32) | i;
+			d.ev_slot[i] = (uint32_t)slot;
 		}
 	}
 }
@@ -1134,6 +1141,10 @@ __global__ void k_slow_collect(Dev d) {
 // of this batch's events from position j0 on.
 // ---------------------------------------------------------------------------------
 constexpr int kWalkThreads = 256;
+#ifndef EBD_WALK_REFILL
+#define EBD_WALK_REFILL 48
+#endif
+constexpr int kWalkRefill = EBD_WALK_REFILL; // lanes of a wave waiting before it ends and starts events
 
 struct Walk {
 	const uint8_t* cb; // carried bytes of the request in progress
@@ -1278,62 +1289,105 @@ __device__ void stream_copy(const Dev& d, const Walk& w, uint32_t jend, uint32_t
 
 // handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
 // (Discovery.cpp:161-192, 210-212) for a request finished by the session path.
-__device__ void emit_session_request(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, const GenParser& g,
-		uint32_t i, ebd_event_result& r) {
-	const EventRec& ev = d.ev[i];
-	const uint32_t hl = (g.f & GPF_HOST) ? g.host_len : 0, ul = g.url_len;
-	const uint32_t cl = (g.f & GPF_CIP_FOUND) ? g.cip_len : 0; // the whole first client-IP value
-	const uint32_t total = hl + ul + cl;
-	const unsigned long long at = wave_add(&d.ctr[CTR_SSTR], (unsigned long long)total);
-	uint8_t info = (uint8_t)((g.mcand == 'P' ? EBD_INFO_POST : 0) | ((g.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0) | EBD_INFO_SESSION);
-	uint8_t cls;
-	uint32_t tb = 0, te = 0;
-	if (at + total > d.sstr_cap) {
-		set_error(d, EBD_ERR_ARENA_FULL);
-		return;
-	}
-	uint8_t* dst = d.sstr + at;
-	stream_copy(d, w, jend, cend, g.host_start, hl, dst);
-	stream_copy(d, w, jend, cend, g.url_start, ul, dst + hl);
-	stream_copy(d, w, jend, cend, g.cip_start, cl, dst + hl + ul);
-	unsigned long long net = 0;
-	if (g.f & GPF_CIP_FOUND) {
-		uint32_t raw = 0; // the value up to its first ',' is the front token's source
-		while (raw < cl && dst[hl + ul + raw] != ',')
-			raw++;
-		front_token(dst + hl + ul, raw, &tb, &te);
-		info |= EBD_INFO_CIP;
-		cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb, &net);
-	} else {
-		cls = classify_source(*d.ifs, ev.flags, ev.sourceIP, &net);
-	}
-	info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
-	// the endpoint's key in block form over its copy (the arena has 64 bytes of slack)
-	const Hash128 key = endpoint_key(d.hkey, ev.pid, 0, hl, hl, ul, [dst](uint32_t o) { return gload8u(dst + o); });
-	bool claimed;
-	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (g.f & GPF_HTTPS) != 0, hl),
-			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
-	if (claimed) // a rare path: one reservation per claim
-		claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull),
-				wave_add(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
-	if (d.net_on && cls == CLS_EXTERNAL)
-		agg_nets(d, slot, net);
-	const unsigned long long q = wave_add(&d.ctr[CTR_SREQ], 1ull); // CTR_REQUESTS: the walkers add CTR_SREQ
-	SessReq sr;
-	sr.seq = d.seq_base + i;
-	sr.pid = ev.pid;
-	sr.str_off = (uint32_t)at;
-	sr.host_len = (uint16_t)hl;
-	sr.url_len = (uint16_t)ul;
-	sr.cip_off = (uint16_t)(hl + ul + tb);
-	sr.cip_len = (uint16_t)(te - tb);
-	sr.info = info;
-	sr.status = EBD_STATUS_FINISHED;
-	sr.pad = 0;
-	sr.pad2 = 0;
-	d.sreq[q] = sr;
-	r.info = info;
+// A request the session path finished, from the walker to k_emit: everything the emission
+// needs, in the session-request slot it will occupy (32 bytes: SessReq's size).  The walker
+// only records it, so the emission (span copies, client class, key, service table) runs
+// for all of the batch's session requests at once in k_emit, on full waves, instead of
+// for the few lanes of a walker wave whose event happened to finish a request.
+struct EmitRec {
+	uint32_t i, jend, j0, carry; // finishing event, its sorted position, the request's first; carried bytes: 1 + index
+	uint16_t host_start, host_len, url_start, url_len, cip_start, cip_len;
+	uint8_t f, mcand, info, pad; // GenParser::f and mcand; the result's info bits so far
+};
+static_assert(sizeof(EmitRec) == sizeof(SessReq), "an emission record fills a session-request slot");
+
+__device__ void defer_emit(const Dev& d, const Walk& w, uint32_t jend, const GenParser& g, uint32_t i, ebd_event_result& r) {
+	const unsigned long long q = wave_add(&d.ctr[CTR_SREQ], 1ull); // CTR_REQUESTS: k_sess_tally adds CTR_SREQ
+	EmitRec e;
+	e.i = i;
+	e.jend = jend;
+	e.j0 = w.j0;
+	e.carry = w.cb ? (uint32_t)(((const uint8_t*)w.cb - (const uint8_t*)d.carry_in) / sizeof(Carry)) + 1u : 0u;
+	e.host_start = (uint16_t)g.host_start;
+	e.host_len = (uint16_t)g.host_len;
+	e.url_start = (uint16_t)g.url_start;
+	e.url_len = (uint16_t)g.url_len;
+	e.cip_start = (uint16_t)g.cip_start;
+	e.cip_len = (uint16_t)g.cip_len;
+	e.f = g.f;
+	e.mcand = g.mcand;
+	e.info = r.info;
+	e.pad = 0;
+	*(EmitRec*)(d.sreq + q) = e;
 	r.u.session.index = (uint32_t)q;
+}
+
+// handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
+// (Discovery.cpp:161-192, 210-212) for the session path's request q.
+__global__ void k_emit(Dev d) {
+	const uint32_t nq = (uint32_t)d.ctr[CTR_SREQ];
+	for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+		const EmitRec e = *(const EmitRec*)(d.sreq + q);
+		const uint32_t i = e.i;
+		const Walk w{e.carry ? d.carry_in[e.carry - 1].bytes : nullptr, e.carry ? d.carry_in[e.carry - 1].nbytes : 0u, e.j0};
+		const uint32_t cend = d.res[i].consumed;
+		const EventRec& ev = d.ev[i];
+		const uint32_t hl = (e.f & GPF_HOST) ? e.host_len : 0, ul = e.url_len;
+		const uint32_t cl = (e.f & GPF_CIP_FOUND) ? e.cip_len : 0; // the whole first client-IP value
+		const uint32_t total = hl + ul + cl;
+		const unsigned long long at = wave_add(&d.ctr[CTR_SSTR], (unsigned long long)total);
+		uint8_t info = (uint8_t)(e.info | (e.mcand == 'P' ? EBD_INFO_POST : 0) | ((e.f & GPF_HTTPS) ? EBD_INFO_HTTPS : 0));
+		SessReq sr;
+		sr.seq = d.seq_base + i;
+		sr.pid = ev.pid;
+		sr.status = EBD_STATUS_FINISHED;
+		sr.pad = 0;
+		sr.pad2 = 0;
+		if (at + total > d.sstr_cap) {
+			set_error(d, EBD_ERR_ARENA_FULL);
+			sr.str_off = 0;
+			sr.host_len = sr.url_len = sr.cip_off = sr.cip_len = 0;
+			sr.info = info;
+			d.sreq[q] = sr;
+			continue;
+		}
+		uint8_t* dst = d.sstr + at;
+		stream_copy(d, w, e.jend, cend, e.host_start, hl, dst);
+		stream_copy(d, w, e.jend, cend, e.url_start, ul, dst + hl);
+		stream_copy(d, w, e.jend, cend, e.cip_start, cl, dst + hl + ul);
+		unsigned long long net = 0;
+		uint8_t cls;
+		uint32_t tb = 0, te = 0;
+		if (e.f & GPF_CIP_FOUND) {
+			uint32_t raw = 0; // the value up to its first ',' is the front token's source
+			while (raw < cl && dst[hl + ul + raw] != ',')
+				raw++;
+			front_token(dst + hl + ul, raw, &tb, &te);
+			info |= EBD_INFO_CIP;
+			cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb, &net);
+		} else {
+			cls = classify_source(*d.ifs, ev.flags, ev.sourceIP, &net);
+		}
+		info |= (uint8_t)(cls << EBD_INFO_CLASS_SHIFT);
+		// the endpoint's key in block form over its copy (the arena has 64 bytes of slack)
+		const Hash128 key = endpoint_key(d.hkey, ev.pid, 0, hl, hl, ul, [dst](uint32_t o) { return gload8u(dst + o); });
+		bool claimed;
+		const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (e.f & GPF_HTTPS) != 0, hl),
+				cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
+		if (claimed)
+			claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull),
+					wave_add(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
+		if (d.net_on && cls == CLS_EXTERNAL)
+			agg_nets(d, slot, net);
+		sr.str_off = (uint32_t)at;
+		sr.host_len = (uint16_t)hl;
+		sr.url_len = (uint16_t)ul;
+		sr.cip_off = (uint16_t)(hl + ul + tb);
+		sr.cip_len = (uint16_t)(te - tb);
+		sr.info = info;
+		d.sreq[q] = sr;
+		d.res[i].info = info;
+	}
 }
 
 // A session as the walkers hold it: the parser (Session, Discovery.h), the request in
@@ -1345,28 +1399,45 @@ struct SessState {
 	unsigned long long stamp;
 	uint32_t live;
 	uint32_t li; // position in the exact walker's live list
-#ifdef EBD_EXP_WALK_PROF // experiment: clock cycles in the parse and in the emission (k_walk)
-	unsigned long long tp, te;
-#endif
 };
-#ifdef EBD_EXP_WALK_PROF
-#define PROF_BEGIN const unsigned long long t0_ = clock64();
-#define PROF_END(x) S.x += clock64() - t0_;
-#else
-#define PROF_BEGIN
-#define PROF_END(x)
-#endif
 
 enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
 
 // Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
 // session's state in S.  Returns the LRU operation it implies; an insert (saveSession,
 // Discovery.cpp:148-150) is left to the caller, which may have to evict first.
-__device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S, uint32_t jj) {
-	const uint32_t i = slow_event(d, jj);
-	const EventRec& ev = d.ev[i];
-	const uint8_t flags = ev.flags;
-	const uint32_t L = d.len[i];
+// An event of the session path from the start to the end of its parse (Discovery.cpp:92-198).
+enum : uint32_t { EV_PARSE = 256, EV_EXISTING = 512 };
+struct EvCtx {
+	uint32_t i, jj, L;
+	uint32_t flags; // the event's flags | EV_PARSE | EV_EXISTING
+};
+
+// handleNewEvent up to parse(): whether the event's buffer is parsed, and with which parser
+// (the saved session's, or a fresh one for a session not in the LRU).
+__device__ __forceinline__ bool ev_begin(const Dev& d, SessState& S, uint32_t jj, uint32_t i, uint32_t flags, uint32_t L, EvCtx& e) {
+	e.i = i;
+	e.jj = jj;
+	e.L = L;
+	e.flags = flags;
+	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || L > EBD_BUFFER_MAX_DATA_SIZE)
+		return false;
+	e.flags |= EV_PARSE;
+	if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
+		S.stamp = d.seq_base + i;
+		e.flags |= EV_EXISTING;
+	} else { // handleNewSession, Discovery.cpp:141-159
+		gp_init(S.g);
+		S.w = Walk{nullptr, 0, jj};
+	}
+	return true;
+}
+
+// handleNewEvent after parse() consumed c bytes: the outcome, the request (FINISHED), the
+// kernel-side delete (INVALID of a saved session), the close.  Returns the LRU operation
+// it implies; an insert (saveSession, Discovery.cpp:148-150) is left to the caller, which
+// may have to evict first.
+__device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvCtx& e, uint32_t c) {
 	ebd_event_result r;
 	r.consumed = 0;
 	r.status = EBD_STATUS_NONE;
@@ -1374,15 +1445,10 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 	r.u.session.index = 0xffffffffu;
 	r.u.session.pad_[0] = r.u.session.pad_[1] = 0;
 	uint32_t op = OP_NONE; // CTR_SESSION_EVENTS: the walkers count the events they replay
-	if ((flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) {
-		const uint8_t* buf = d.payload + d.off[i];
-		if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
-			S.stamp = d.seq_base + i;
+	if (e.flags & EV_PARSE) {
+		r.consumed = (uint16_t)c;
+		if (e.flags & EV_EXISTING) {
 			r.info |= EBD_INFO_EXISTING;
-			PROF_BEGIN
-			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
-			PROF_END(tp)
-			r.consumed = (uint16_t)c;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
 				atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
@@ -1390,53 +1456,46 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 				op = OP_ERASE;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-#ifndef EBD_EXP_WALK_NOEMIT // experiment: no request emission (results are wrong)
-				{
-					PROF_BEGIN
-					emit_session_request(d, S.w, jj, c, S.g, i, r);
-					PROF_END(te)
-				}
-#endif
+				defer_emit(d, S.w, e.jj, S.g, e.i, r);
 				gp_reset(S.g); // session.reset(); stays saved
-				S.w = Walk{nullptr, 0, jj + 1};
+				S.w = Walk{nullptr, 0, e.jj + 1};
 			} else {
 				r.status = EBD_STATUS_UNFINISHED;
 			}
-		} else { // handleNewSession, Discovery.cpp:141-159
-			gp_init(S.g);
-			S.w = Walk{nullptr, 0, jj};
-			PROF_BEGIN
-			const uint32_t c = dfa_parse_dev(S.g, tb, d.di, buf, L, flags);
-			PROF_END(tp)
-			r.consumed = (uint16_t)c;
+		} else {
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-#ifndef EBD_EXP_WALK_NOEMIT // experiment: no request emission (results are wrong)
-				{
-					PROF_BEGIN
-					emit_session_request(d, S.w, jj, c, S.g, i, r);
-					PROF_END(te)
-				}
-#endif
+				defer_emit(d, S.w, e.jj, S.g, e.i, r);
 			} else {
 				r.status = EBD_STATUS_UNFINISHED;
-				if (!(flags & FLAG_END))
+				if (!(e.flags & FLAG_END))
 					op = OP_INSERT;
 			}
 		}
 	}
-	if ((flags & FLAG_END) && S.live) { // handleCloseEvent, Discovery.cpp:194-198
+	if ((e.flags & FLAG_END) && S.live) { // handleCloseEvent, Discovery.cpp:194-198
 		S.live = 0;
 		op = OP_ERASE;
 	}
-	d.res[i] = r;
+	d.res[e.i] = r;
 	return op;
 }
 
+// Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
+// session's state in S, the whole buffer at once (the exact LRU walker's form).
+__device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S, uint32_t jj) {
+	const uint32_t i = slow_event(d, jj);
+	EvCtx e;
+	uint32_t c = 0;
+	if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], e))
+		c = dfa_parse_dev(S.g, tb, d.di, d.payload + d.off[i], e.L, (uint8_t)e.flags);
+	return ev_end(d, S, e, c);
+}
+
 // The session's state at its first event of the batch (sorted position j).
-__device__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t slot) {
+__device__ __forceinline__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t slot) {
 	SSlot* ss = d.sset + slot;
 	ss->visited = 1;
 	S.w = Walk{nullptr, 0, j};
@@ -1458,7 +1517,7 @@ __device__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t s
 
 // A session still in the LRU after the batch, with the bytes of its request in progress
 // (which ends with the session's last event jlast of the batch, fully consumed).
-__device__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, uint32_t jlast) {
+__device__ __forceinline__ void session_carry_out(const Dev& d, const SessState& S, uint32_t j, uint32_t jlast) {
 	const unsigned long long c = wave_add(&d.ctr[CTR_CARRY_OUT], 1ull);
 	if (c >= d.carry_cap) {
 		set_error(d, EBD_ERR_LRU_OVERFLOW);
@@ -1490,46 +1549,89 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
 		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
 	__syncthreads();
-	const SessTabs tb{tabs, tabs + kLdsTableBytes};
+	const LdsTable T{tabs};
+	const ByteTab A{tabs + kLdsTableBytes};
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
-#ifdef EBD_EXP_WALK_PROF
-	unsigned long long p_parse = 0, p_emit = 0, p_all = 0, p_sess = 0;
-#endif
-	for (uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x; h < nh; h += gridDim.x * kWalkThreads) {
-#ifdef EBD_EXP_WALK_PROF
-		const unsigned long long ts_ = clock64();
-#endif
-		const uint32_t j = d.heads[h];
-		const uint32_t slot = (uint32_t)(d.slow_keys[j] >> 32);
-		SessState S;
-		session_begin(d, S, j, slot);
-#ifdef EBD_EXP_WALK_PROF
-		S.tp = S.te = 0;
-#endif
-		uint32_t jj = j;
-		for (; jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == slot; jj++) {
-			const uint32_t op = session_event(d, tb, S, jj);
-			if (op == OP_INSERT) {
-				S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
-				S.stamp = d.seq_base + slow_event(d, jj);
-				wave_add(&d.ctr[CTR_INSERTS], 1ull);
+	const uint32_t stride = gridDim.x * kWalkThreads;
+	// A lane walks its sessions one 16-byte block per iteration.  A lane whose event ended
+	// waits until half of the wave has (or none is still parsing); then the wave ends those
+	// events and starts the next ones together: one buffer per lane and step made each wave
+	// step as long as its longest buffer, while ending and starting events one lane at a time
+	// ran the long end-of-event path (outcome, emission, next event's loads) for a few lanes
+	// at a time.
+	uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x;
+	bool have = false, in_ev = false, ended = false;
+	SessState S;
+	uint32_t grp = 0, jj = 0, jhead = 0;
+	EvCtx e;
+	DfaWalk w;
+	uint32_t pos0 = 0, ne = 0, k0 = 0, nb = 0, bi = 0;
+	uintptr_t b0 = 0;
+	uint4 cur = uint4{0u, 0u, 0u, 0u};
+	for (;;) {
+		const unsigned long long busy = __ballot(in_ev), wait = __ballot(!in_ev && (ended || h < nh));
+		if (busy == 0 && wait == 0)
+			break;
+		if (busy == 0 || __popcll(wait) >= kWalkRefill) {
+			if (ended) {
+				const uint32_t c = dfa_walk_store(d.di, w, pos0, ne, e.L, (uint8_t)e.flags, S.g);
+				if (ev_end(d, S, e, c) == OP_INSERT) {
+					S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
+					S.stamp = d.seq_base + e.i;
+					wave_add(&d.ctr[CTR_INSERTS], 1ull);
+				}
+				ended = false;
+			}
+			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
+				if (!have) {
+					jhead = jj = d.heads[h];
+					grp = (uint32_t)(d.slow_keys[jj] >> 32);
+					session_begin(d, S, jj, d.ev_slot[slow_event(d, jj)]);
+					have = true;
+				}
+				if (jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == grp) {
+					const uint32_t i = slow_event(d, jj);
+					if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], e)) {
+						dfa_walk_load(S.g, A[S.g.ds], w);
+						pos0 = w.pos;
+						ne = dfa_allow(pos0, e.L);
+						const uintptr_t p = (uintptr_t)(d.payload + d.off[i]);
+						b0 = p & ~(uintptr_t)15;
+						k0 = (uint32_t)(p & 15u);
+						nb = ne ? (k0 + ne + 15u) >> 4 : 0u;
+						bi = 0;
+						if (nb)
+							cur = *(const uint4*)b0;
+						in_ev = true;
+					} else {
+						ev_end(d, S, e, 0);
+					}
+					jj++;
+				} else {
+					if (S.live)
+						session_carry_out(d, S, jhead, jj - 1);
+					have = false;
+					h += stride;
+				}
 			}
 		}
-		if (S.live)
-			session_carry_out(d, S, j, jj - 1);
-#ifdef EBD_EXP_WALK_PROF
-		p_parse += S.tp;
-		p_emit += S.te;
-		p_all += clock64() - ts_;
-		p_sess++;
-#endif
+		if (in_ev) {
+			if (bi < nb) { // one block: 16 predicated steps (dfa_parse_dev's)
+				const uint4 nx = bi + 1 < nb ? *(const uint4*)(b0 + 16u * (bi + 1)) : cur;
+				const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
+				const uint32_t base = 16u * bi - k0;
+#pragma unroll
+				for (int k = 0; k < 16; k++)
+					dfa_walk_step(T, A, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu, base + (uint32_t)k < ne);
+				cur = nx;
+				bi++;
+			}
+			if (bi >= nb || w.tpos != kNone) {
+				in_ev = false;
+				ended = true;
+			}
+		}
 	}
-#ifdef EBD_EXP_WALK_PROF // into counters no walk test reads (stats: hash_collisions, lru_evictions, kernel_deletes, live...)
-	atomicAdd(&d.ctr[CTR_COLLISIONS], p_parse);
-	atomicAdd(&d.ctr[CTR_EVICTIONS_TOTAL], p_emit);
-	atomicAdd(&d.ctr[CTR_KDELETES], p_all);
-	atomicAdd(&d.ctr[CTR_KEEP], p_sess);
-#endif
 }
 
 // After a walker: every sorted session event was replayed once (Discovery::handleNewEvent)
@@ -1580,7 +1682,7 @@ __global__ void k_carry_pass(Dev d) {
 __global__ void k_lru_delta(Dev d, uint32_t nslow, int* delta, uint8_t* minus) {
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
 		const uint32_t i = slow_event(d, j);
-		const SSlot& ss = d.sset[(uint32_t)(d.slow_keys[j] >> 32)];
+		const SSlot& ss = d.sset[d.ev_slot[i]];
 		const bool carried = ss.carry != 0;
 		const uint32_t first = ss.first_c ? ~ss.first_c : kNone;
 		const bool plus = !carried && first == i;
@@ -1652,7 +1754,7 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 	// every session's state at the batch start; the carried ones are in the LRU
 	for (uint32_t j = t; j < nslow; j += kLruThreads)
 		if (head[j] == j) {
-			session_begin(d, S[j], j, (uint32_t)(d.slow_keys[j] >> 32));
+			session_begin(d, S[j], j, d.ev_slot[slow_event(d, j)]);
 			if (S[j].live) {
 				const uint32_t k = atomicAdd(&nlive, 1u);
 				S[j].li = k;
@@ -2578,14 +2680,20 @@ hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_
 	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, jpos, head);
 	hipLaunchKernelGGL(k_walk_lru, dim3(1), dim3(kLruThreads), 0, st, d, nslow, (const uint32_t*)jpos, (const uint32_t*)head, S,
 			live, cap);
-	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
+
 	return hipGetLastError();
 }
 size_t sess_state_bytes() { return sizeof(SessState); }
+// After either walker: the session requests' emission, then the tallies.
+hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_emit, dim3(cus * 8), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
+	return hipGetLastError();
+}
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * 3)), dim3(kWalkThreads), 0, st, d);
-	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
+
 	return hipGetLastError();
 }
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
