@@ -19,7 +19,7 @@
 
 namespace ebd {
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
-hipError_t launch_carry_insert(const Dev& d, hipStream_t st);
+hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus);
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
 hipError_t launch_emit(const Dev& d, hipStream_t st, int cus);
@@ -131,6 +131,7 @@ struct ebd_ctx {
 	uint32_t sset_cap = 0;
 	uint32_t* d_dirty = nullptr;
 	uint32_t* d_evslot = nullptr;
+	uint32_t* d_smask = nullptr; // the session set's mask for the batch (k_sset_size)
 	unsigned long long* d_slow[2] = {nullptr, nullptr};
 	void* d_sort_tmp = nullptr;
 	size_t sort_tmp_bytes = 0;
@@ -219,7 +220,7 @@ struct ebd_ctx {
 	uint64_t kt_n[16] = {0};
 };
 
-static const char* kKernelNames[] = {"k_fresh", "k_carry_insert", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
+static const char* kKernelNames[] = {"k_fresh", "k_sset_build", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
 		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used", "k_emit"};
 enum { KT_FRESH, KT_CARRY_INSERT, KT_SLOW_COLLECT, KT_SORT, KT_WALK, KT_CARRY_PASS, KT_AGG, KT_PUBLISH, KT_SSET_CLEAR, KT_VERIFY,
 	KT_CLEAR, KT_EMIT, KT_N };
@@ -289,7 +290,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.sarena = c->d_sarena;
 	d.sarena_cap = c->sarena_cap;
 	d.sset = c->d_sset;
-	d.sset_mask = c->sset_cap - 1;
+	d.sset_mask = c->d_smask;
 	d.dirty = c->d_dirty;
 	d.ev_slot = c->d_evslot;
 	d.slow_keys = c->d_slow[0];
@@ -323,7 +324,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
-			c->d_sset, c->d_dirty, c->d_evslot, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
@@ -483,6 +484,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMemsetAsync(c->d_sset, 0, (size_t)c->sset_cap * sizeof(SSlot), c->stream));
 	CTX_TRY(hipMalloc(&c->d_dirty, (n + lru) * sizeof(uint32_t)));
 	CTX_TRY(hipMalloc(&c->d_evslot, (size_t)n * sizeof(uint32_t)));
+	CTX_TRY(hipMalloc(&c->d_smask, sizeof(uint32_t)));
 	CTX_TRY(hipMalloc(&c->d_slow[0], n * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_slow[1], n * sizeof(unsigned long long)));
 	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
@@ -611,9 +613,8 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		c->batch_valid = 1;
 		return 0;
 	}
-	if (c->n_carry)
-		HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_carry_insert(d, c->stream); }));
 	HIP_TRY(timed(c, KT_FRESH, [&] { return launch_fresh(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_sset_build(d, c->sset_cap, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipEventRecord(c->ev_mid, c->stream));

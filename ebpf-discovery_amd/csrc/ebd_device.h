@@ -32,7 +32,7 @@ struct SSlot {
 	unsigned int first_c;  // ~(first event of the batch whose fresh parse was UNFINISHED), 0 = none (atomicMax)
 	unsigned int carry;    // 1 + index into the carried-session array, 0 = none
 	unsigned int visited;
-	unsigned int last_ev;  // 1 + the session's last event in the batch (atomicMax)
+	unsigned int last_ev;  // (unused: k_lru_delta finds a session's last event in the sorted order)
 	unsigned int pad;
 	unsigned long long pad2;
 };
@@ -166,7 +166,7 @@ struct Dev {
 	unsigned long long sarena_cap;
 	// session path
 	SSlot* sset;
-	uint32_t sset_mask;
+	uint32_t* sset_mask; // in device memory: k_sset_size picks it per batch
 	uint32_t* dirty;
 	unsigned long long* slow_keys; // session group << 32 | event (k_slow_collect), sorted
 	uint32_t* ev_slot;             // per event: its session's session-set slot (session-path events only)

@@ -268,9 +268,10 @@ __device__ __forceinline__ unsigned long long sset_tag(unsigned long long kv, ui
 __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry, uint32_t ev) {
 	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
 	const unsigned long long tag = sset_tag(kv, sid);
-	uint32_t idx = (uint32_t)tag & d.sset_mask;
+	const uint32_t mask = *d.sset_mask;
+	uint32_t idx = (uint32_t)tag & mask;
 	int res = -1;
-	for (uint32_t probe = 0; probe <= d.sset_mask; probe++) {
+	for (uint32_t probe = 0; probe <= mask; probe++) {
 		SSlot* s = d.sset + idx;
 		unsigned long long t = ld_relaxed(&s->tag);
 		if (t == 0) {
@@ -287,7 +288,7 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 			res = (int)idx;
 			break;
 		}
-		idx = (idx + 1) & d.sset_mask;
+		idx = (idx + 1) & mask;
 	}
 	if (res < 0) {
 		set_error(d, EBD_ERR_SESSION_FULL);
@@ -304,8 +305,9 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) {
 	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
 	const unsigned long long tag = sset_tag(kv, sid);
-	uint32_t idx = (uint32_t)tag & d.sset_mask;
-	for (uint32_t probe = 0; probe <= d.sset_mask; probe++) {
+	const uint32_t mask = *d.sset_mask;
+	uint32_t idx = (uint32_t)tag & mask;
+	for (uint32_t probe = 0; probe <= mask; probe++) {
 		const SSlot* s = d.sset + idx;
 		const unsigned long long t = s->tag;
 		if (t == 0)
@@ -315,7 +317,7 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 				return (int)idx;
 			set_error(d, EBD_ERR_COLLISION); // two sessions share a 64-bit tag
 		}
-		idx = (idx + 1) & d.sset_mask;
+		idx = (idx + 1) & mask;
 	}
 	return -1;
 }
@@ -581,8 +583,8 @@ __device__ __forceinline__ void write_empty(const Dev& d, uint32_t i) {
 	r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
 	d.res[i] = r;
 	const EventRec& ev = d.ev[i];
-	wave_add(&d.ctr[CTR_UNFINISHED], 1ull);
-	sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
+	d.ev_slot[wave_add(&d.ctr[CTR_UNFINISHED], 1ull)] = i; // k_sset_build inserts its session
+	(void)ev;
 }
 
 // A finished scan waiting for fresh_finalize: 16 words, kept in the ring as 16 arrays of
@@ -695,8 +697,8 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 #endif
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
-		wave_add(&d.ctr[CTR_UNFINISHED], 1ull);
-		sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
+		d.ev_slot[wave_add(&d.ctr[CTR_UNFINISHED], 1ull)] = i; // k_sset_build inserts its session
+		(void)ev;
 	}
 	d.res[i] = fr.r;
 }
@@ -1104,10 +1106,29 @@ __device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_e
 	return cls;
 }
 
-__global__ void k_carry_insert(Dev d) {
-	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d.n_carry_in; c += gridDim.x * blockDim.x) {
-		const Carry& cr = d.carry_in[c];
-		sset_insert(d, cr.pid, cr.fd, cr.sid, c + 1, kNone);
+// The session set of the batch, sized to what it holds: the sessions carried from earlier
+// batches and those of the fresh parses k_fresh left unfinished (k_fresh lists them in
+// ev_slot).  Its mask is chosen on the device (no host round trip) at a load of at most 1/2
+// of the sessions it can hold, so the probes of k_slow_collect (one per event of the batch)
+// land in a table of a few times the live sessions instead of one sized for every event.
+__global__ void k_sset_size(Dev d, uint32_t cap) {
+	const unsigned long long want = 2ull * (d.ctr[CTR_UNFINISHED] + d.n_carry_in);
+	uint32_t m = 1024;
+	while (m < want && m < cap)
+		m <<= 1;
+	*d.sset_mask = m - 1u;
+}
+__global__ void k_sset_build(Dev d) {
+	const uint32_t nu = (uint32_t)d.ctr[CTR_UNFINISHED];
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < d.n_carry_in + nu; k += gridDim.x * blockDim.x) {
+		if (k < d.n_carry_in) {
+			const Carry& cr = d.carry_in[k];
+			sset_insert(d, cr.pid, cr.fd, cr.sid, k + 1, kNone);
+		} else {
+			const uint32_t i = d.ev_slot[k - d.n_carry_in];
+			const EventRec& ev = d.ev[i];
+			sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
+		}
 	}
 }
 
@@ -1121,7 +1142,6 @@ __global__ void k_slow_collect(Dev d) {
 		const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
 		if (slot >= 0) {
 			d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
-			atomicMax(&d.sset[slot].last_ev, i + 1);
 			const unsigned long long k = wave_add(&d.ctr[CTR_SLOW], 1ull);
 			// grouped by session, sessions in the order of their first UNFINISHED fresh parse
 			// (carried ones first): the lanes of a walker wave then follow sessions that started
@@ -1568,6 +1588,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 	uint32_t pos0 = 0, ne = 0, k0 = 0, nb = 0, bi = 0;
 	uintptr_t b0 = 0;
 	uint4 cur = uint4{0u, 0u, 0u, 0u};
+	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
+	unsigned long long pf_off = 0;
 	for (;;) {
 		const unsigned long long busy = __ballot(in_ev), wait = __ballot(!in_ev && (ended || h < nh));
 		if (busy == 0 && wait == 0)
@@ -1590,12 +1612,31 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 					have = true;
 				}
 				if (jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == grp) {
-					const uint32_t i = slow_event(d, jj);
-					if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], e)) {
+					uint32_t i, fl, L;
+					unsigned long long off;
+					if (pf_j == jj) { // loaded while the session's previous event was walked
+						i = pf_i, fl = pf_fl, L = pf_L, off = pf_off;
+					} else {
+						i = slow_event(d, jj);
+						fl = d.ev[i].flags, L = d.len[i], off = d.off[i];
+					}
+					// the session's next event: its loads travel while this one is walked
+					pf_j = kNone;
+					if (jj + 1 < nslow) {
+						const unsigned long long k2 = d.slow_keys[jj + 1];
+						if ((uint32_t)(k2 >> 32) == grp) {
+							pf_j = jj + 1;
+							pf_i = (uint32_t)k2;
+							pf_fl = d.ev[pf_i].flags;
+							pf_L = d.len[pf_i];
+							pf_off = d.off[pf_i];
+						}
+					}
+					if (ev_begin(d, S, jj, i, fl, L, e)) {
 						dfa_walk_load(S.g, A[S.g.ds], w);
 						pos0 = w.pos;
 						ne = dfa_allow(pos0, e.L);
-						const uintptr_t p = (uintptr_t)(d.payload + d.off[i]);
+						const uintptr_t p = (uintptr_t)(d.payload + off);
 						b0 = p & ~(uintptr_t)15;
 						k0 = (uint32_t)(p & 15u);
 						nb = ne ? (k0 + ne + 15u) >> 4 : 0u;
@@ -1686,7 +1727,9 @@ __global__ void k_lru_delta(Dev d, uint32_t nslow, int* delta, uint8_t* minus) {
 		const bool carried = ss.carry != 0;
 		const uint32_t first = ss.first_c ? ~ss.first_c : kNone;
 		const bool plus = !carried && first == i;
-		const bool close = (d.ev[i].flags & FLAG_END) && i + 1 == ss.last_ev && (carried || (first != kNone && first <= i));
+		// the session's last event of the batch: the last of its group in the sorted order
+		const bool last = j + 1 == nslow || (uint32_t)(d.slow_keys[j + 1] >> 32) != (uint32_t)(d.slow_keys[j] >> 32);
+		const bool close = (d.ev[i].flags & FLAG_END) && last && (carried || (first != kNone && first <= i));
 		delta[i] = (plus ? 1 : 0) - (close ? 1 : 0);
 		minus[i] = close ? 1 : 0;
 	}
@@ -2658,8 +2701,9 @@ hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
-hipError_t launch_carry_insert(const Dev& d, hipStream_t st) {
-	hipLaunchKernelGGL(k_carry_insert, dim3(grid_for(d.n_carry_in, 256, 256)), dim3(256), 0, st, d);
+hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_sset_size, dim3(1), dim3(1), 0, st, d, cap);
+	hipLaunchKernelGGL(k_sset_build, dim3(cus * 4), dim3(256), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus) {
