@@ -23,6 +23,7 @@ hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
 hipError_t launch_emit(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_net_merge(const Dev& d, const ebd_service_net* rec, uint32_t n, hipStream_t st, int cus);
 struct SessState;
 hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* minus, int* scan, void* tmp, size_t tmp_bytes,
 		hipStream_t st, int cus);
@@ -1151,6 +1152,57 @@ int ebd_collect_networks(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_
 		return -ENOSPC;
 	if (cnt)
 		HIP_TRY(hipMemcpy(out, c->d_netdump, cnt * sizeof(ebd_service_net), hipMemcpyDeviceToHost));
+	return 0;
+}
+
+int ebd_collect_networks_device(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_t* n) {
+	if (!c || !n)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	*n = 0;
+	if (!c->net_on)
+		return 0;
+	HIP_TRY(hipSetDevice(c->device));
+	if (!out && !c->d_netdump)
+		HIP_TRY(hipMalloc(&c->d_netdump, (size_t)c->net_cap * sizeof(ebd_service_net)));
+	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_net_dump(make_dev(c), out ? out : c->d_netdump, out ? cap : c->net_cap, c->d_cnt, c->stream, c->cus));
+	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	const uint64_t cnt = c->h_ctr[CTR_COUNT];
+	*n = (uint32_t)cnt;
+	return out && cnt > cap ? -ENOSPC : 0;
+}
+
+int ebd_merge_networks_device(ebd_ctx* c, const ebd_service_net* recs, uint32_t n) {
+	if (!c || (n && !recs))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	if (n == 0)
+		return 0;
+	if (!c->net_on)
+		return -EINVAL; // a context without network counters has no maps to merge into
+	HIP_TRY(hipSetDevice(c->device));
+	Dev d = make_dev(c);
+	d.n = 0;
+	HIP_TRY(launch_net_merge(d, recs, n, c->stream, c->cus));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_reset_services(ebd_ctx* c) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
+	if (c->net_on) {
+		HIP_TRY(hipMemsetAsync(c->d_nets[c->net_cur], 0, (size_t)c->net_cap * sizeof(NetEnt), c->stream));
+		HIP_TRY(hipMemsetAsync(c->d_v6d[c->net_cur], 0, (size_t)c->v6d_cap * sizeof(unsigned long long), c->stream));
+		HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_NETS, 0, 2 * sizeof(unsigned long long), c->stream)); // CTR_NETS, CTR_V6D
+	}
 	return 0;
 }
 

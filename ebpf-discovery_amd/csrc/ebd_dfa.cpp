@@ -136,7 +136,7 @@ GenParser represent(const KeyTrie* t, const AState& a, int variant) {
 void build_lds_image(const DfaTable* t, uint8_t* out) {
 	std::memset(out, 0, kLdsTableBytes);
 	for (uint32_t st = 0; st < kLdsRows; st++)
-		for (uint32_t b = 0; b < 256; b++)
+		for (uint32_t b = 0; b < kLdsCols; b++)
 #ifdef EBD_STATE_MAJOR
 			out[st * 256 + b] = t->next[st * 256 + b];
 #else
@@ -318,6 +318,10 @@ int build_dfa(const KeyTrie* trie, DfaTable* out) {
 	}
 	if (nvl > 2)
 		return -6;
+	for (uint32_t st = 0; st < 256; st++) // the LDS image's 128 columns (ebd_dfa.h kLdsCols)
+		for (uint32_t b = 128; b < 256; b++)
+			if (out->next[st * 256 + b] != out->next[st * 256 + 127])
+				return -8;
 	for (uint32_t st = 0; st < 256; st++) {
 		uint32_t a = out->attr[st];
 		a |= st == in.url_id ? A_URL : 0u;

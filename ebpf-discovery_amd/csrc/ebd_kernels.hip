@@ -351,7 +351,7 @@ struct LdsTable {
 #ifdef EBD_STATE_MAJOR
 	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
 #else
-	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[(i & 0xffu) * kLdsStride + (i >> 8)]; }
+	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[min(i & 0xffu, kLdsCols - 1) * kLdsStride + (i >> 8)]; }
 #endif
 };
 
@@ -421,7 +421,7 @@ __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t x, int k) {
 #ifdef EBD_STATE_MAJOR // entry (s, b) at s * 256 + b: one v_perm_b32 builds the index
 	return __builtin_amdgcn_perm(s, x, 0x0c0c0400u | (uint32_t)(k & 3));
 #else
-	return __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8) * kLdsStride + s;
+	return min(__builtin_amdgcn_ubfe(x, 8 * (k & 3), 8), kLdsCols - 1) * kLdsStride + s;
 #endif
 }
 
@@ -614,7 +614,11 @@ static_assert(R_WORDS == 20, "finalize record is 20 words");
 // that left L2 while the lane scanned the rest of the buffer.  Rows are structure of
 // arrays too: word j of the row of lane (or slot) l at [j * stride + l], one row of slack.
 #ifndef EBD_NO_STAGING
-constexpr uint32_t kStage = 64, kStageWords = kStage / 4;
+#ifndef EBD_STAGE
+#define EBD_STAGE 96 // window 0 and the first half of window 1 (the request line and, mostly, Host)
+#endif
+constexpr uint32_t kStage = EBD_STAGE, kStageWords = kStage / 4;
+static_assert(kStage >= 64 && kStage <= 128 && kStage % 16 == 0, "staging: window 0 plus whole chunks of window 1");
 #else // experiment: finalize reads every byte from the buffer (no LDS staging)
 constexpr uint32_t kStage = 0, kStageWords = 1;
 #endif
@@ -973,6 +977,15 @@ void k_fresh(Dev d) {
 						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
 #endif
 			}
+#ifndef EBD_NO_STAGING
+			if (w0 == 1) {
+#pragma unroll
+				for (int k = 0; k < (int)(kStage - 64) / 16; k++) // window 1's first chunks
+#pragma unroll
+					for (int j = 0; j < 4; j++)
+						stg[(16 + 4 * k + j) * kScanLanes] = X[k].w[j];
+			}
+#endif
 #if defined(EBD_EXP_SPLIT4) // experiment: every chunk its own chain (ILP probe; results are wrong)
 			{
 				uint32_t sx[4], m[4], qs[4], qm[4];
@@ -2475,6 +2488,45 @@ __global__ void k_net_dump(Dev d, ebd_service_net* out, uint32_t cap, unsigned l
 	}
 }
 
+// The slot of the service with key (lo, hi), kNone if the table has none (find only).
+__device__ uint32_t slot_find(const Dev& d, unsigned long long lo, unsigned long long hi) {
+	uint32_t idx = (uint32_t)lo & d.slot_mask;
+	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
+		const Slot* s = d.slots + idx;
+		const unsigned long long t = s->tag;
+		if (t == 0)
+			return kNone;
+		if (t == lo && s->hi == hi)
+			return idx;
+		idx = (idx + 1) & d.slot_mask;
+	}
+	return kNone;
+}
+
+// Network-map entries of other GPUs (ebd_service_net, k_net_dump's records) into the maps of
+// this context's services: the entry's service is found by its key, the entry is claimed or
+// found like a request's (net_touch), its last-seen time is the later one, and an entry new
+// to the map (or erased there) adds one to the map's size (Aggregator.cpp:89-106 across GPUs).
+__global__ void k_net_merge(Dev d, const ebd_service_net* rec, uint32_t n) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const ebd_service_net r = rec[k];
+		const uint32_t slot = slot_find(d, r.key_lo, r.key_hi);
+		if (slot == kNone || r.kind < NET_V4_16 || r.kind > NET_V6 || r.time_ns == 0) {
+			set_error(d, EBD_ERR_INTERNAL); // not what an export of merged services sends
+			continue;
+		}
+		unsigned long long pfx = 0;
+		for (int b = 0; b < 6; b++)
+			pfx |= (unsigned long long)r.prefix[b] << (8 * b);
+		const uint32_t v = r.kind == NET_V6 ? v6d_index(d, pfx) : (uint32_t)pfx;
+		if (v == kNone)
+			continue;
+		NetEnt* e = net_find_or_claim(d, d.nets, d.net_mask, net_key(r.kind, slot, v));
+		if (e && atomicMax(&e->time, r.time_ns) == 0)
+			atomicAdd(&d.slots[slot].nets[r.kind - 1], 1u);
+	}
+}
+
 // ---------------------------------------------------------------------------------
 // Cross-GPU merge.  Export: the collected services grouped by owner GPU
 // (key_lo % world) with their endpoint bytes; merge: received records inserted into the
@@ -2807,6 +2859,10 @@ hipError_t launch_net_remap(const Dev& d, const NetEnt* old, uint32_t old_mask, 
 		const unsigned long long* old_v6d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_net_remap, dim3(grid_for((uint64_t)old_mask + 1, 256, cus * 8)), dim3(256), 0, st, d, old, old_mask, remap,
 			old_v6d);
+	return hipGetLastError();
+}
+hipError_t launch_net_merge(const Dev& d, const ebd_service_net* rec, uint32_t n, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_net_merge, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n);
 	return hipGetLastError();
 }
 hipError_t launch_net_dump(const Dev& d, ebd_service_net* out, uint32_t cap, unsigned long long* count, hipStream_t st, int cus) {

@@ -118,6 +118,9 @@ _SIGS = {
     "ebd_collect_services": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
                                        C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_clear": (C.c_int, [C.c_void_p]),
+    "ebd_reset_services": (C.c_int, [C.c_void_p]),
+    "ebd_collect_networks_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "ebd_merge_networks_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "ebd_set_clock": (C.c_int, [C.c_void_p, C.c_uint64]),
     "ebd_network_counters_cleaning": (C.c_int, [C.c_void_p, C.c_uint64]),
     "ebd_collect_networks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
@@ -363,6 +366,28 @@ class Context:
 
     def clear(self):
         _check(lib().ebd_clear(self.h), "ebd_clear")
+
+    def reset_services(self):
+        """ebd_reset_services: every service and network-map entry goes (the merge's start)."""
+        _check(lib().ebd_reset_services(self.h), "ebd_reset_services")
+
+    def networks_device(self, device):
+        """ebd_collect_networks_device: the network-map entries as a device uint8 tensor of
+        SERVICE_NET_DTYPE records (32 bytes each)."""
+        import torch
+        n = C.c_uint32()
+        _check(lib().ebd_collect_networks_device(self.h, None, 0, C.byref(n)), "ebd_collect_networks_device")
+        out = torch.empty(max(n.value, 1) * SERVICE_NET_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        _check(lib().ebd_collect_networks_device(self.h, C.c_void_p(out.data_ptr()), max(n.value, 1), C.byref(n)),
+               "ebd_collect_networks_device")
+        return out[:n.value * SERVICE_NET_DTYPE.itemsize]
+
+    def merge_networks_device(self, recs):
+        """ebd_merge_networks_device: SERVICE_NET_DTYPE records (device uint8 tensor) into the
+        maps of this table's services (merge the services first)."""
+        n = recs.numel() // SERVICE_NET_DTYPE.itemsize
+        _check(lib().ebd_merge_networks_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n),
+               "ebd_merge_networks_device")
 
     def set_clock(self, now_ns):
         """Aggregator::getCurrentTime (steady-clock ns) of the next batches' requests; 0 = CLOCK_MONOTONIC."""

@@ -275,23 +275,72 @@ def gather_rows(table, group=None):
 
 def device_exchange_merge(ctx, device, group=None, map_first=None):
     """GPU path: export by owner on the device, exchange over RCCL, merge on the device into
-    this rank's context (cleared first).  map_first(first_seq int64 tensor) -> trace
-    positions, applied before the exchange.  Returns {sent, received, record_bytes,
-    string_bytes}: this rank's records out and in, and the bytes it sent."""
+    this rank's context (reset first).  With network counters the services' network-map
+    entries follow their services to the owner (one more all_to_all of 32-byte records) and
+    merge into its maps (union, later last-seen time).  map_first(first_seq int64 tensor) ->
+    trace positions, applied before the exchange.  Returns {sent, received, record_bytes,
+    string_bytes, net_sent, net_received}: this rank's records out and in, and the bytes it
+    sent."""
     import torch.distributed as dist
-    if getattr(ctx, "network_counters", False):
-        # the merge carries client counters only: network maps are per context (DESIGN.md section 7)
-        raise ValueError("device_exchange_merge: contexts with network counters are not merged across GPUs")
     world = dist.get_world_size(group)
     check_same_hash_key(ctx, device, group)
     recs, strs, counts, scounts = ctx.export_services_device(world, device)
     if map_first is not None:
         map_wire_first(recs, map_first)
+    nets = ncounts = None
+    if getattr(ctx, "network_counters", False):
+        nets, ncounts = group_by_owner(ctx.networks_device(device), NET_REC_BYTES, world)
     out_r, out_s = exchange(recs, strs, counts, scounts, group)
-    ctx.clear()
+    ctx.reset_services()
     ctx.merge_services_device(out_r, out_s)
+    out_n = None
+    if nets is not None:
+        out_n = exchange_fixed(nets, ncounts, NET_REC_BYTES, group)
+        ctx.merge_networks_device(out_n)
     return {"sent": int(counts.sum()), "received": out_r.numel() // REC.itemsize,
-            "record_bytes": recs.numel(), "string_bytes": strs.numel()}
+            "record_bytes": recs.numel(), "string_bytes": strs.numel(),
+            "net_sent": int(ncounts.sum()) if ncounts is not None else 0,
+            "net_received": out_n.numel() // NET_REC_BYTES if out_n is not None else 0}
+
+
+NET_REC_BYTES = 32  # ebd_service_net
+
+
+def owner_of(key_lo, world):
+    """key_lo % world for uint64 keys held in an int64 tensor (the services' owner rule)."""
+    hi = (key_lo >> 32) & 0xFFFFFFFF
+    lo = key_lo & 0xFFFFFFFF
+    return (hi * ((1 << 32) % world) + lo) % world
+
+
+def group_by_owner(recs, size, world):
+    """Records (uint8 tensor of `size`-byte records starting with key_lo) reordered by owner
+    (stable); returns (records, counts[world] numpy)."""
+    import torch
+    n = recs.numel() // size
+    if n == 0:
+        return recs, np.zeros(world, np.int64)
+    key_lo = recs.view(torch.int64).view(n, size // 8)[:, 0]
+    own = owner_of(key_lo, world)
+    order = torch.argsort(own, stable=True)
+    out = recs.view(n, size)[order].reshape(-1)
+    return out, torch.bincount(own, minlength=world).cpu().numpy().astype(np.int64)
+
+
+def exchange_fixed(recs, counts, size, group=None):
+    """One all_to_all_single of owner-grouped fixed-size records (counts per destination)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    dev = recs.device
+    sizes = torch.tensor(np.asarray(counts, np.int64), device=dev)
+    rsizes = torch.empty_like(sizes)
+    dist.all_to_all_single(rsizes, sizes, group=group)
+    rc = rsizes.cpu().numpy()
+    out = torch.empty(int(rc.sum()) * size, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out, recs, output_split_sizes=[int(c) * size for c in rc],
+                           input_split_sizes=[int(c) * size for c in counts], group=group)
+    return out
 
 
 def map_wire_first(recs, fn):

@@ -296,6 +296,10 @@ int ebd_collect_services(ebd_ctx* ctx, ebd_service* out, uint32_t cap, uint32_t*
  * On: a service whose three network sets are all empty goes; the others stay with their
  * client counters zeroed (their domain, scheme and sets are kept). */
 int ebd_clear(ebd_ctx* ctx);
+/* Every service and every network-map entry goes: the table as ebd_ctx_create left it.
+ * The cross-GPU merge starts from it (ebd_clear keeps the services that have network maps,
+ * which would then be reported by their owner GPU and by this one). */
+int ebd_reset_services(ebd_ctx* ctx);
 
 /* --- network counters (EBD_CFG_NETWORK_COUNTERS) -------------------------------------- */
 /* Aggregator::getCurrentTime for the requests of the batches submitted from now on
@@ -308,6 +312,16 @@ int ebd_set_clock(ebd_ctx* ctx, uint64_t now_ns);
 int ebd_network_counters_cleaning(ebd_ctx* ctx, uint64_t now_ns);
 /* The network-set entries of every service (out == NULL: count only).  Order unspecified. */
 int ebd_collect_networks(ebd_ctx* ctx, ebd_service_net* out, uint32_t cap, uint32_t* n);
+/* The same records into a DEVICE array (out == NULL: *n only; -ENOSPC past cap): what a GPU
+ * sends to the owners of its services for the cross-GPU merge (owner = key_lo % world). */
+int ebd_collect_networks_device(ebd_ctx* ctx, ebd_service_net* out, uint32_t cap, uint32_t* n);
+/* Merges n network-map entries (a DEVICE array, ebd_service_net records of other GPUs) into
+ * the maps of this context's services, found by key: merge the services first
+ * (ebd_merge_services_device); an entry whose service is missing is reported as
+ * EBD_ERR_INTERNAL.  An entry new to its map adds one to the map's size; the last-seen time
+ * is the later one (Aggregator.cpp:89-106, 182-209 across GPUs).  -EINVAL without network
+ * counters. */
+int ebd_merge_networks_device(ebd_ctx* ctx, const ebd_service_net* recs, uint32_t n);
 
 /* --- the service report (Discovery::outputServicesToStdout, Discovery.cpp:60-71) ------- */
 /* The report text byte for byte: {"service":[...]} through boost::json::ext::print

@@ -204,3 +204,68 @@ def test_v6_dictionary_does_not_fill_across_cleanings_and_clears():
             ctx.clear()
             o.clear()
         assert gpu_nets(ctx) == o.nets(), k
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config5_network_maps_merge_across_shards(world):
+    """Config 5 with network counters: each connection shard on its own context with its
+    own clock (shard r at T0 + r min), services and network-map entries exported by owner,
+    merged into owner contexts (ebd_merge_services_device, then ebd_merge_networks_device).
+    The owners' services with their map sizes equal the oracle's over the whole trace, and
+    every map entry is the union of the shards' entries with the latest last-seen time."""
+    import torch
+    from ebd import shard
+    dev = torch.device("cuda:0")
+    N = 200_000
+    ev_all, lens_all, offs_all, pay_all = ebd.generate_host(5, 5, 0, N, align=16)
+    segs = [[] for _ in range(world)]
+    want_nets = {}
+    for r in range(world):
+        ctx = ebd.Context(max_events=N, service_capacity=1 << 19, hash_key=ebd.TEST_HASH_KEY, network_counters=True,
+                          net_capacity=1 << 20)
+        ctx.set_clock(T0 + r * MIN)
+        k, size = ebd.trace_size_device(ctx, 5, 5, 0, N, align=16, shard=(world, r), with_events=True)
+        ev = torch.empty(k * 36, dtype=torch.uint8, device=dev)
+        ln = torch.empty(k, dtype=torch.int32, device=dev)
+        of = torch.empty(k, dtype=torch.int64, device=dev)
+        gi = torch.empty(k, dtype=torch.int64, device=dev)
+        pay = torch.zeros(size + 64, dtype=torch.uint8, device=dev)
+        ebd.generate_device(ctx, 5, 5, 0, N, ev, ln, of, pay, pay.numel(), align=16, shard=(world, r), gidx=gi)
+        ctx.submit_device(ev, ln, of, pay, k)
+        ctx.sync()
+        assert ctx.stats()["errors"] == 0
+        recs, strs, counts, scounts = ctx.export_services_device(world, dev)
+        shard.map_wire_first(recs, lambda f: gi[f])
+        nets, ncounts = shard.group_by_owner(ctx.networks_device(dev), shard.NET_REC_BYTES, world)
+        ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))]) * ebd.WIRE_DTYPE.itemsize
+        so = np.concatenate([[0], np.cumsum(scounts.astype(np.int64))])
+        no = np.concatenate([[0], np.cumsum(ncounts)]) * shard.NET_REC_BYTES
+        for w in range(world):
+            segs[w].append((recs[ro[w]:ro[w + 1]], strs[so[w]:so[w + 1]], nets[no[w]:no[w + 1]]))
+        # the shard's own entries, from the oracle over the shard at the shard's clock
+        idx = gi.cpu().numpy()
+        lens_s, offs_s, pay_s = T.pack([pay_all[offs_all[i]:offs_all[i] + lens_all[i]].tobytes() for i in idx])
+        o_r = O.Oracle(network_counters=True)
+        o_r.set_time(T0 + r * MIN)
+        o_r.process(ev_all[idx], lens_s, offs_s, pay_s)
+        for (pid, ep, kind, pfx, t) in o_r.nets():
+            want_nets[(pid, ep, kind, pfx)] = max(t, want_nets.get((pid, ep, kind, pfx), 0))
+        ctx.close()
+    got_svc, got_nets = [], []
+    for parts in segs:
+        m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY, network_counters=True,
+                        net_capacity=1 << 20)
+        m.merge_services_device(torch.cat([r for r, _, _ in parts]),
+                                torch.cat([s for _, s, _ in parts] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8,
+                                                                                  device=dev)]))
+        m.merge_networks_device(torch.cat([n for _, _, n in parts]))
+        assert m.stats()["errors"] == 0, m.stats()
+        got_svc += m.services(with_nets=True)
+        got_nets += gpu_nets(m)
+        m.close()
+    o = O.Oracle(network_counters=True)
+    o.set_time(T0)
+    o.process(ev_all, lens_all, offs_all, pay_all)
+    assert sorted(got_svc) == o.services_nets()
+    assert sorted(got_nets) == sorted((pid, ep, kind, pfx, t) for (pid, ep, kind, pfx), t in want_nets.items())
+    assert len(got_nets) == len(o.nets())

@@ -182,3 +182,41 @@ def test_exchange_checks_hash_keys_and_keeps_missing_endpoints(same, tmp_path):
     assert r0["eps"] == [None, None, "ab1"]
     assert r1["eps"] == ["ab0"]
     assert r0["nbytes"] == 8 + shard.STR_SLACK
+
+
+def _net_worker(rank, world, port, out_path):
+    """Network-map records (ebd_service_net, 32 B, key_lo first) grouped by owner and
+    exchanged with one all_to_all: every rank must receive exactly the records it owns."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
+    try:
+        rng = np.random.default_rng(40 + rank)
+        recs = np.zeros(500 + 37 * rank, ebd.SERVICE_NET_DTYPE)
+        recs["key_lo"] = rng.integers(0, 2**64, recs.size, dtype=np.uint64)  # high bit set half the time
+        recs["key_hi"] = rng.integers(0, 2**64, recs.size, dtype=np.uint64)
+        recs["kind"] = 1 + rank
+        recs["time_ns"] = np.arange(recs.size, dtype=np.uint64) + 1000 * rank
+        t = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+        grouped, counts = shard.group_by_owner(t, shard.NET_REC_BYTES, world)
+        got = shard.exchange_fixed(grouped, counts, shard.NET_REC_BYTES).numpy().view(ebd.SERVICE_NET_DTYPE)
+        owners = (got["key_lo"] % np.uint64(world)).astype(int).tolist()
+        with open(out_path % rank, "w") as f:
+            json.dump({"n": int(recs.size), "counts": counts.tolist(), "owners": owners,
+                       "sent_own": int(np.sum(recs["key_lo"] % np.uint64(world) == np.uint64(rank))),
+                       "got": sorted([int(x) for x in got["key_lo"]])}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_network_records_reach_their_owner(tmp_path):
+    """The network-map exchange of device_exchange_merge (shard.group_by_owner's uint64
+    owner rule on int64 tensors, shard.exchange_fixed) over a world-2 gloo group."""
+    out_path = str(tmp_path / "n%d.json")
+    mp.start_processes(_net_worker, args=(2, _free_port(), out_path), nprocs=2, join=True, start_method="spawn")
+    r = [json.load(open(out_path % k)) for k in (0, 1)]
+    for k in (0, 1):
+        assert all(o == k for o in r[k]["owners"])
+        assert sum(r[k]["counts"]) == r[k]["n"]
+    assert len(r[0]["got"]) + len(r[1]["got"]) == r[0]["n"] + r[1]["n"]
+    assert r[0]["counts"][0] == r[0]["sent_own"] and r[1]["counts"][1] == r[1]["sent_own"]
