@@ -167,6 +167,7 @@ struct ebd_ctx {
 	unsigned long long* d_v6d[2] = {nullptr, nullptr}; // v6 prefix dictionary, swapped with d_nets
 	uint32_t v6d_cap = 0;
 	uint64_t clock_ns = 0; // ebd_set_clock (0: CLOCK_MONOTONIC per batch)
+	const uint64_t* ev_times = nullptr; // ebd_set_event_clock: the next batch's per-event readings (device)
 	KeepRec* d_keep = nullptr;
 	uint64_t keep_cap = 0;
 	unsigned long long* d_kbytes = nullptr;
@@ -604,6 +605,8 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	d.payload = payload;
 	d.n = n;
 	d.now = ctx_now(c);
+	d.times = (const unsigned long long*)c->ev_times; // for this batch only
+	c->ev_times = nullptr;
 	d.cstage_per = agg_stage_per_block(n, c->cus);
 	c->last_n = n;
 	c->last_slow_ran = 0;
@@ -1104,6 +1107,14 @@ int ebd_set_clock(ebd_ctx* c, uint64_t now_ns) {
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	c->clock_ns = now_ns;
+	return 0;
+}
+
+int ebd_set_event_clock(ebd_ctx* c, const uint64_t* time_ns) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	c->ev_times = time_ns;
 	return 0;
 }
 

@@ -181,6 +181,7 @@ struct Dev {
 	// network counters (EBD_CFG_NETWORK_COUNTERS)
 	uint32_t net_on;
 	unsigned long long now; // Aggregator::getCurrentTime of this batch's requests (>= 1)
+	const unsigned long long* times; // or per event (ebd_set_event_clock), nullptr: `now` for all
 	NetEnt* nets;
 	uint32_t net_mask;
 	unsigned long long* v6d;

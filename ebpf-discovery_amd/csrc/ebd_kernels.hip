@@ -234,23 +234,27 @@ __device__ NetEnt* net_find_or_claim(const Dev& d, NetEnt* nets, uint32_t mask, 
 	return nullptr;
 }
 
-__device__ void net_touch(const Dev& d, uint32_t slot, uint32_t kind, uint32_t value) {
+__device__ void net_touch(const Dev& d, uint32_t slot, uint32_t kind, uint32_t value, unsigned long long now) {
 	NetEnt* e = net_find_or_claim(d, d.nets, d.net_mask, net_key(kind, slot, value));
-	if (e && atomicMax(&e->time, d.now) == 0) // new, or erased by networkCountersCleaning
+	if (e && atomicMax(&e->time, now) == 0) // new, or erased by networkCountersCleaning
 		atomicAdd(&d.slots[slot].nets[kind - 1], 1u);
 }
 
 // incrementServiceClientsNumber's network part for an external client (net: net_pack).
-__device__ void agg_nets(const Dev& d, uint32_t slot, unsigned long long net) {
+// Aggregator::getCurrentTime of the request finished by event i: the event's own reading when
+// the batch carries them (ebd_set_event_clock), else the batch's.
+__device__ __forceinline__ unsigned long long request_time(const Dev& d, uint32_t i) { return d.times ? d.times[i] : d.now; }
+
+__device__ void agg_nets(const Dev& d, uint32_t slot, unsigned long long net, unsigned long long now) {
 	if (slot == kNone)
 		return;
 	if (net & kNetV6) {
 		const uint32_t v = v6d_index(d, net & 0xffffffffffffull);
 		if (v != kNone)
-			net_touch(d, slot, NET_V6, v);
+			net_touch(d, slot, NET_V6, v, now);
 	} else {
-		net_touch(d, slot, NET_V4_24, (uint32_t)(net & 0xffffffu));
-		net_touch(d, slot, NET_V4_16, (uint32_t)(net & 0xffffu));
+		net_touch(d, slot, NET_V4_24, (uint32_t)(net & 0xffffffu), now);
+		net_touch(d, slot, NET_V4_16, (uint32_t)(net & 0xffffu), now);
 	}
 }
 
@@ -1411,7 +1415,7 @@ __global__ void k_emit(Dev d) {
 			claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull),
 					wave_add(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)), ev.pid, dst, hl, dst + hl, ul);
 		if (d.net_on && cls == CLS_EXTERNAL)
-			agg_nets(d, slot, net);
+			agg_nets(d, slot, net, request_time(d, i));
 		sr.str_off = (uint32_t)at;
 		sr.host_len = (uint16_t)hl;
 		sr.url_len = (uint16_t)ul;
@@ -1983,7 +1987,7 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
 			cls == CLS_INTERNAL, cls == CLS_EXTERNAL, &claimed);
 	if (d.net_on && cls == CLS_EXTERNAL)
-		agg_nets(d, slot, net);
+		agg_nets(d, slot, net, request_time(d, i));
 	if (claimed) { // at most one claim per event: the block's stretch holds them all
 		const uint32_t k = atomicAdd(&sh.cn, 1u);
 		const unsigned long long at = (unsigned long long)blockIdx.x * d.cstage_per + k;

@@ -119,6 +119,7 @@ _SIGS = {
                                        C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_clear": (C.c_int, [C.c_void_p]),
     "ebd_reset_services": (C.c_int, [C.c_void_p]),
+    "ebd_set_event_clock": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ebd_collect_networks_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     "ebd_merge_networks_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "ebd_set_clock": (C.c_int, [C.c_void_p, C.c_uint64]),
@@ -392,6 +393,13 @@ class Context:
     def set_clock(self, now_ns):
         """Aggregator::getCurrentTime (steady-clock ns) of the next batches' requests; 0 = CLOCK_MONOTONIC."""
         _check(lib().ebd_set_clock(self.h, now_ns), "ebd_set_clock")
+
+    def set_event_clock(self, times):
+        """ebd_set_event_clock: per-event getCurrentTime readings (a device int64/uint64 tensor
+        of the next batch's n events; kept referenced until the batch is done) or None."""
+        self._ev_times = times
+        _check(lib().ebd_set_event_clock(self.h, C.c_void_p(times.data_ptr()) if times is not None else None),
+               "ebd_set_event_clock")
 
     def network_counters_cleaning(self, now_ns=0):
         _check(lib().ebd_network_counters_cleaning(self.h, now_ns), "ebd_network_counters_cleaning")

@@ -307,6 +307,12 @@ int ebd_reset_services(ebd_ctx* ctx);
  * CLOCK_MONOTONIC is read when each batch is submitted.  The reference reads the clock per
  * request; one reading per poll cycle differs by at most the cycle's length. */
 int ebd_set_clock(ebd_ctx* ctx, uint64_t now_ns);
+/* Aggregator::getCurrentTime per request, as the reference reads it (Aggregator.cpp:162,165):
+ * time_ns is a DEVICE array of the next submitted batch's n events, and the request an event
+ * finishes takes that event's reading (the consumer's clock when it handled the event).  It
+ * applies to that one batch (NULL: the batch clock of ebd_set_clock).  The array must stay
+ * valid until the batch's work is done (ebd_sync). */
+int ebd_set_event_clock(ebd_ctx* ctx, const uint64_t* time_ns);
 /* Aggregator::networkCountersCleaning (Aggregator.cpp:182-209): every set entry last seen
  * at least one hour before now_ns is erased (0 = the context clock). */
 int ebd_network_counters_cleaning(ebd_ctx* ctx, uint64_t now_ns);

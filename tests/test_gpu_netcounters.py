@@ -269,3 +269,36 @@ def test_config5_network_maps_merge_across_shards(world):
     assert sorted(got_svc) == o.services_nets()
     assert sorted(got_nets) == sorted((pid, ep, kind, pfx, t) for (pid, ep, kind, pfx), t in want_nets.items())
     assert len(got_nets) == len(o.nets())
+
+
+@pytest.mark.parametrize("trace", ["config3", "fragmented"])
+def test_per_event_clock_matches_per_request_time(trace):
+    """ebd_set_event_clock: every request takes the clock reading of the event that finishes
+    it, as the reference reads getCurrentTime per request (Aggregator.cpp:162,165); the
+    oracle is fed one event at a time at that event's time.  The readings span 1.7 hours,
+    so the cleaning at +1.5 h erases exactly the entries last seen in the first half hour."""
+    import torch
+    if trace == "config3":
+        ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 4000)
+    else:
+        ev, lens, offs, payload = T.fragmented_trace(300, seed=12)
+    n = len(ev)
+    times = (T0 + np.arange(n, dtype=np.int64) * (6000 * 10**9 // n)).astype(np.int64)
+    ctx = ebd.Context(max_events=n, max_payload=payload.size, network_counters=True, net_capacity=1 << 16)
+    ctx.set_clock(T0)
+    ctx.set_event_clock(torch.from_numpy(times).to("cuda:0"))
+    ctx.submit(ev, lens, offs, payload)
+    ctx.sync()
+    o = O.Oracle(network_counters=True)
+    for i in range(n):
+        o.set_time(int(times[i]))
+        o.process(ev[i:i + 1], lens[i:i + 1], offs[i:i + 1], payload)
+    assert ctx.stats()["errors"] == 0
+    assert ctx.services(with_nets=True) == o.services_nets()
+    assert gpu_nets(ctx) == o.nets()
+    assert len({t for (_, _, _, _, t) in o.nets()}) > 100  # the readings differ per request
+    ctx.network_counters_cleaning(T0 + 90 * MIN)
+    o.network_counters_cleaning(T0 + 90 * MIN)
+    assert ctx.services(with_nets=True) == o.services_nets()
+    assert gpu_nets(ctx) == o.nets()
+    assert json_objects(ctx.report_json()) == json_objects(o.services_json())

@@ -25,12 +25,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=20_000_000)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--lru", type=int, default=0, help="LRU capacity (0: EBD_MAX_SESSIONS); below the trace's 4096 "
+                    "live connections the batch takes the exact LRU walker")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     E = args.events
     ctx = ebd.Context(max_events=E, service_capacity=1 << max(20, int(np.ceil(np.log2(E / 3.2 * 0.8)))),
-                      string_arena=max(256 << 20, E * 16), timing=True)
+                      string_arena=max(256 << 20, E * 16), timing=True, lru_capacity=args.lru)
     ev, ln, of, pay, gidx, n, size = bench.generate_shard(ctx, 4, 4, E, 1, 0, dev)
     for k in range(args.reps):
         ctx.clear()
