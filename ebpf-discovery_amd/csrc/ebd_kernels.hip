@@ -2496,12 +2496,19 @@ __global__ void k_net_dump(Dev d, ebd_service_net* out, uint32_t cap, unsigned l
 __device__ uint32_t slot_find(const Dev& d, unsigned long long lo, unsigned long long hi) {
 	uint32_t idx = (uint32_t)lo & d.slot_mask;
 	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
-		const Slot* s = d.slots + idx;
-		const unsigned long long t = s->tag;
+		Slot* s = d.slots + idx;
+		unsigned long long t = s->tag;
+		if (t == 0) // a plain load may see a stale line: the memory-side word decides
+			t = rmw_read(&s->tag);
 		if (t == 0)
 			return kNone;
-		if (t == lo && s->hi == hi)
-			return idx;
+		if (t == lo) {
+			unsigned long long h = s->hi;
+			if (h != hi)
+				h = rmw_read(&s->hi);
+			if (h == hi)
+				return idx;
+		}
 		idx = (idx + 1) & d.slot_mask;
 	}
 	return kNone;
@@ -2533,10 +2540,17 @@ __global__ void k_net_merge(Dev d, const ebd_service_net* rec, uint32_t n) {
 
 // ---------------------------------------------------------------------------------
 // Cross-GPU merge.  Export: the collected services grouped by owner GPU
-// (key_lo % world) with their endpoint bytes; merge: received records inserted into the
+// (owner_of(key_lo)) with their endpoint bytes; merge: received records inserted into the
 // owner's table with agg_insert (counters add, the smallest first word wins).
 // ---------------------------------------------------------------------------------
 constexpr int kOwnerMax = 64;
+
+// The GPU that owns a service in the cross-GPU merge: the key's high word mod world.  (Its low
+// bit is always set, the used-slot mark, so key_lo mod world would leave every even GPU
+// without services.)
+__device__ __forceinline__ uint32_t owner_of(unsigned long long key_lo, uint32_t world) {
+	return (uint32_t)(key_lo >> 32) % world;
+}
 
 // Per owner: records and (8-aligned) string bytes, block histograms in LDS.
 __global__ void k_owner_count(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cnt,
@@ -2547,7 +2561,7 @@ __global__ void k_owner_count(const ebd_service* rec, const unsigned long long* 
 	__syncthreads();
 	const unsigned long long n = ctr[CTR_SERVICES];
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-		const uint32_t w = (uint32_t)(rec[k].key_lo % world);
+		const uint32_t w = owner_of(rec[k].key_lo, world);
 		atomicAdd(&hc[w], 1ull);
 		atomicAdd(&hb[w], rec[k].endpoint_off == ~0ull ? 0ull : (unsigned long long)((rec[k].endpoint_len + 7u) & ~7u));
 	}
@@ -2568,7 +2582,7 @@ __global__ void k_owner_scatter(const ebd_service* rec, const unsigned long long
 	const unsigned long long n = ctr[CTR_SERVICES];
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
 		const ebd_service v = rec[k];
-		const uint32_t w = (uint32_t)(v.key_lo % world);
+		const uint32_t w = owner_of(v.key_lo, world);
 		const unsigned long long at = atomicAdd(&cur[w], 1ull);
 		ebd_wire_service o;
 		o.key_lo = v.key_lo;

@@ -292,8 +292,21 @@ class Context:
         _check(lib().ebd_fetch_results_async(self.h, _p(out), out.size, C.byref(n)), "ebd_fetch_results_async")
         return n.value
 
+    def _fence(self, *tensors):
+        """The context stream waits for the work torch queued for these tensors on its current
+        stream (the context stream is a non-blocking stream: it does not order itself after
+        torch's).  Raw pointers are the caller's to order."""
+        import torch
+        ts = [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
+        if not ts:
+            return
+        if getattr(self, "_ext", None) is None:
+            self._ext = torch.cuda.ExternalStream(lib().ebd_ctx_stream(self.h), device=ts[0].device)
+        self._ext.wait_stream(torch.cuda.current_stream(ts[0].device))
+
     def submit_device(self, events, lens, offs, payload, n):
         """Device-resident batch (torch tensors on the context's device or raw pointers)."""
+        self._fence(events, lens, offs, payload)
         b = DeviceBatch(events=_ptrval(events), len=_ptrval(lens), off=_ptrval(offs), payload=_ptrval(payload), n=n)
         _check(lib().ebd_submit_batch_device(self.h, C.byref(b)), "ebd_submit_batch_device")
 
@@ -387,6 +400,7 @@ class Context:
         """ebd_merge_networks_device: SERVICE_NET_DTYPE records (device uint8 tensor) into the
         maps of this table's services (merge the services first)."""
         n = recs.numel() // SERVICE_NET_DTYPE.itemsize
+        self._fence(recs)
         _check(lib().ebd_merge_networks_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n),
                "ebd_merge_networks_device")
 
@@ -398,6 +412,8 @@ class Context:
         """ebd_set_event_clock: per-event getCurrentTime readings (a device int64/uint64 tensor
         of the next batch's n events; kept referenced until the batch is done) or None."""
         self._ev_times = times
+        if times is not None:
+            self._fence(times)
         _check(lib().ebd_set_event_clock(self.h, C.c_void_p(times.data_ptr()) if times is not None else None),
                "ebd_set_event_clock")
 
@@ -426,7 +442,7 @@ class Context:
             buf = C.create_string_buffer(ln.value)
 
     def export_services_device(self, world, device):
-        """The services grouped by owner (key_lo % world) in device tensors: (WIRE_DTYPE
+        """The services grouped by owner ((key_lo >> 32) % world) in device tensors: (WIRE_DTYPE
         records as uint8 [n * 40], their endpoint bytes uint8, counts[world], str_counts[world])."""
         import torch
         counts = np.zeros(world, np.uint32)
@@ -444,6 +460,7 @@ class Context:
         """Inserts wire records (device uint8 tensors; strings readable 8 bytes past their
         bytes) into this table."""
         n = recs.numel() // WIRE_DTYPE.itemsize
+        self._fence(recs, strings)
         _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
                                                C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                strings.numel()), "ebd_merge_services_device")

@@ -8,7 +8,8 @@ collective.  The one exchange is at the end, the Aggregator merge:
   * every service carries its 128-bit key (a keyed PRF of pid + endpoint, the same on every
     GPU because the ranks share the key), its uint32 counters and the trace position of
     its first request with that request's scheme and host/url split;
-  * owner = key_lo mod world.  The GPU groups its services by owner on the device
+  * owner = (key_lo >> 32) mod world (key_lo is always odd: its low bit marks a used slot).
+    The GPU groups its services by owner on the device
     (ebd_export_services_device) and ONE all_to_all_single of 40-byte wire records and one
     of endpoint bytes ship each service to its owner, over RCCL (xGMI) on GPU tensors.  A
     record's bytes follow the previous record's (8-byte padded), so the received segments
@@ -143,7 +144,7 @@ class ServiceTable:
     def to_wire(self, world):
         """(wire records grouped by owner, their endpoint bytes in record order, each padded
         to 8, counts[world], str_counts[world]): what ebd_export_services_device returns."""
-        owner = (self.rec["key_lo"] % np.uint64(world)).astype(np.int64)
+        owner = owner_np(self.rec["key_lo"], world)
         order = np.argsort(owner, kind="stable")
         r, owner = self.rec[order], owner[order]
         w = np.zeros(r.size, REC)
@@ -307,10 +308,14 @@ NET_REC_BYTES = 32  # ebd_service_net
 
 
 def owner_of(key_lo, world):
-    """key_lo % world for uint64 keys held in an int64 tensor (the services' owner rule)."""
-    hi = (key_lo >> 32) & 0xFFFFFFFF
-    lo = key_lo & 0xFFFFFFFF
-    return (hi * ((1 << 32) % world) + lo) % world
+    """The owner GPU of uint64 keys held in an int64 tensor: (key_lo >> 32) % world (ebd_kernels.hip
+    owner_of)."""
+    return ((key_lo >> 32) & 0xFFFFFFFF) % world
+
+
+def owner_np(key_lo, world):
+    """owner_of for a numpy uint64 array."""
+    return ((np.asarray(key_lo, np.uint64) >> np.uint64(32)) % np.uint64(world)).astype(np.int64)
 
 
 def group_by_owner(recs, size, world):
@@ -372,7 +377,7 @@ def host_domain(host):
 
 
 def check_same_hash_key(ctx, device, group=None):
-    """Owners are key_lo mod world: a rank keyed with another secret would send the same
+    """Owners come from the key: a rank keyed with another secret would send the same
     (pid, endpoint) to another owner and the merged table would hold it twice.  Raises unless
     every rank's context uses the same service-key secret."""
     import torch

@@ -243,7 +243,10 @@ int ebd_set_interfaces(ebd_ctx* ctx, const ebd_ipv4_network* v4, uint32_t n4, co
 int ebd_submit_batch(ebd_ctx* ctx, const ebd_discovery_event* events, const uint32_t* len, const uint64_t* off,
 		const uint8_t* payload, uint64_t payload_bytes, uint32_t n);
 /* The same with the batch already in HBM.  The host waits only for the fresh pass's counters
- * (is there session work?); the rest stays queued on the context stream (ebd_sync). */
+ * (is there session work?); the rest stays queued on the context stream (ebd_sync).
+ * DEVICE inputs, here and in every *_device call, are read on the context stream
+ * (ebd_ctx_stream), a non-blocking stream: work that produces them on another stream must be
+ * ordered before the call (e.g. hipStreamWaitEvent on the context stream). */
 int ebd_submit_batch_device(ebd_ctx* ctx, const ebd_device_batch* batch);
 /* Waits for every queued upload, batch and read-back of the context. */
 int ebd_sync(ebd_ctx* ctx);
@@ -319,7 +322,7 @@ int ebd_network_counters_cleaning(ebd_ctx* ctx, uint64_t now_ns);
 /* The network-set entries of every service (out == NULL: count only).  Order unspecified. */
 int ebd_collect_networks(ebd_ctx* ctx, ebd_service_net* out, uint32_t cap, uint32_t* n);
 /* The same records into a DEVICE array (out == NULL: *n only; -ENOSPC past cap): what a GPU
- * sends to the owners of its services for the cross-GPU merge (owner = key_lo % world). */
+ * sends to the owners of its services for the cross-GPU merge (owner = (key_lo >> 32) % world). */
 int ebd_collect_networks_device(ebd_ctx* ctx, ebd_service_net* out, uint32_t cap, uint32_t* n);
 /* Merges n network-map entries (a DEVICE array, ebd_service_net records of other GPUs) into
  * the maps of this context's services, found by key: merge the services first
@@ -358,7 +361,8 @@ typedef struct ebd_wire_service {
 /* Bytes a wire record's endpoint takes in the strings. */
 #define EBD_WIRE_BYTES(len) (((len) & EBD_WIRE_NO_BYTES) ? 0u : (((len) + 7u) & ~7u))
 
-/* The context's services grouped by owner GPU, owner = key_lo % world, into DEVICE arrays:
+/* The context's services grouped by owner GPU, owner = (key_lo >> 32) % world (key_lo is always
+ * odd: its low bit marks a used slot), into DEVICE arrays:
  * recs[] ordered by owner (counts[w] records for owner w), strings[] their endpoint bytes in
  * record order (str_counts[w] bytes for owner w).  counts / str_counts are host arrays of
  * `world` entries.  recs == NULL: sizes only. */

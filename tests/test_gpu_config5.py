@@ -78,7 +78,7 @@ def test_config5_shards_device_merge_equals_oracle(world):
         recs, strs, counts, scounts = ctx.export_services_device(world, dev)
         shard.map_wire_first(recs, lambda f: gi[f])  # first arrival: shard order -> trace position
         if recs.numel():
-            owner = (recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64) % np.uint64(world))
+            owner = shard.owner_np(recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64), world)
             assert np.all(np.diff(owner.astype(np.int64)) >= 0)
         ro = np.concatenate([[0], np.cumsum(counts.astype(np.int64))]) * ebd.WIRE_DTYPE.itemsize
         so = np.concatenate([[0], np.cumsum(scounts.astype(np.int64))])

@@ -258,6 +258,7 @@ def test_config5_network_maps_merge_across_shards(world):
         m.merge_services_device(torch.cat([r for r, _, _ in parts]),
                                 torch.cat([s for _, s, _ in parts] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8,
                                                                                   device=dev)]))
+        assert m.stats()["errors"] == 0, ("services", m.stats())
         m.merge_networks_device(torch.cat([n for _, _, n in parts]))
         assert m.stats()["errors"] == 0, m.stats()
         got_svc += m.services(with_nets=True)

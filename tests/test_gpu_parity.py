@@ -250,7 +250,7 @@ def test_device_export_by_owner_and_merge_equals_whole_trace():
             gpos = torch.tensor(idx.astype(np.int64), device=dev)
             shard.map_wire_first(recs, lambda f: gpos[f])  # first arrival: shard order -> trace position
             if recs.numel():
-                owner = (recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64) % np.uint64(W))
+                owner = shard.owner_np(recs.view(torch.int64).view(-1, 5)[:, 0].cpu().numpy().view(np.uint64), W)
                 assert np.all(np.diff(owner.astype(np.int64)) >= 0)  # grouped by owner
             for w, seg in enumerate(_owner_segments(recs, strs, counts, scounts)):
                 segs[w].append(seg)

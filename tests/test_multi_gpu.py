@@ -58,7 +58,7 @@ def _worker(rank, world, port, kind, out_path):
             assert np.array_equal(gidx, idx) and np.array_equal(sev, ev[idx])
         table = _shard_table(ev, lens, offs, payload, idx)
         mine = shard.exchange_merge(table, device="cpu")
-        owner = (mine.rec["key_lo"] % np.uint64(world)).astype(np.int64)
+        owner = shard.owner_np(mine.rec["key_lo"], world)
         assert np.all(owner == rank)  # every merged service is on its owner
         rows = shard.gather_rows(mine)
         if rank == 0:
@@ -200,10 +200,10 @@ def _net_worker(rank, world, port, out_path):
         t = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
         grouped, counts = shard.group_by_owner(t, shard.NET_REC_BYTES, world)
         got = shard.exchange_fixed(grouped, counts, shard.NET_REC_BYTES).numpy().view(ebd.SERVICE_NET_DTYPE)
-        owners = (got["key_lo"] % np.uint64(world)).astype(int).tolist()
+        owners = shard.owner_np(got["key_lo"], world).tolist()
         with open(out_path % rank, "w") as f:
             json.dump({"n": int(recs.size), "counts": counts.tolist(), "owners": owners,
-                       "sent_own": int(np.sum(recs["key_lo"] % np.uint64(world) == np.uint64(rank))),
+                       "sent_own": int(np.sum(shard.owner_np(recs["key_lo"], world) == rank)),
                        "got": sorted([int(x) for x in got["key_lo"]])}, f)
     finally:
         dist.destroy_process_group()
@@ -220,3 +220,13 @@ def test_network_records_reach_their_owner(tmp_path):
         assert sum(r[k]["counts"]) == r[k]["n"]
     assert len(r[0]["got"]) + len(r[1]["got"]) == r[0]["n"] + r[1]["n"]
     assert r[0]["counts"][0] == r[0]["sent_own"] and r[1]["counts"][1] == r[1]["sent_own"]
+
+
+def test_owner_rule_uses_every_rank():
+    """Service keys are odd (their low bit marks a used slot), so the owner comes from the
+    high word: every rank of 2, 4 and 8 owns about its share of the services."""
+    keys = np.array([ebd.host_endpoint_key(1000 + k % 7, b"h%d/p%d" % (k, k * 31))[0] for k in range(4000)], np.uint64)
+    assert np.all(keys & np.uint64(1) == 1)
+    for world in (2, 4, 8):
+        counts = np.bincount(shard.owner_np(keys, world), minlength=world)
+        assert counts.size == world and counts.min() > 0.8 * len(keys) / world, (world, counts)
