@@ -32,11 +32,8 @@ struct SSlot {
 	unsigned int first_c;  // ~(first event of the batch whose fresh parse was UNFINISHED), 0 = none (atomicMax)
 	unsigned int carry;    // 1 + index into the carried-session array, 0 = none
 	unsigned int visited;
-	unsigned int last_ev;  // (unused: k_lru_delta finds a session's last event in the sorted order)
-	unsigned int pad;
-	unsigned long long pad2;
 };
-static_assert(sizeof(SSlot) == 48, "session slot is 48 bytes");
+static_assert(sizeof(SSlot) == 32, "session slot is 32 bytes (a probe never straddles two lines)");
 
 constexpr uint32_t kCarryBytes = 8200; // > DISCOVERY_MAX_HTTP_REQUEST_LENGTH + 1
 

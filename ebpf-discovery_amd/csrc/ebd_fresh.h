@@ -241,13 +241,15 @@ EBD_HD void fresh_finalize(const Tab& T, const DfaInfo& di, const ScanRec& sr, u
 // the last header-key state it left (DfaTable::attr bits 0-2) and applies P:309-316 itself:
 // the first client-IP value sets clientIPKey when none is set (it stays set across reset,
 // P:374-379), and only the first header whose key equals it is the client address.
-// A step is branch-free (lanes of a wave walk different sessions): one table read, one
-// attribute read, and selects on the attribute bits that changed.  Terminal states step to
+// The walk goes 16 bytes at a time (dfa_walk_block): the state chain first (one table read
+// and one attribute read per byte), then the bookkeeping only at the bytes whose state
+// attribute differs from the previous state's (a few per request: URL, Host and client-IP
+// value edges, header keys), since no field changes anywhere else.  Terminal states step to
 // themselves, so bytes after the end change nothing but the position.
 // Spans are request-stream positions, as gp_step's.
 // ---------------------------------------------------------------------------------
 struct DfaWalk {
-	uint32_t s, a, kid, pos, f, cipkey, mcand, tpos;
+	uint32_t s, a, kid, pos, f, cipkey, mcand, tpos, lcp;
 	uint32_t url_start, url_end, host_start, host_end, cip_start, cip_end;
 };
 
@@ -260,6 +262,7 @@ EBD_HD void dfa_walk_load(const GenParser& g, uint32_t attr_s, DfaWalk& w) {
 	w.cipkey = g.cipkey;
 	w.mcand = g.mcand;
 	w.tpos = kNone;
+	w.lcp = kNone;
 	w.url_start = g.url_start;
 	w.url_end = g.url_start + g.url_len;
 	w.host_start = g.host_start;
@@ -268,15 +271,13 @@ EBD_HD void dfa_walk_load(const GenParser& g, uint32_t attr_s, DfaWalk& w) {
 	w.cip_end = g.cip_start + g.cip_len;
 }
 
-// One byte b if `valid` (otherwise nothing changes); w.tpos = the bytes of the request up
-// to and including the byte that made the state terminal.
-template <typename Tab, typename At>
-EBD_HD void dfa_walk_step(const Tab& T, const At& A, DfaWalk& w, uint32_t b, bool valid) {
-	const uint32_t ns = valid ? (uint32_t)T[(w.s << 8) | b] : w.s;
-	const uint32_t an = A[ns], ao = w.a, x = an ^ ao, en = an & x, lv = ao & x;
-	const uint32_t ko = ao & 7u, pos = w.pos;
+// The byte at request position pos moved the walk from a state with attribute ao to one with
+// attribute an != ao.  gp_step's per-byte rules reduced to such bytes: the client id of the
+// last header-key state (kid) is that of the state before the byte, which has not changed
+// since the previous such byte (dfa_walk_store applies the final state's at the end).
+EBD_HD void dfa_walk_change(DfaWalk& w, uint32_t ao, uint32_t an, uint32_t pos) {
+	const uint32_t x = an ^ ao, en = an & x, lv = ao & x, ko = ao & 7u;
 	w.kid = ko != kKcKeep ? ko : w.kid;
-	w.mcand = pos == 0 && valid ? b : w.mcand;
 	w.url_start = (en & A_URL) ? pos : w.url_start; // P:190-199: the URL starts with its '/'
 	w.url_end = (lv & A_URL) ? pos : w.url_end;     // P:201-213: it ends before the space
 	w.host_start = (en & A_HVH) ? pos : w.host_start; // P:309-310: the first Host value byte
@@ -292,10 +293,51 @@ EBD_HD void dfa_walk_step(const Tab& T, const At& A, DfaWalk& w, uint32_t b, boo
 	const bool cl = (lv & A_HVC) && (w.f & GPF_IN_CIP); // the value's CR (P:248-257 parses it)
 	w.cip_end = cl ? pos : w.cip_end;
 	w.f = cl ? ((w.f & ~(uint32_t)GPF_IN_CIP) | GPF_CIP_FOUND) : w.f;
-	w.tpos = valid && (an & A_TERM) && w.tpos == kNone ? pos + 1 : w.tpos; // (a parse() on an ended parser takes one byte)
-	w.s = ns;
-	w.a = an;
-	w.pos = pos + (valid ? 1u : 0u);
+	w.tpos = (en & A_TERM) && w.tpos == kNone ? pos + 1 : w.tpos;
+	w.lcp = pos;
+}
+
+// Byte k (0..15) of a 16-byte block held as four words.
+EBD_HD uint32_t blk_byte(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3, uint32_t k) {
+	const uint32_t lo = (k & 4u) ? v1 : v0, hi = (k & 4u) ? v3 : v2; // selects (an indexed array went to scratch)
+	return (((k & 8u) ? hi : lo) >> (8u * (k & 3u))) & 0xffu;
+}
+
+// One 16-byte block of a parse: byte k (of the words wd) is valid when base + k < ne (base:
+// the buffer offset of byte 0, wrapping below 0 for a buffer that starts inside the block)
+// and lies at request position pbase + k; valid bytes are consecutive.  w.tpos = the bytes of
+// the request up to and including the byte that made the state terminal (a parse() on an
+// ended parser takes one byte).
+template <typename Tab, typename At>
+EBD_HD void dfa_walk_block(const Tab& T, const At& A, DfaWalk& w, const uint32_t (&wd)[4], uint32_t base, uint32_t pbase, uint32_t ne) {
+	const uint32_t a0 = w.a;
+	uint32_t s = w.s, a = a0, chg = 0, nv = 0;
+	uint32_t P[4] = {0u, 0u, 0u, 0u}; // the attribute after each byte
+#pragma unroll
+	for (int k = 0; k < 16; k++) {
+		const uint32_t b = (wd[k >> 2] >> (8 * (k & 3))) & 0xffu;
+		const bool v = base + (uint32_t)k < ne;
+		const uint32_t ns = v ? (uint32_t)T[(s << 8) | b] : s;
+		const uint32_t an = A[ns];
+		chg |= an != a ? 1u << k : 0u;
+		P[k >> 2] |= an << (8 * (k & 3));
+		nv += v ? 1u : 0u;
+		s = ns;
+		a = an;
+	}
+	if (nv) {
+		if (w.pos == 0) // P:162: handleCharMethod: the request's first byte is the method candidate
+			w.mcand = blk_byte(wd[0], wd[1], wd[2], wd[3], 0u - pbase);
+		if ((a0 & A_TERM) && w.tpos == kNone)
+			w.tpos = w.pos + 1;
+	}
+	for (uint32_t m = chg; m; m &= m - 1u) {
+		const uint32_t k = (uint32_t)__builtin_ctz(m);
+		dfa_walk_change(w, k ? blk_byte(P[0], P[1], P[2], P[3], k - 1u) : a0, blk_byte(P[0], P[1], P[2], P[3], k), pbase + k);
+	}
+	w.s = s;
+	w.a = a;
+	w.pos += nv;
 }
 
 // The end of a parse() call that walked `ne` of the buffer's `n` bytes (ne < n: the request
@@ -305,6 +347,10 @@ EBD_HD uint32_t dfa_walk_store(const DfaInfo& di, DfaWalk& w, uint32_t pos0, uin
 		GenParser& g) {
 	uint32_t consumed = ne, f = w.f;
 	bool done = false;
+	if (w.pos != pos0 && w.lcp != w.pos - 1u) { // the bytes after the last change: kid of the final state
+		const uint32_t ko = w.a & 7u;
+		w.kid = ko != kKcKeep ? ko : w.kid;
+	}
 	if (w.tpos != kNone) {
 		consumed = w.tpos - pos0;
 		done = true;
@@ -338,15 +384,19 @@ EBD_HD uint32_t dfa_allow(uint32_t pos, uint32_t n) {
 	return n < allow ? n : allow;
 }
 
-// P:85-106 parse() of one buffer with the DFA: returns the bytes consumed (the host twin
-// of the device walker, which reads the buffer 16 bytes at a time).
+// P:85-106 parse() of one buffer with the DFA, 16 bytes at a time: returns the bytes consumed
+// (the host twin of the device walker).
 template <typename Tab, typename At, typename ByteAt>
 EBD_HD uint32_t dfa_parse(GenParser& g, const Tab& T, const At& A, const DfaInfo& di, ByteAt at, uint32_t n, uint8_t flags) {
 	DfaWalk w;
 	dfa_walk_load(g, A[g.ds], w);
 	const uint32_t pos0 = w.pos, ne = dfa_allow(pos0, n);
-	for (uint32_t i = 0; i < ne && w.tpos == kNone; i++)
-		dfa_walk_step(T, A, w, at(i), true);
+	for (uint32_t base = 0; base < ne && w.tpos == kNone; base += 16) {
+		uint32_t wd[4] = {0u, 0u, 0u, 0u};
+		for (uint32_t k = 0; k < 16 && base + k < ne; k++)
+			wd[k >> 2] |= (at(base + k) & 0xffu) << (8 * (k & 3));
+		dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
+	}
 	return dfa_walk_store(di, w, pos0, ne, n, flags, g);
 }
 

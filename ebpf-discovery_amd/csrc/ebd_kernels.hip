@@ -1182,6 +1182,9 @@ constexpr int kWalkThreads = 256;
 #define EBD_WALK_REFILL 48
 #endif
 constexpr int kWalkRefill = EBD_WALK_REFILL; // lanes of a wave waiting before it ends and starts events
+#ifndef EBD_WALK_BLOCKS
+#define EBD_WALK_BLOCKS 3 // k_walk blocks per CU
+#endif
 
 struct Walk {
 	const uint8_t* cb; // carried bytes of the request in progress
@@ -1230,8 +1233,8 @@ struct ByteTab {
 };
 
 // dfa_parse (ebd_fresh.h) over one buffer on the device: 16-byte aligned blocks, the next
-// one loaded while the current one is walked, 16 predicated branch-free steps per block (a
-// byte is valid when its buffer offset is below the bytes the request may take).  The
+// one loaded while the current one is walked, dfa_walk_block per block (a byte is valid
+// when its buffer offset is below the bytes the request may take).  The
 // aligned block holding a valid byte never leaves that byte's page, so the over-read cannot
 // fault.  The walk stops after the block in which the state became terminal.
 __device__ uint32_t dfa_parse_dev(GenParser& g, const SessTabs& tb, const DfaInfo& di, const uint8_t* p, uint32_t n, uint8_t flags) {
@@ -1248,9 +1251,7 @@ __device__ uint32_t dfa_parse_dev(GenParser& g, const SessTabs& tb, const DfaInf
 			const uint4 nx = bi + 1 < nb ? *(const uint4*)(b0 + 16u * (bi + 1)) : cur;
 			const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
 			const uint32_t base = 16u * bi - k0; // buffer offset of the block's byte 0 (wraps below 0)
-#pragma unroll
-			for (int k = 0; k < 16; k++)
-				dfa_walk_step(T, A, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu, base + (uint32_t)k < ne);
+			dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
 			cur = nx;
 		}
 	}
@@ -1292,10 +1293,18 @@ __device__ uint32_t stream_visit(const Dev& d, const Walk& w, uint32_t jend, uin
 	return done;
 }
 
-// Copies stream bytes [a, a + n) to dst: 8-byte loads and stores inside each piece, byte
-// stores for a piece's last < 8 bytes (the next request's bytes follow dst's in the arena).
-__device__ void stream_copy(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, uint32_t a, uint32_t n, uint8_t* dst) {
-	const uint32_t b = a + n;
+// Copies the stream bytes of three spans, [a[k], a[k] + n[k]) to dst[k], in one pass over the
+// request's pieces (each piece's event is looked up once, not once per span): 8-byte loads
+// and stores inside each piece, byte stores for a piece's last < 8 bytes (the next span's or
+// request's bytes follow dst[k]'s in the arena).
+__device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_t cend, const uint32_t (&a)[3], const uint32_t (&n)[3],
+		uint8_t* const (&dst)[3]) {
+	uint32_t b = 0;
+#pragma unroll
+	for (int k = 0; k < 3; k++)
+		b = n[k] && a[k] + n[k] > b ? a[k] + n[k] : b;
+	if (b == 0)
+		return;
 	auto copy = [](const uint8_t* src, uint8_t* out, uint32_t len) {
 		uint32_t k = 0;
 		for (; k + 8 <= len; k += 8)
@@ -1303,23 +1312,29 @@ __device__ void stream_copy(const Dev& d, const Walk& w, uint32_t jend, uint32_t
 		for (; k < len; k++)
 			out[k] = src[k];
 	};
+	// the spans' parts inside piece [pos, pos + pl), whose bytes start at src
+	auto piece = [&](const uint8_t* src, uint32_t pos, uint32_t pl) {
+#pragma unroll
+		for (int k = 0; k < 3; k++) {
+			const uint32_t lo = a[k] > pos ? a[k] : pos, hi = a[k] + n[k] < pos + pl ? a[k] + n[k] : pos + pl;
+			if (lo < hi)
+				copy(src + (lo - pos), dst[k] + (lo - a[k]), hi - lo);
+		}
+	};
 	uint32_t pos = 0;
-	if (n == 0)
-		return;
 	if (w.clen) {
-		if (a < w.clen)
-			copy(w.cb + a, dst, min(b, w.clen) - a);
+		piece(w.cb, 0, w.clen);
 		pos = w.clen;
 	}
 	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
-		uint32_t pl = piece_len(d, j);
+		const uint32_t i = slow_event(d, j);
+		const uint32_t L = d.len[i];
+		uint32_t pl = ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) ? L : 0; // piece_len
 		if (j == jend)
 			pl = cend;
 		if (pl == 0)
 			continue;
-		const uint32_t lo = a > pos ? a : pos, hi = b < pos + pl ? b : pos + pl;
-		if (lo < hi)
-			copy(d.payload + d.off[slow_event(d, j)] + (lo - pos), dst + (lo - a), hi - lo);
+		piece(d.payload + d.off[i], pos, pl);
 		pos += pl;
 	}
 }
@@ -1389,9 +1404,9 @@ __global__ void k_emit(Dev d) {
 			continue;
 		}
 		uint8_t* dst = d.sstr + at;
-		stream_copy(d, w, e.jend, cend, e.host_start, hl, dst);
-		stream_copy(d, w, e.jend, cend, e.url_start, ul, dst + hl);
-		stream_copy(d, w, e.jend, cend, e.cip_start, cl, dst + hl + ul);
+		const uint32_t sa[3] = {e.host_start, e.url_start, e.cip_start}, sn[3] = {hl, ul, cl};
+		uint8_t* const sd[3] = {dst, dst + hl, dst + hl + ul};
+		stream_copy3(d, w, e.jend, cend, sa, sn, sd);
 		unsigned long long net = 0;
 		uint8_t cls;
 		uint32_t tb = 0, te = 0;
@@ -1674,13 +1689,11 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 			}
 		}
 		if (in_ev) {
-			if (bi < nb) { // one block: 16 predicated steps (dfa_parse_dev's)
+			if (bi < nb) { // one block (dfa_parse_dev's)
 				const uint4 nx = bi + 1 < nb ? *(const uint4*)(b0 + 16u * (bi + 1)) : cur;
 				const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
 				const uint32_t base = 16u * bi - k0;
-#pragma unroll
-				for (int k = 0; k < 16; k++)
-					dfa_walk_step(T, A, w, (wd[k >> 2] >> (8 * (k & 3))) & 0xffu, base + (uint32_t)k < ne);
+				dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
 				cur = nx;
 				bi++;
 			}
@@ -2313,9 +2326,6 @@ __global__ void k_sset_clear(Dev d) {
 		s->first_c = 0;
 		s->carry = 0;
 		s->visited = 0;
-		s->last_ev = 0;
-		s->pad = 0;
-		s->pad2 = 0;
 	}
 }
 
@@ -2806,7 +2816,7 @@ hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
 }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
-	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * 3)), dim3(kWalkThreads), 0, st, d);
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d);
 
 	return hipGetLastError();
 }

@@ -392,6 +392,7 @@ class Context:
         n = C.c_uint32()
         _check(lib().ebd_collect_networks_device(self.h, None, 0, C.byref(n)), "ebd_collect_networks_device")
         out = torch.empty(max(n.value, 1) * SERVICE_NET_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self._fence(out)
         _check(lib().ebd_collect_networks_device(self.h, C.c_void_p(out.data_ptr()), max(n.value, 1), C.byref(n)),
                "ebd_collect_networks_device")
         return out[:n.value * SERVICE_NET_DTYPE.itemsize]
@@ -451,6 +452,7 @@ class Context:
         n, sb = int(counts.sum()), int(scounts.sum())
         recs = torch.empty(max(n, 1) * WIRE_DTYPE.itemsize, dtype=torch.uint8, device=device)
         strs = torch.empty(max(sb, 8), dtype=torch.uint8, device=device)
+        self._fence(recs, strs)  # torch may hand back memory its stream still uses
         _check(lib().ebd_export_services_device(self.h, world, C.c_void_p(recs.data_ptr()), max(n, 1),
                                                 C.c_void_p(strs.data_ptr()), strs.numel(), _p(counts), _p(scounts)),
                "ebd_export_services_device")
