@@ -1179,7 +1179,7 @@ __global__ void k_slow_collect(Dev d) {
 // ---------------------------------------------------------------------------------
 constexpr int kWalkThreads = 256;
 #ifndef EBD_WALK_REFILL
-#define EBD_WALK_REFILL 48
+#define EBD_WALK_REFILL 60
 #endif
 constexpr int kWalkRefill = EBD_WALK_REFILL; // lanes of a wave waiting before it ends and starts events
 #ifndef EBD_WALK_BLOCKS
@@ -1376,7 +1376,9 @@ __device__ void defer_emit(const Dev& d, const Walk& w, uint32_t jend, const Gen
 
 // handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
 // (Discovery.cpp:161-192, 210-212) for the session path's request q.
-__global__ void k_emit(Dev d) {
+__global__ __launch_bounds__(256) void k_emit(Dev d) {
+	__shared__ __attribute__((aligned(8))) uint8_t rows[256 * kCipStride];
+	uint8_t* row = rows + threadIdx.x * kCipStride; // this lane's client-IP value, parsed from LDS
 	const uint32_t nq = (uint32_t)d.ctr[CTR_SREQ];
 	for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
 		const EmitRec e = *(const EmitRec*)(d.sreq + q);
@@ -1411,12 +1413,22 @@ __global__ void k_emit(Dev d) {
 		uint8_t cls;
 		uint32_t tb = 0, te = 0;
 		if (e.f & GPF_CIP_FOUND) {
+			// the value (just copied to the arena) goes to the lane's LDS row with 8-byte loads
+			// (the arena has 64 bytes of slack), so the byte-serial parse below reads LDS
+			const uint8_t* cv = dst + hl + ul;
+			if (cl <= (uint32_t)kCipRaw) {
+#pragma unroll
+				for (uint32_t h = 0; h < (uint32_t)kCipRaw / 8; h++)
+					if (8 * h < cl)
+						*(unsigned long long*)(row + 8 * h) = gload8u(cv + 8 * h);
+				cv = row;
+			}
 			uint32_t raw = 0; // the value up to its first ',' is the front token's source
-			while (raw < cl && dst[hl + ul + raw] != ',')
+			while (raw < cl && cv[raw] != ',')
 				raw++;
-			front_token(dst + hl + ul, raw, &tb, &te);
+			front_token(cv, raw, &tb, &te);
 			info |= EBD_INFO_CIP;
-			cls = classify_token(*d.ifs, dst + hl + ul + tb, te - tb, &net);
+			cls = classify_token(*d.ifs, cv + tb, te - tb, &net);
 		} else {
 			cls = classify_source(*d.ifs, ev.flags, ev.sourceIP, &net);
 		}
@@ -1606,7 +1618,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	const uint32_t stride = gridDim.x * kWalkThreads;
 	// A lane walks its sessions one 16-byte block per iteration.  A lane whose event ended
-	// waits until half of the wave has (or none is still parsing); then the wave ends those
+	// waits until 60 of the 64 lanes have (or none is still parsing); then the wave ends those
 	// events and starts the next ones together: one buffer per lane and step made each wave
 	// step as long as its longest buffer, while ending and starting events one lane at a time
 	// ran the long end-of-event path (outcome, emission, next event's loads) for a few lanes
