@@ -1762,18 +1762,23 @@ __global__ void k_carry_pass(Dev d) {
 // least recently used session (which then parses its next buffer as a new session,
 // Discovery.cpp:141), close and INVALID erase.
 // ---------------------------------------------------------------------------------
+// Everything but the close flag comes from the sort key: a session's group is its carry index
+// (carried) or carry_cap + its first UNFINISHED event (k_slow_collect), and its last event of
+// the batch is the last of its group.  Only a session's entry and close events write (delta
+// and minus are zeroed before), and only a session's last event reads its event record.
 __global__ void k_lru_delta(Dev d, uint32_t nslow, int* delta, uint8_t* minus) {
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
-		const uint32_t i = slow_event(d, j);
-		const SSlot& ss = d.sset[d.ev_slot[i]];
-		const bool carried = ss.carry != 0;
-		const uint32_t first = ss.first_c ? ~ss.first_c : kNone;
+		const unsigned long long key = d.slow_keys[j];
+		const uint32_t grp = (uint32_t)(key >> 32), i = (uint32_t)key;
+		const bool carried = grp < d.carry_cap;
+		const uint32_t first = carried ? kNone : grp - d.carry_cap;
 		const bool plus = !carried && first == i;
-		// the session's last event of the batch: the last of its group in the sorted order
-		const bool last = j + 1 == nslow || (uint32_t)(d.slow_keys[j + 1] >> 32) != (uint32_t)(d.slow_keys[j] >> 32);
-		const bool close = (d.ev[i].flags & FLAG_END) && last && (carried || (first != kNone && first <= i));
-		delta[i] = (plus ? 1 : 0) - (close ? 1 : 0);
-		minus[i] = close ? 1 : 0;
+		const bool last = j + 1 == nslow || (uint32_t)(d.slow_keys[j + 1] >> 32) != grp;
+		const bool close = last && (carried || first <= i) && (d.ev[i].flags & FLAG_END);
+		if (plus != close)
+			delta[i] = plus ? 1 : -1;
+		if (close)
+			minus[i] = 1;
 	}
 }
 
