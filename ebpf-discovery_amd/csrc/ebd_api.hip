@@ -184,6 +184,7 @@ struct ebd_ctx {
 		uint64_t* off = nullptr;
 		uint8_t* payload = nullptr;
 		uint64_t pay_cap = 0;
+		uint64_t pay_bytes = 0; // the staged batch's payload_bytes
 		uint32_t n = 0;
 		uint64_t ticket = 0;
 		int staged = 0, used_valid = 0;
@@ -588,7 +589,7 @@ static int finish_pending(ebd_ctx* c) {
 // work returns with its kernels still queued, and a batch with some returns once the session
 // path is queued (its carried-session count is read by the next call, finish_pending).
 static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const uint64_t* off, const uint8_t* payload,
-		uint32_t n) {
+		uint64_t payload_bytes, uint32_t n) {
 	if (n > c->max_events)
 		return -EINVAL;
 	HIP_TRY(hipSetDevice(c->device));
@@ -603,6 +604,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	d.len = len;
 	d.off = off;
 	d.payload = payload;
+	d.payload_bytes = payload_bytes;
 	d.n = n;
 	d.now = ctx_now(c);
 	d.times = (const unsigned long long*)c->ev_times; // for this batch only
@@ -706,7 +708,7 @@ int ebd_submit_batch_device(ebd_ctx* c, const ebd_device_batch* b) {
 	if (!c || !b || (b->n && (!b->events || !b->len || !b->off || !b->payload)))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
-	return run_batch(c, (const EventRec*)b->events, b->len, b->off, b->payload, b->n);
+	return run_batch(c, (const EventRec*)b->events, b->len, b->off, b->payload, b->payload_bytes, b->n);
 }
 
 int ebd_set_seq_base(ebd_ctx* c, uint64_t seq) {
@@ -872,6 +874,7 @@ static int stage_locked(ebd_ctx* c, const ebd_discovery_event* events, const uin
 	HIP_TRY(hipEventRecord(g.up, c->cstream));
 	c->next_slot = s ^ 1; // only once the slot is staged
 	g.n = n;
+	g.pay_bytes = payload_bytes;
 	g.staged = 1;
 	g.ticket = c->next_ticket++;
 	*ticket = g.ticket;
@@ -893,7 +896,7 @@ static int submit_staged_locked(ebd_ctx* c, uint64_t ticket) {
 				(void*)g.payload, (unsigned long long)g.pay_cap, (void*)g.ev, (void*)g.len, (void*)g.off, (void*)c->d_res,
 				(void*)c->d_keys, (void*)c->d_sset, (void*)c->d_carry[0], (void*)c->d_carry[1]);
 	g.staged = 0;
-	const int rc = run_batch(c, g.ev, g.len, g.off, g.payload, g.n);
+	const int rc = run_batch(c, g.ev, g.len, g.off, g.payload, g.pay_bytes, g.n);
 	HIP_TRY(hipEventRecord(g.used, c->stream));
 	g.used_valid = 1;
 	return rc;

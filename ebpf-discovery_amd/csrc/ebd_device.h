@@ -137,6 +137,7 @@ struct Dev {
 	const uint32_t* len;
 	const uint64_t* off;
 	const uint8_t* payload;
+	unsigned long long payload_bytes; // buffers lie in [payload, payload + payload_bytes)
 	uint32_t n;
 	unsigned long long seq_base;
 	// per-event outputs

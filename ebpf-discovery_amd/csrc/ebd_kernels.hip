@@ -22,6 +22,13 @@ namespace ebd {
 
 __device__ __forceinline__ void set_error(const Dev& d, unsigned long long bit) { atomicOr(&d.ctr[CTR_ERRORS], bit); }
 
+// A saved buffer the kernels may read: at most EBD_BUFFER_MAX_DATA_SIZE long and inside the
+// batch's payload.  An event whose buffer is not is handled as one whose buffer is missing
+// (Discovery.cpp:103-107); k_fresh reports it as EBD_ERR_BAD_INPUT.
+__device__ __forceinline__ bool buf_in(const Dev& d, uint32_t L, unsigned long long off) {
+	return L <= EBD_BUFFER_MAX_DATA_SIZE && off <= d.payload_bytes && L <= d.payload_bytes - off;
+}
+
 // A global counter bumped by the active lanes of a wave together: one atomic for the wave
 // instead of one per lane (a hot counter serialises its atomics at the memory side; the
 // session path bumps several per event).  Returns this lane's offset: the counter's value
@@ -243,7 +250,10 @@ __device__ void net_touch(const Dev& d, uint32_t slot, uint32_t kind, uint32_t v
 // incrementServiceClientsNumber's network part for an external client (net: net_pack).
 // Aggregator::getCurrentTime of the request finished by event i: the event's own reading when
 // the batch carries them (ebd_set_event_clock), else the batch's.
-__device__ __forceinline__ unsigned long long request_time(const Dev& d, uint32_t i) { return d.times ? d.times[i] : d.now; }
+// A map entry's time 0 means "erased", so a reading of 0 counts as 1 (the batch clock is >= 1 too).
+__device__ __forceinline__ unsigned long long request_time(const Dev& d, uint32_t i) {
+	return d.times ? max(d.times[i], 1ull) : d.now;
+}
 
 __device__ void agg_nets(const Dev& d, uint32_t slot, unsigned long long net, unsigned long long now) {
 	if (slot == kNone)
@@ -561,7 +571,7 @@ __device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end
 	e.flags = flags;
 	const uint32_t L = d.len[i];
 	const uint64_t off = d.off[i];
-	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : (L > EBD_BUFFER_MAX_DATA_SIZE || off >> 40) ? EK_BAD : EK_PARSE;
+	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : !buf_in(d, L, off) ? EK_BAD : EK_PARSE;
 	e.L = e.kind == EK_PARSE ? L : 0;
 	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
 	return e;
@@ -1130,7 +1140,7 @@ __device__ __forceinline__ uint32_t cip_classify(const Dev& d, uint32_t i, ebd_e
 // land in a table of a few times the live sessions instead of one sized for every event.
 __global__ void k_sset_size(Dev d, uint32_t cap) {
 	const unsigned long long want = 2ull * (d.ctr[CTR_UNFINISHED] + d.n_carry_in);
-	uint32_t m = 1024;
+	uint32_t m = cap < 1024u ? cap : 1024u; // never past the allocation (cap: a power of two)
 	while (m < want && m < cap)
 		m <<= 1;
 	*d.sset_mask = m - 1u;
@@ -1197,7 +1207,7 @@ __device__ __forceinline__ uint32_t slow_event(const Dev& d, uint32_t j) { retur
 __device__ __forceinline__ uint32_t piece_len(const Dev& d, uint32_t j) {
 	const uint32_t i = slow_event(d, j);
 	const uint32_t L = d.len[i];
-	return ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) ? L : 0;
+	return ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && buf_in(d, L, d.off[i])) ? L : 0;
 }
 
 // Sequential byte reads through a 16-B register window: one aligned dwordx4 load per 16
@@ -1329,7 +1339,7 @@ __device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_
 	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
 		const uint32_t i = slow_event(d, j);
 		const uint32_t L = d.len[i];
-		uint32_t pl = ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && L <= EBD_BUFFER_MAX_DATA_SIZE) ? L : 0; // piece_len
+		uint32_t pl = ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && buf_in(d, L, d.off[i])) ? L : 0; // piece_len
 		if (j == jend)
 			pl = cend;
 		if (pl == 0)
@@ -1398,11 +1408,15 @@ __global__ __launch_bounds__(256) void k_emit(Dev d) {
 		sr.pad = 0;
 		sr.pad2 = 0;
 		if (at + total > d.sstr_cap) {
+			// no room for its strings: the request is not aggregated, is marked so, and is not
+			// counted (k_sess_tally adds CTR_SREQ to CTR_REQUESTS)
 			set_error(d, EBD_ERR_ARENA_FULL);
+			atomicAdd(&d.ctr[CTR_REQUESTS], ~0ull);
 			sr.str_off = 0;
 			sr.host_len = sr.url_len = sr.cip_off = sr.cip_len = 0;
-			sr.info = info;
+			sr.info = (uint8_t)(info | EBD_INFO_DROPPED);
 			d.sreq[q] = sr;
+			d.res[i].info = sr.info;
 			continue;
 		}
 		uint8_t* dst = d.sstr + at;
@@ -1479,12 +1493,13 @@ struct EvCtx {
 
 // handleNewEvent up to parse(): whether the event's buffer is parsed, and with which parser
 // (the saved session's, or a fresh one for a session not in the LRU).
-__device__ __forceinline__ bool ev_begin(const Dev& d, SessState& S, uint32_t jj, uint32_t i, uint32_t flags, uint32_t L, EvCtx& e) {
+__device__ __forceinline__ bool ev_begin(const Dev& d, SessState& S, uint32_t jj, uint32_t i, uint32_t flags, uint32_t L,
+		unsigned long long off, EvCtx& e) {
 	e.i = i;
 	e.jj = jj;
 	e.L = L;
 	e.flags = flags;
-	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || L > EBD_BUFFER_MAX_DATA_SIZE)
+	if (!(flags & FLAG_NEW) || L == EBD_NO_BUFFER || !buf_in(d, L, off))
 		return false;
 	e.flags |= EV_PARSE;
 	if (S.live) { // handleExistingSession, Discovery.cpp:123-139 (find touched it)
@@ -1553,7 +1568,7 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 	const uint32_t i = slow_event(d, jj);
 	EvCtx e;
 	uint32_t c = 0;
-	if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], e))
+	if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], d.off[i], e))
 		c = dfa_parse_dev(S.g, tb, d.di, d.payload + d.off[i], e.L, (uint8_t)e.flags);
 	return ev_end(d, S, e, c);
 }
@@ -1676,7 +1691,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 							pf_off = d.off[pf_i];
 						}
 					}
-					if (ev_begin(d, S, jj, i, fl, L, e)) {
+					if (ev_begin(d, S, jj, i, fl, L, off, e)) {
 						dfa_walk_load(S.g, A[S.g.ds], w);
 						pos0 = w.pos;
 						ne = dfa_allow(pos0, e.L);
@@ -1896,7 +1911,7 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 				sink ^= sp[0] ^ sp[sizeof(SessState) / 4 - 1];
 				const uint32_t L = d.len[i];
 				const unsigned long long po = d.off[i];
-				if ((d.ev[i].flags & FLAG_NEW) && L != 0 && L <= EBD_BUFFER_MAX_DATA_SIZE) {
+				if ((d.ev[i].flags & FLAG_NEW) && L != 0 && buf_in(d, L, po)) {
 					const unsigned long long pe = po + min(L, 512u);
 					for (unsigned long long o = po & ~127ull; o < pe; o += 128)
 						sink ^= *(const volatile uint32_t*)(d.payload + o); // inside the buffer's page

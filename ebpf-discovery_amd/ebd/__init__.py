@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("EBD_LIB") or os.path.join(PKG_DIR, "libebd_amd.so")
 FLAG_IPV4, FLAG_IPV6, FLAG_UNENCRYPTED, FLAG_SSL, FLAG_NEW_DATA, FLAG_DATA_END = 2, 4, 8, 16, 32, 64
 NO_BUFFER = 0xFFFFFFFF
 STATUS_NONE, STATUS_UNFINISHED, STATUS_FINISHED, STATUS_INVALID = 0, 1, 2, 3
-INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING = 0x01, 0x02, 0x04, 0x08, 0x40
+INFO_POST, INFO_HTTPS, INFO_SESSION, INFO_CIP, INFO_EXISTING, INFO_DROPPED = 0x01, 0x02, 0x04, 0x08, 0x40, 0x80
 CLASS_NONE, CLASS_INTERNAL, CLASS_EXTERNAL = 0, 1, 2
 ERR_BITS = {1: "TABLE_FULL", 2: "ARENA_FULL", 4: "LRU_OVERFLOW", 8: "SESSION_FULL", 16: "VERIFY_FULL", 32: "BAD_INPUT",
             64: "COLLISION", 128: "INTERNAL", 256: "NET_FULL"}
@@ -64,7 +64,10 @@ class Config(C.Structure):
 
 class DeviceBatch(C.Structure):
     _fields_ = [("events", C.c_void_p), ("len", C.c_void_p), ("off", C.c_void_p), ("payload", C.c_void_p),
-                ("n", C.c_uint32)]
+                ("payload_bytes", C.c_uint64), ("n", C.c_uint32)]
+
+
+PAYLOAD_PAD = 16  # EBD_PAYLOAD_PAD
 
 
 class Stats(C.Structure):
@@ -303,11 +306,22 @@ class Context:
         if getattr(self, "_ext", None) is None:
             self._ext = torch.cuda.ExternalStream(lib().ebd_ctx_stream(self.h), device=ts[0].device)
         self._ext.wait_stream(torch.cuda.current_stream(ts[0].device))
+        # and torch's caching allocator may not hand their memory out again before the work
+        # queued on the context stream by now (which reads or writes them) is done
+        for t in ts:
+            t.record_stream(self._ext)
 
-    def submit_device(self, events, lens, offs, payload, n):
-        """Device-resident batch (torch tensors on the context's device or raw pointers)."""
+    def submit_device(self, events, lens, offs, payload, n, payload_bytes=None):
+        """Device-resident batch (torch tensors on the context's device or raw pointers).
+        payload_bytes: the bytes buffers may occupy; for a payload tensor it defaults to its
+        size less the EBD_PAYLOAD_PAD readable bytes the kernels need past the last buffer."""
+        if payload_bytes is None:
+            if not hasattr(payload, "numel"):
+                raise ValueError("submit_device: payload_bytes is required with a raw payload pointer")
+            payload_bytes = max(payload.numel() - PAYLOAD_PAD, 0)
         self._fence(events, lens, offs, payload)
-        b = DeviceBatch(events=_ptrval(events), len=_ptrval(lens), off=_ptrval(offs), payload=_ptrval(payload), n=n)
+        b = DeviceBatch(events=_ptrval(events), len=_ptrval(lens), off=_ptrval(offs), payload=_ptrval(payload),
+                        payload_bytes=payload_bytes, n=n)
         _check(lib().ebd_submit_batch_device(self.h, C.byref(b)), "ebd_submit_batch_device")
 
     def sync(self):
@@ -411,7 +425,8 @@ class Context:
 
     def set_event_clock(self, times):
         """ebd_set_event_clock: per-event getCurrentTime readings (a device int64/uint64 tensor
-        of the next batch's n events; kept referenced until the batch is done) or None."""
+        of the next batch's n events) or None.  The batch's kernels read it after submit
+        returns; _fence's record_stream keeps its memory from being reused before they ran."""
         self._ev_times = times
         if times is not None:
             self._fence(times)

@@ -87,6 +87,8 @@ enum {
 #define EBD_INFO_CIP 0x08      /* request.clientIp non-empty (cip_* spans the front token) */
 #define EBD_INFO_CLASS_SHIFT 4 /* bits 4-5: 0 not counted, 1 internal, 2 external */
 #define EBD_INFO_EXISTING 0x40 /* parsed by a saved session (Discovery.cpp:123-139) */
+#define EBD_INFO_DROPPED 0x80  /* FINISHED, but not aggregated or counted: a capacity error
+                                  (EBD_ERR_ARENA_FULL) left no room for its strings */
 
 /* 16 bytes.  consumed = HttpRequestParser::parse() return value for this buffer.
  * Fast-path (single-buffer) requests: spans are byte offsets inside this event's
@@ -214,15 +216,19 @@ typedef struct ebd_config {
 typedef struct ebd_ctx ebd_ctx;
 
 /* Device-resident batch: every pointer is a device (HBM) pointer that stays valid
- * until the next ebd_sync.  payload reads are done in aligned 16-byte blocks and 8-byte
- * pieces, so the allocation must be readable from the 16-byte boundary at or below each
- * buffer to EBD_PAYLOAD_PAD bytes past its end. */
+ * until the next ebd_sync.  Buffer i is [off[i], off[i] + len[i]) of payload and must lie
+ * inside [0, payload_bytes); a buffer that does not is not read: the event counts as one
+ * with no saved buffer and EBD_ERR_BAD_INPUT is set (the host entry points reject such a
+ * batch with -EINVAL instead, ebd_submit_batch).  payload reads are done in aligned 16-byte
+ * blocks and 8-byte pieces, so the allocation must be readable from the 16-byte boundary at
+ * or below payload to EBD_PAYLOAD_PAD bytes past payload + payload_bytes. */
 #define EBD_PAYLOAD_PAD 16u
 typedef struct ebd_device_batch {
 	const ebd_discovery_event* events;
 	const uint32_t* len;
 	const uint64_t* off;
 	const uint8_t* payload;
+	uint64_t payload_bytes;
 	uint32_t n;
 } ebd_device_batch;
 
