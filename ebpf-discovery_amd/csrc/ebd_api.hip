@@ -55,6 +55,7 @@ hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsig
 		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus);
 hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
 		const unsigned long long* offs, hipStream_t st, int cus);
+hipError_t launch_agg_requests(const Dev& d, const ebd_request* rq, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
 hipError_t launch_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt, hipStream_t st);
 hipError_t launch_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
 		const uint32_t* stt, unsigned long long* alen, hipStream_t st);
@@ -76,6 +77,7 @@ using namespace ebd;
 static_assert(sizeof(ebd_config) == 64, "ebd_config layout");
 static_assert(sizeof(ebd_stats) == 88, "ebd_stats layout");
 static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 80 && sizeof(ebd_service_net) == 32, "result layouts");
+static_assert(sizeof(ebd_request) == 40 && sizeof(ebd_device_batch) == 48, "request / batch layouts");
 
 #define HIP_TRY(x)                                                                                                   \
 	do {                                                                                                             \
@@ -1323,6 +1325,49 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 	HIP_TRY(launch_verify(d, c->stream, c->cus));
 	HIP_TRY(hipFreeAsync(tmp, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, const char* strings, uint64_t strings_len) {
+	if (!c || (n && (!reqs || (!strings && strings_len))))
+		return -EINVAL;
+	for (uint32_t k = 0; k < n; k++) { // the strings of every request inside the buffer
+		const ebd_request& q = reqs[k];
+		const uint64_t need = (uint64_t)q.host_len + q.url_len + (q.cip_len == EBD_NO_CLIENT_IP ? 0u : q.cip_len);
+		if (q.host_len + q.url_len > EBD_MAX_HTTP_REQUEST_LENGTH ||
+				(q.cip_len != EBD_NO_CLIENT_IP && q.cip_len > EBD_MAX_HTTP_REQUEST_LENGTH) || q.str_off > strings_len ||
+				need > strings_len - q.str_off)
+			return -EINVAL;
+	}
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (int rc = finish_pending(c))
+		return rc;
+	if (n == 0)
+		return 0;
+	Dev d = make_dev(c);
+	d.n = 0;
+	d.now = ctx_now(c);
+	ebd_request* drq = nullptr;
+	uint8_t* dstr = nullptr; // 16 bytes of slack: the key reads 8-byte pieces
+	HIP_TRY(hipMallocAsync((void**)&drq, (size_t)n * sizeof(ebd_request), c->stream));
+	HIP_TRY(hipMallocAsync((void**)&dstr, (size_t)strings_len + 16, c->stream));
+	hipError_t e = hipMemcpyAsync(drq, reqs, (size_t)n * sizeof(ebd_request), hipMemcpyHostToDevice, c->stream);
+	if (e == hipSuccess && strings_len)
+		e = hipMemcpyAsync(dstr, strings, (size_t)strings_len, hipMemcpyHostToDevice, c->stream);
+	if (e == hipSuccess)
+		e = hipMemsetAsync(dstr + strings_len, 0, 16, c->stream);
+	if (e == hipSuccess)
+		e = hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream);
+	if (e == hipSuccess)
+		e = launch_agg_requests(d, drq, n, dstr, c->stream, c->cus);
+	if (e == hipSuccess)
+		e = launch_verify(d, c->stream, c->cus);
+	(void)hipFreeAsync(drq, c->stream);
+	(void)hipFreeAsync(dstr, c->stream);
+	HIP_TRY(e);
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	c->seq_base += n;
 	return 0;
 }
 

@@ -2713,6 +2713,32 @@ __global__ void k_merge(Dev d, const ebd_wire_service* rec, uint32_t n, const ui
 	}
 }
 
+// service::Aggregator::newRequest (Aggregator.cpp:155-168) for requests parsed elsewhere
+// (ebd_aggregate_requests): the service key over (pid, host + url), the client class of
+// clientIp.front() or of the session's source address (Aggregator.cpp:50-88), the
+// first-arrival word and the network maps, as k_emit does for a session request.
+static_assert(sizeof(ebd_request) == 40, "ebd_request is 40 bytes");
+__global__ void k_agg_requests(Dev d, const ebd_request* rq, uint32_t n, const uint8_t* strings) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const ebd_request q = rq[k];
+		const uint8_t* h = strings + q.str_off;
+		const uint32_t hl = q.host_len, ul = q.url_len;
+		unsigned long long net = 0;
+		const uint8_t cls = q.cip_len != EBD_NO_CLIENT_IP ? classify_token(*d.ifs, h + hl + ul, q.cip_len, &net)
+		                                                  : classify_source(*d.ifs, q.flags, q.source_ip, &net);
+		const Hash128 key = endpoint_key(d.hkey, q.pid, 0, hl, hl, ul, [h](uint32_t o) { return gload8u(h + o); });
+		bool claimed;
+		const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + k, q.is_https != 0, hl), cls == CLS_INTERNAL,
+				cls == CLS_EXTERNAL, &claimed);
+		if (claimed)
+			claim_publish(d, slot, wave_add(&d.ctr[CTR_SERVICES], 1ull), wave_add(&d.ctr[CTR_SARENA], (unsigned long long)((hl + ul + 7u) & ~7u)),
+					q.pid, h, hl, h + hl, ul);
+		if (d.net_on && cls == CLS_EXTERNAL)
+			agg_nets(d, slot, net, d.now);
+		wave_add(&d.ctr[CTR_REQUESTS], 1ull);
+	}
+}
+
 // ---------------------------------------------------------------------------------
 // Synthetic trace generation in HBM (ebd_gen.h).
 // ---------------------------------------------------------------------------------
@@ -2991,6 +3017,10 @@ hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned l
 hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
 		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_wire_copy, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, offs, srcoff, arena, strings);
+	return hipGetLastError();
+}
+hipError_t launch_agg_requests(const Dev& d, const ebd_request* rq, uint32_t n, const uint8_t* strings, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_agg_requests, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rq, n, strings);
 	return hipGetLastError();
 }
 hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,

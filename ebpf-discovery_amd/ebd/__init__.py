@@ -46,6 +46,11 @@ SERVICE_NET_DTYPE = np.dtype([("key_lo", "<u8"), ("key_hi", "<u8"), ("kind", "u1
 WIRE_DTYPE = np.dtype([("key_lo", "<u8"), ("key_hi", "<u8"), ("first", "<u8"), ("pid", "<u4"), ("internal", "<u4"),
                        ("external", "<u4"), ("endpoint_len", "<u4")])
 WIRE_NO_BYTES = 0x80000000
+# ebd_request: an HttpRequest + DiscoverySessionMeta parsed elsewhere (ebd_aggregate_requests)
+REQUEST_DTYPE = np.dtype([("str_off", "<u8"), ("pid", "<u4"), ("host_len", "<u2"), ("url_len", "<u2"), ("cip_len", "<u2"),
+                          ("flags", "u1"), ("is_https", "u1"), ("source_ip", "u1", (16,)), ("pad", "<u4")])
+NO_CLIENT_IP = 0xFFFF
+assert REQUEST_DTYPE.itemsize == 40
 assert WIRE_DTYPE.itemsize == 40
 assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
 assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 80 and SERVICE_NET_DTYPE.itemsize == 32
@@ -134,6 +139,7 @@ _SIGS = {
     "ebd_export_services_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.c_void_p, C.c_void_p]),
     "ebd_merge_services_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "ebd_aggregate_requests": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ebd_strerror": (C.c_char_p, [C.c_int]),
     "ebd_build_id": (C.c_char_p, []),
@@ -481,6 +487,22 @@ class Context:
         _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
                                                C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                strings.numel()), "ebd_merge_services_device")
+
+    def aggregate_requests(self, reqs):
+        """ebd_aggregate_requests: Aggregator::newRequest for requests parsed elsewhere, in order.
+        reqs: (pid, host, url, client_ip or None, flags, is_https, source_ip16) tuples, where
+        client_ip is HttpRequest::clientIp.front() (None: clientIp empty)."""
+        recs = np.zeros(len(reqs), REQUEST_DTYPE)
+        strings = bytearray()
+        for k, (pid, host, url, cip, flags, https, src) in enumerate(reqs):
+            recs[k]["str_off"] = len(strings)
+            recs[k]["pid"], recs[k]["flags"], recs[k]["is_https"] = pid, flags, 1 if https else 0
+            recs[k]["host_len"], recs[k]["url_len"] = len(host), len(url)
+            recs[k]["cip_len"] = NO_CLIENT_IP if cip is None else len(cip)
+            recs[k]["source_ip"] = np.frombuffer(bytes(src).ljust(16, b"\0")[:16], np.uint8)
+            strings += host + url + (cip or b"")
+        sb = np.frombuffer(bytes(strings) or b"\0", np.uint8)
+        _check(lib().ebd_aggregate_requests(self.h, _p(recs), len(recs), _p(sb), len(strings)), "ebd_aggregate_requests")
 
     def stats(self):
         s = Stats()

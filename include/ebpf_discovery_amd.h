@@ -381,6 +381,29 @@ int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_wire_service* r
  * and reported as EBD_ERR_INTERNAL. */
 int ebd_merge_services_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings,
 		uint64_t strlen);
+/* --- requests parsed elsewhere (service::Aggregator::newRequest, Aggregator.h:56) -------
+ * One httpparser::HttpRequest with its DiscoverySessionMeta (Aggregator.h:40-44): what
+ * Aggregator::newRequest reads of them (Aggregator.cpp:44-130, 155-168).  Its strings lie at
+ * strings + str_off: host_len bytes of host, url_len bytes of url, then cip_len bytes of
+ * clientIp.front() (cip_len = EBD_NO_CLIENT_IP: clientIp is empty, the client is the source
+ * address). */
+#define EBD_NO_CLIENT_IP 0xffffu
+typedef struct ebd_request {
+	uint64_t str_off;
+	uint32_t pid;          /* DiscoverySessionMeta.pid */
+	uint16_t host_len, url_len;
+	uint16_t cip_len;
+	uint8_t flags;         /* DiscoverySessionMeta.flags (EBD_FLAG_SESSION_*: IPv4 / IPv6 source) */
+	uint8_t is_https;      /* HttpRequest::isHttps: the scheme of a service it creates */
+	uint8_t source_ip[16]; /* DiscoverySessionMeta.sourceIP */
+	uint32_t pad_;
+} ebd_request; /* 40 bytes */
+/* Aggregator::newRequest for n such requests in order (host memory), as one batch: the same
+ * service key, first-arrival scheme and domain, client class and network maps as requests the
+ * parse path finishes (they take the next n positions of the global event order).  Blocks
+ * until done.  Lengths over EBD_MAX_HTTP_REQUEST_LENGTH, or strings past strings_len: -EINVAL. */
+int ebd_aggregate_requests(ebd_ctx* ctx, const ebd_request* reqs, uint32_t n, const char* strings, uint64_t strings_len);
+
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
 /* Hash of the sources this library was built from (profiles/ name the build they measured). */

@@ -4,9 +4,13 @@
  * aggregator's callers change as little as possible:
  *
  *   ebdamd::Aggregator  ~ service::Aggregator      (libservice/headers/service/Aggregator.h:46-68):
- *                         clear, collectServices, networkCountersCleaning, getCurrentTime; the
- *                         per-request newRequest becomes newEvents over one poll cycle's batch,
- *                         because HttpRequestParser::parse runs inside the same GPU pass
+ *                         clear, collectServices, networkCountersCleaning, getCurrentTime;
+ *                         newEvents takes one poll cycle's captured buffers (HttpRequestParser::parse
+ *                         runs inside the same GPU pass), and newRequest(HttpRequest,
+ *                         DiscoverySessionMeta) takes requests parsed elsewhere, queued and handed
+ *                         to the GPU in batches (ebd_aggregate_requests)
+ *   ebdamd::HttpRequest ~ httpparser::HttpRequest  (HttpRequestParser.h:28-39)
+ *   ebdamd::DiscoverySessionMeta ~ DiscoverySessionMeta (Aggregator.h:40-44)
  *   ebdamd::Service     ~ service::Service         (Service.h:43-66; the network maps as their sizes,
  *                         which is all the report prints, Service.h:84-98)
  *   ebdamd::Discovery   ~ ebpfdiscovery::Discovery (Discovery.h:33-44): init, fetchAndHandleEvents,
@@ -23,6 +27,7 @@
 
 #include "ebpf_discovery_amd.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdint>
 #include <cstring>
@@ -74,6 +79,34 @@ struct Service {
 				externalIPv4_16ClientNets == o.externalIPv4_16ClientNets &&
 				externalIPv4_24ClientNets == o.externalIPv4_24ClientNets && externalIPv6ClientsNets == o.externalIPv6ClientsNets;
 	}
+};
+
+/* httpparser::HttpRequest (HttpRequestParser.h:28-39): the fields a parse fills. */
+struct HttpRequest {
+	std::string method;
+	std::string url;
+	std::string protocol;
+	std::string host;
+	std::string clientIPKey;
+	std::vector<std::string> clientIp;
+	bool isHttps = false;
+
+	/* HttpRequest::clear (HttpRequestParser.cpp:67-80) */
+	void clear() {
+		method.clear();
+		url.clear();
+		protocol.clear();
+		host.clear();
+		clientIp.clear();
+		isHttps = false;
+	}
+};
+
+/* DiscoverySessionMeta (Aggregator.h:40-44): the session a request came in on. */
+struct DiscoverySessionMeta {
+	uint8_t sourceIP[16] = {}; /* DiscoverySockSourceIP: in_addr or in6_addr bytes */
+	uint32_t pid = 0;
+	uint8_t flags = 0;         /* DiscoveryFlags (EBD_FLAG_SESSION_IPV4 / _IPV6 select the family) */
 };
 
 /* One poll cycle's events with their saved buffers, packed back to back: what
@@ -154,13 +187,61 @@ public:
 	Aggregator& operator=(const Aggregator&) = delete;
 
 	/* Aggregator::clear (Aggregator.cpp:136-153) */
-	void clear() { check(ebd_clear(ctx_), "ebd_clear"); }
+	void clear() {
+		flush();
+		check(ebd_clear(ctx_), "ebd_clear");
+	}
+
+	/* Aggregator::newRequest (Aggregator.cpp:155-168) for a request parsed elsewhere.  Batched:
+	 * the request is queued with its getCurrentTime() reading, and the queue goes to the GPU as
+	 * one ebd_aggregate_requests call when the reading changes, at kMaxQueued requests, on
+	 * flush(), and before anything that reads or changes the services (collectServices, report,
+	 * stats, clear, networkCountersCleaning, newEvents).  Throws ebdamd::Error when the library
+	 * refuses the batch (e.g. host + url longer than EBD_MAX_HTTP_REQUEST_LENGTH). */
+	void newRequest(const HttpRequest& request, const DiscoverySessionMeta& meta) {
+		const uint64_t now = getCurrentTime();
+		if (!queue_.empty() && now != queueClock_)
+			flush();
+		queueClock_ = now;
+		ebd_request q{};
+		q.str_off = queueStrings_.size();
+		q.pid = meta.pid;
+		q.host_len = (uint16_t)std::min<size_t>(request.host.size(), 0xffffu);
+		q.url_len = (uint16_t)std::min<size_t>(request.url.size(), 0xffffu);
+		q.flags = meta.flags;
+		q.is_https = request.isHttps ? 1 : 0;
+		std::memcpy(q.source_ip, meta.sourceIP, sizeof(q.source_ip));
+		queueStrings_ += request.host;
+		queueStrings_ += request.url;
+		if (request.clientIp.empty()) { // the source address decides (Aggregator.cpp:60-66, 85-88)
+			q.cip_len = EBD_NO_CLIENT_IP;
+		} else { // clientIp.front() decides (Aggregator.cpp:50-59)
+			q.cip_len = (uint16_t)std::min<size_t>(request.clientIp.front().size(), EBD_NO_CLIENT_IP - 1u);
+			queueStrings_ += request.clientIp.front();
+		}
+		queue_.push_back(q);
+		if (queue_.size() >= kMaxQueued)
+			flush();
+	}
+
+	/* The queued newRequest calls to the GPU now. */
+	void flush() {
+		if (queue_.empty())
+			return;
+		if (queueClock_)
+			check(ebd_set_clock(ctx_, queueClock_), "ebd_set_clock");
+		const int rc = ebd_aggregate_requests(ctx_, queue_.data(), (uint32_t)queue_.size(), queueStrings_.data(), queueStrings_.size());
+		queue_.clear();
+		queueStrings_.clear();
+		check(rc, "ebd_aggregate_requests");
+	}
 
 	/* Discovery::handleNewEvent for every event of the batch (Discovery.cpp:92-198), i.e.
 	 * HttpRequestParser::parse on each buffer and Aggregator::newRequest on each finished
 	 * request (Aggregator.cpp:155-168).  Returns 0 or -errno; the per-event outcomes are in
 	 * lastResults(). */
 	int newEvents(const EventBatch& batch) {
+		flush();
 		if (batch.empty())
 			return 0;
 		if (const uint64_t now = getCurrentTime())
@@ -181,7 +262,8 @@ public:
 	}
 
 	/* Aggregator::collectServices (Aggregator.cpp:170-181); order unspecified. */
-	std::vector<Service> collectServices() const {
+	std::vector<Service> collectServices() {
+		flush();
 		uint32_t n = 0;
 		uint64_t bytes = 0;
 		check(ebd_collect_services(ctx_, nullptr, 0, &n, nullptr, 0, &bytes), "ebd_collect_services");
@@ -208,10 +290,14 @@ public:
 	}
 
 	/* Aggregator::networkCountersCleaning (Aggregator.cpp:182-209) at getCurrentTime(). */
-	void networkCountersCleaning() { check(ebd_network_counters_cleaning(ctx_, getCurrentTime()), "ebd_network_counters_cleaning"); }
+	void networkCountersCleaning() {
+		flush();
+		check(ebd_network_counters_cleaning(ctx_, getCurrentTime()), "ebd_network_counters_cleaning");
+	}
 
 	/* The text Discovery::outputServicesToStdout prints (Discovery.cpp:60-71); "" without services. */
-	std::string report() const {
+	std::string report() {
+		flush();
 		uint64_t len = 0;
 		check(ebd_report_json(ctx_, nullptr, 0, &len), "ebd_report_json");
 		std::string text(len, '\0');
@@ -221,7 +307,8 @@ public:
 		return text;
 	}
 
-	ebd_stats stats() const {
+	ebd_stats stats() {
+		flush();
 		ebd_stats s{};
 		check(ebd_get_stats(ctx_, &s), "ebd_get_stats");
 		return s;
@@ -236,7 +323,11 @@ protected:
 	virtual uint64_t getCurrentTime() const { return 0; }
 
 private:
+	static constexpr size_t kMaxQueued = 1u << 16;
 	ebd_ctx* ctx_ = nullptr;
+	std::vector<ebd_request> queue_;
+	std::string queueStrings_;
+	uint64_t queueClock_ = 0;
 };
 
 /* The BPF side of Discovery (DiscoveryBpf.h; Discovery.cpp:73-110, 125-129, 210-226). */

@@ -7,7 +7,9 @@
 //                     config 1 (35-B and 31-B payloads), a saved session that
 //                     goes INVALID (bpfDiscoveryDeleteSession, Discovery.cpp:125-129), the
 //                     report and clear of outputServicesToStdout (Discovery.cpp:60-71) and the
-//                     network counters with an overridden getCurrentTime (AggregatorTest.cpp:41-46)
+//                     network counters with an overridden getCurrentTime (AggregatorTest.cpp:41-46);
+//                     AggregatorTest's two scenarios (AggregatorTest.cpp:69-172, 174-285) rebuilt on
+//                     Aggregator::newRequest(HttpRequest, DiscoverySessionMeta), the batching adapter
 // Prints "ok" and exits 0 when every check passes.
 #include "ebpf_discovery_amd.hpp"
 
@@ -114,6 +116,132 @@ protected:
 	uint64_t getCurrentTime() const override { return now; }
 };
 
+// ServiceAggregatorTest::makeRequest (AggregatorTest.cpp:48-62).  The reference's tests mock
+// IpAddressChecker's verdict per call; here the real checker (no interfaces) classifies the
+// session source address, so each request carries an address with the verdict the test mocks:
+// external 8.8.8.8 / 2001:4860::8888, internal 10.0.0.1 / ::1.
+std::pair<ebdamd::HttpRequest, ebdamd::DiscoverySessionMeta> makeRequest(uint32_t pid, const std::string& host,
+		const std::string& url, int flags = -1, bool external = false) {
+	ebdamd::HttpRequest request;
+	request.host = host;
+	request.url = url;
+	ebdamd::DiscoverySessionMeta meta;
+	if (flags >= 0) {
+		request.isHttps = (flags & EBD_FLAG_SESSION_SSL_HTTP) != 0;
+		meta.flags = (uint8_t)flags;
+	}
+	meta.pid = pid;
+	if (meta.flags & EBD_FLAG_SESSION_IPV4) {
+		const uint8_t a[4] = {8, 8, 8, 8}, b[4] = {10, 0, 0, 1};
+		std::memcpy(meta.sourceIP, external ? a : b, 4);
+	} else if (meta.flags & EBD_FLAG_SESSION_IPV6) {
+		if (external) {
+			const uint8_t a[16] = {0x20, 0x01, 0x48, 0x60, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x88, 0x88};
+			std::memcpy(meta.sourceIP, a, 16);
+		} else {
+			meta.sourceIP[15] = 1;
+		}
+	}
+	return {request, meta};
+}
+
+ebdamd::Service svc(uint32_t pid, const char* ep, const char* dom, const char* scheme, uint32_t in, uint32_t ex,
+		uint32_t n16 = 0, uint32_t n24 = 0, uint32_t n6 = 0) {
+	ebdamd::Service s;
+	s.pid = pid;
+	s.endpoint = ep;
+	s.domain = dom;
+	s.scheme = scheme;
+	s.internalClientsNumber = in;
+	s.externalClientsNumber = ex;
+	s.externalIPv4_16ClientNets = n16;
+	s.externalIPv4_24ClientNets = n24;
+	s.externalIPv6ClientsNets = n6;
+	return s;
+}
+
+bool contains(const std::vector<ebdamd::Service>& v, const ebdamd::Service& s) {
+	for (const auto& x : v)
+		if (x == s)
+			return true;
+	std::fprintf(stderr, "missing service pid %u endpoint '%s' domain '%s' scheme '%s' internal %u external %u\n", s.pid,
+			s.endpoint.c_str(), s.domain.c_str(), s.scheme.c_str(), s.internalClientsNumber, s.externalClientsNumber);
+	return false;
+}
+
+void aggregator_test_scenarios() {
+	constexpr int V4 = EBD_FLAG_SESSION_IPV4, V6 = EBD_FLAG_SESSION_IPV6, PLAIN = EBD_FLAG_SESSION_UNENCRYPTED_HTTP,
+			  SSL = EBD_FLAG_SESSION_SSL_HTTP;
+	// ServiceAggregatorTest.aggregate (AggregatorTest.cpp:69-172)
+	{
+		ebdamd::Aggregator aggregator(ebdamd::IpInterfaces{}, false);
+		CHECK(aggregator.collectServices().empty());
+		auto add = [&](uint32_t pid, const char* host, const char* url, int flags, bool external) {
+			const auto r = makeRequest(pid, host, url, flags, external);
+			aggregator.newRequest(r.first, r.second);
+		};
+		add(100, "host", "/url", V4, true);                                             // Service 1
+		add(100, "host", "/url", -1, false);                                            //   no flags: not counted
+		add(100, "host", "/url2", V4, false);                                           // Service 2
+		add(200, "host", "/url2", V4, true);                                            // Service 3
+		add(200, "host", "/url2", V4, false);
+		add(200, "host", "/url2", V4, true);
+		add(400, "google.com", "/url123", V4 | PLAIN, true);                            // Service 4
+		add(500, "8.8.8.8", "/url123", V4 | PLAIN, true);                               // Service 5
+		add(600, "dynatrace.com", "/url123", V4 | SSL, true);                           // Service 6
+		add(700, "[::1]", "/url123", V6 | PLAIN, false);                                // Service 7
+		add(800, "[2001:0db8:85a3:0001:0000:0000:0000:0000]", "/url123", V6 | SSL, true); // Service 8
+		add(900, "[2001:0db8:85a3:0001::]", "/url123", V6 | SSL, true);                 // Service 9
+		const auto services = aggregator.collectServices();
+		CHECK(services.size() == 9);
+		CHECK(contains(services, svc(100, "host/url", "host", "http", 0, 1)));
+		CHECK(contains(services, svc(100, "host/url2", "host", "http", 1, 0)));
+		CHECK(contains(services, svc(200, "host/url2", "host", "http", 1, 2)));
+		CHECK(contains(services, svc(400, "google.com/url123", "google.com", "http", 0, 1)));
+		CHECK(contains(services, svc(500, "8.8.8.8/url123", "8.8.8.8", "http", 0, 1)));
+		CHECK(contains(services, svc(600, "dynatrace.com/url123", "dynatrace.com", "https", 0, 1)));
+		CHECK(contains(services, svc(700, "[::1]/url123", "[::1]", "http", 1, 0)));
+		CHECK(contains(services, svc(800, "[2001:0db8:85a3:0001:0000:0000:0000:0000]/url123",
+				"[2001:0db8:85a3:0001:0000:0000:0000:0000]", "https", 0, 1)));
+		CHECK(contains(services, svc(900, "[2001:0db8:85a3:0001::]/url123", "[2001:0db8:85a3:0001::]", "https", 0, 1)));
+		CHECK(aggregator.stats().requests == 12);
+		aggregator.clear();
+		CHECK(aggregator.collectServices().empty());
+	}
+	// ServiceAggregatorTest.aggregateNetworkCounters (AggregatorTest.cpp:174-285), with the mocked
+	// clock's epoch at 1000 s (a map entry's time 0 means erased on the device)
+	{
+		ClockedAggregator aggregator(ebdamd::IpInterfaces{}, true);
+		const uint64_t t0 = aggregator.now, minute = 60ull * 1000000000ull;
+		CHECK(aggregator.collectServices().empty());
+		const char* clients[] = {"172.143.4.5", "172.143.6.89", "172.199.45.55", "1234:2345:3456:4567:5678:6789:7890:8901",
+				"2001:4860:4860:0000:0000:0000:0000:8888"};
+		for (uint32_t pid : {100u, 200u})
+			for (int k = 0; k < 5; k++) {
+				auto r = makeRequest(pid, "host", "/url", (k < 3 ? V4 : V6) | (pid == 100 ? PLAIN : SSL), true);
+				r.first.clientIp = {clients[k]};
+				aggregator.newRequest(r.first, r.second);
+			}
+		auto services = aggregator.collectServices();
+		CHECK(services.size() == 2);
+		CHECK(contains(services, svc(100, "host/url", "host", "http", 0, 5, 2, 3, 2)));
+		CHECK(contains(services, svc(200, "host/url", "host", "https", 0, 5, 2, 3, 2)));
+		aggregator.now = t0 + 59 * minute;
+		aggregator.networkCountersCleaning();
+		aggregator.clear();
+		services = aggregator.collectServices();
+		CHECK(services.size() == 2);
+		for (const auto& s : services)
+			CHECK(s.externalClientsNumber == 0 && s.externalIPv4_16ClientNets == 2 && s.externalIPv4_24ClientNets == 3 &&
+					s.externalIPv6ClientsNets == 2);
+		aggregator.now = t0 + 60 * minute;
+		aggregator.networkCountersCleaning();
+		aggregator.clear();
+		CHECK(aggregator.collectServices().empty());
+		CHECK(aggregator.stats().errors == 0);
+	}
+}
+
 int run_gpu() {
 	// config 1: 1000 x the 35-byte GET, one connection per event
 	{
@@ -211,6 +339,7 @@ int run_gpu() {
 		CHECK(agg.collectServices().empty());
 		CHECK(agg.stats().errors == 0);
 	}
+	aggregator_test_scenarios();
 	return 0;
 }
 

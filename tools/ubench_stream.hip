@@ -7,8 +7,10 @@
 //   quad64   k_fresh r03: a lane per event; the 4 lanes of a quad load 64-B event-relative
 //            windows (one member's window per instruction, 16 windows per instruction), DPP
 //            4x4 transpose, the next window in flight while the current one is consumed
+//   quad64a  quad64 with the windows aligned to 64 B (whole half lines; an event's first and
+//            last window are shared with its neighbours)
 //   oct128   a lane per event; 8 lanes load 128-B line-aligned windows (one member's line per
-//            instruction: every instruction = 8 whole lines), 8x8 transpose
+//            instruction: every instruction = 8 whole lines), 8x8 transpose, next line in flight
 //   dma<L,D> L loader waves copy the workgroup's span into an LDS ring of 16-KiB slots by
 //            global_load_lds_dwordx4 (1 KiB per wave instruction), D slots in flight per
 //            loader; the other waves read each ready slot once (ds_read_b128) and free it
@@ -147,12 +149,14 @@ __global__ __launch_bounds__(kThreads) void k_quad64(const uint8_t* pay, const u
 		const bool valid = e0.idx < re && tidx == e0.idx && tw == w0;
 		v4u X[4] = {W[0], W[1], W[2], W[3]};
 		const uint32_t nwin = (e0.L + 63) >> 6;
-		if (!valid)
-			issue(e0.p, e0.L, w0), tidx = e0.idx, tw = w0;
-		else if (w0 + 1 < nwin)
-			issue(e0.p, e0.L, w0 + 1), tidx = e0.idx, tw = w0 + 1;
-		else
-			issue(e1.p, e1.L, 0), tidx = e1.idx, tw = 0;
+		{ // the next window's address is chosen per lane; the quad-cooperative loads run uniformly
+			const bool same = !valid || w0 + 1 < nwin;
+			const uint32_t nw = !valid ? w0 : same ? w0 + 1 : 0;
+			const Ev& ne = same ? e0 : e1;
+			issue(ne.p, ne.L, nw);
+			tidx = ne.idx;
+			tw = nw;
+		}
 		transpose_quad(X, r);
 		if (valid) {
 #pragma unroll
@@ -193,41 +197,129 @@ __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const u
 	uint32_t rb, re;
 	wg_range(n, rb, re);
 	if (threadIdx.x == 0)
-		next = rb + kThreads;
+		next = rb + 2 * kThreads;
 	__syncthreads();
 	const uint32_t lane = threadIdx.x & 63, r = lane & 7, ob = lane & ~7u;
-	uint32_t ei = rb + threadIdx.x, w = 0, nl = 0, acc = 0;
-	unsigned long long a0 = 0;
-	auto load_ev = [&]() {
-		if (ei < re) {
-			const unsigned long long a = (unsigned long long)(uintptr_t)(pay + off[ei]);
-			a0 = a & ~127ull;
-			nl = (uint32_t)(((a & 127ull) + len[ei] + 127ull) >> 7);
-		} else {
-			a0 = (unsigned long long)(uintptr_t)pay;
-			nl = 0;
-		}
-		w = 0;
+	// a lane's event as line-aligned 128-B windows: first line a0, nl lines
+	struct LEv {
+		uint32_t idx, nl;
+		unsigned long long a0;
 	};
-	load_ev();
-	while (__any(ei < re)) {
+	auto lev = [&](uint32_t i) {
+		LEv e;
+		e.idx = i;
+		if (i < re) {
+			const unsigned long long a = (unsigned long long)(uintptr_t)(pay + off[i]);
+			e.a0 = a & ~127ull;
+			e.nl = (uint32_t)(((a & 127ull) + len[i] + 127ull) >> 7);
+		} else {
+			e.a0 = (unsigned long long)(uintptr_t)pay;
+			e.nl = 0;
+		}
+		return e;
+	};
+	LEv e0 = lev(rb + threadIdx.x), e1 = lev(rb + kThreads + threadIdx.x);
+	uint32_t w0 = 0, acc = 0, tidx = e0.idx, tw = 0;
+	v4u W[8];
+	auto issue = [&](unsigned long long a0, uint32_t nl, uint32_t w) {
 		const unsigned long long la = a0 + 128ull * min(w, nl ? nl - 1 : 0u);
-		v4u X[8];
 #pragma unroll
 		for (int k = 0; k < 8; k++) {
 			const unsigned long long ak = (unsigned long long)__shfl((long long)la, (int)(ob + k));
-			X[k] = ld16((const uint8_t*)(uintptr_t)(ak + 16ull * r));
+			W[k] = ld16((const uint8_t*)(uintptr_t)(ak + 16ull * r));
+		}
+	};
+	issue(e0.a0, e0.nl, 0);
+	while (__any(e0.idx < re)) {
+		const bool valid = e0.idx < re && tidx == e0.idx && tw == w0;
+		v4u X[8];
+#pragma unroll
+		for (int k = 0; k < 8; k++)
+			X[k] = W[k];
+		{
+			const bool same = !valid || w0 + 1 < e0.nl;
+			const uint32_t nw = !valid ? w0 : same ? w0 + 1 : 0;
+			const LEv& ne = same ? e0 : e1;
+			issue(ne.a0, ne.nl, nw);
+			tidx = ne.idx;
+			tw = nw;
 		}
 		xstage<4>(X, r);
 		xstage<2>(X, r);
 		xstage<1>(X, r);
-		if (ei < re) {
+		if (valid) {
 #pragma unroll
 			for (int k = 0; k < 8; k++)
 				acc ^= fold(X[k]);
-			if (++w >= nl) {
-				ei = atomicAdd(&next, 1u);
-				load_ev();
+			if (++w0 >= e0.nl) {
+				e0 = e1;
+				e1 = lev(atomicAdd(&next, 1u));
+				w0 = 0;
+			}
+		}
+	}
+	out[blockIdx.x * kThreads + threadIdx.x] = acc;
+}
+
+// quad64a: quad64 with 64-B windows aligned to 64 B (each a whole half line)
+__global__ __launch_bounds__(kThreads) void k_quad64a(const uint8_t* pay, const uint64_t* off, const uint32_t* len, uint32_t n,
+		uint32_t* out) {
+	__shared__ uint32_t next;
+	uint32_t rb, re;
+	wg_range(n, rb, re);
+	if (threadIdx.x == 0)
+		next = rb + 2 * kThreads;
+	__syncthreads();
+	const uint32_t r = threadIdx.x & 3;
+	struct QEv {
+		uint32_t idx, nw;
+		unsigned long long a0;
+	};
+	auto qev = [&](uint32_t i) {
+		QEv e;
+		e.idx = i;
+		if (i < re) {
+			const unsigned long long a = (unsigned long long)(uintptr_t)(pay + off[i]);
+			e.a0 = a & ~63ull;
+			e.nw = (uint32_t)(((a & 63ull) + len[i] + 63ull) >> 6);
+		} else {
+			e.a0 = (unsigned long long)(uintptr_t)pay;
+			e.nw = 0;
+		}
+		return e;
+	};
+	QEv e0 = qev(rb + threadIdx.x), e1 = qev(rb + kThreads + threadIdx.x);
+	uint32_t w0 = 0, acc = 0, tidx = e0.idx, tw = 0;
+	v4u W[4];
+	auto issue = [&](unsigned long long a0, uint32_t nw, uint32_t w) {
+		const unsigned long long a = a0 + 64ull * min(w, nw ? nw - 1 : 0u);
+		unsigned long long ak[4];
+		ak[0] = qbcast64<0>(a), ak[1] = qbcast64<1>(a), ak[2] = qbcast64<2>(a), ak[3] = qbcast64<3>(a);
+#pragma unroll
+		for (int k = 0; k < 4; k++)
+			W[k] = ld16((const uint8_t*)(uintptr_t)(ak[k] + 16ull * r));
+	};
+	issue(e0.a0, e0.nw, 0);
+	while (__any(e0.idx < re)) {
+		const bool valid = e0.idx < re && tidx == e0.idx && tw == w0;
+		v4u X[4] = {W[0], W[1], W[2], W[3]};
+		{
+			const bool same = !valid || w0 + 1 < e0.nw;
+			const uint32_t nw = !valid ? w0 : same ? w0 + 1 : 0;
+			const QEv& ne = same ? e0 : e1;
+			issue(ne.a0, ne.nw, nw);
+			tidx = ne.idx;
+			tw = nw;
+		}
+		transpose_quad(X, r);
+		if (valid) {
+#pragma unroll
+			for (int k = 0; k < 4; k++)
+				acc ^= fold(X[k]);
+			if (++w0 >= e0.nw) {
+				e0 = e1;
+				e1 = qev(atomicAdd(&next, 1u));
+				w0 = 0;
 			}
 		}
 	}
@@ -388,6 +480,7 @@ int main(int argc, char** argv) {
 	const dim3 g(cus), b(kThreads);
 	run("read", [&] { hipLaunchKernelGGL(k_read, g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("quad64", [&] { hipLaunchKernelGGL(k_quad64, g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("quad64a", [&] { hipLaunchKernelGGL(k_quad64a, g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("oct128", [&] { hipLaunchKernelGGL(k_oct128, g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("dma1x3", [&] { hipLaunchKernelGGL((k_dma<1, 3>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
 	run("dma2x2", [&] { hipLaunchKernelGGL((k_dma<2, 2>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
