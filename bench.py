@@ -258,8 +258,15 @@ def main():
     G = E * world if cfg == 5 else E  # trace positions per step (candidates)
 
     cuts = list(range(0, n, sub)) + [n]
+    if world > 1:
+        from ebd import shard
 
-    def step(k, cold, each=None):
+        def map_first(f):  # local first_seq (k * G + local index) -> trace position (k * G + gidx)
+            k = torch.div(f, G, rounding_mode="floor")
+            return k * G + gidx_t[f - k * G]
+    merges = []  # per cold step at N > 1: (ms, exchange stats)
+
+    def step(k, cold, each=None, merge=False):
         if cold:
             ctx.clear()  # Aggregator::clear after the previous interval's report (Aggregator.cpp:136-153)
         # global trace order: step k's event i is at k * G + its position in the trace
@@ -269,6 +276,12 @@ def main():
             if each is not None:
                 ctx.sync()
                 each(a, z)
+        if merge:
+            # the interval's report needs the merged table (Discovery.cpp:60-71): each GPU's
+            # services go to their owners and merge there, inside the step
+            tm = time.perf_counter()
+            x = shard.device_exchange_merge(ctx, dev, map_first=map_first)
+            merges.append(((time.perf_counter() - tm) * 1e3, x))
 
     def timed_steps(k0, cold):
         if world > 1:
@@ -276,7 +289,7 @@ def main():
         torch.cuda.synchronize()
         t = time.perf_counter()
         for k in range(k0, k0 + args.steps):
-            step(k, cold)
+            step(k, cold, merge=world > 1 and cold)
         ctx.sync()
         torch.cuda.synchronize()
         if world > 1:
@@ -290,12 +303,14 @@ def main():
 
     cold = args.mode == "cold"
     for k in range(args.warmup):
-        step(k, cold)
+        step(k, cold, merge=world > 1 and cold)
     ctx.sync()
     ctx.reset_kernel_times()
+    merges.clear()
     elapsed = timed_steps(args.warmup, cold)
     kt = ctx.kernel_times()
     st = ctx.stats()
+    step_merges = list(merges)
     # the other mode, reported beside (same batch, same number of steps)
     other_mode = "warm" if cold else "cold"
     ctx.reset_kernel_times()
@@ -338,32 +353,34 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
 
-    # the final per-(pid, endpoint) merge across GPUs, once, after the timed steps:
-    # owner-partitioned all_to_all over RCCL and a device merge on each owner (ebd.shard)
+    # the per-(pid, endpoint) merge across GPUs: owner-partitioned all_to_all over RCCL and a
+    # device merge on each owner (ebd.shard).  Cold mode: inside every timed step (one report
+    # interval per step), so `value` includes it.  Warm mode: once, after the timed steps.
     merge = None
     n_all = n
     if world > 1:
-        from ebd import shard
-        def map_first(f):  # local first_seq (k * G + local index) -> trace position (k * G + gidx)
-            k = torch.div(f, G, rounding_mode="floor")
-            return k * G + gidx_t[f - k * G]
-
-        torch.distributed.barrier()
-        torch.cuda.synchronize()
-        tm = time.perf_counter()
-        x = shard.device_exchange_merge(ctx, dev, map_first=map_first)
-        ctx.sync()
-        torch.distributed.barrier()
-        merge_ms = (time.perf_counter() - tm) * 1e3
+        if step_merges:
+            merge_ms = max(m for m, _ in step_merges)
+            x = step_merges[-1][1]
+            where = "inside every timed step (cold: one report interval per step), included in value"
+        else:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+            tm = time.perf_counter()
+            x = shard.device_exchange_merge(ctx, dev, map_first=map_first)
+            ctx.sync()
+            torch.distributed.barrier()
+            merge_ms = (time.perf_counter() - tm) * 1e3
+            where = "once after the timed steps (warm: the table of all steps), not in value"
         owned = ctx.stats()["services"]
         tot = torch.tensor([n, owned, x["sent"], x["record_bytes"], x["string_bytes"]], dtype=torch.int64, device=dev)
         torch.distributed.all_reduce(tot)
         mt = torch.tensor([merge_ms], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(mt, op=torch.distributed.ReduceOp.MAX)
         n_all = int(tot[0])
-        merge = {"merge_ms": float(mt.item()), "services_merged": int(tot[1]), "records_exchanged": int(tot[2]),
-                 "record_bytes": int(tot[3]), "string_bytes": int(tot[4]), "record_size": shard.REC.itemsize,
-                 "table_state": "the last timed step's interval (cold) or all steps (warm)"}
+        merge = {"merge_ms": float(mt.item()), "where": where, "services_merged": int(tot[1]),
+                 "records_exchanged": int(tot[2]), "record_bytes_per_interval": int(tot[3]),
+                 "string_bytes_per_interval": int(tot[4]), "record_size": shard.REC.itemsize}
         if rank != 0:
             torch.distributed.destroy_process_group()
             return
