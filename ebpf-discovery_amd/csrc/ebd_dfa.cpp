@@ -137,11 +137,7 @@ void build_lds_image(const DfaTable* t, uint8_t* out) {
 	std::memset(out, 0, kLdsTableBytes);
 	for (uint32_t st = 0; st < kLdsRows; st++)
 		for (uint32_t b = 0; b < kLdsCols; b++)
-#ifdef EBD_STATE_MAJOR
-			out[st * 256 + b] = t->next[st * 256 + b];
-#else
 			out[b * kLdsStride + st] = t->next[st * 256 + b];
-#endif
 }
 
 int build_dfa(const KeyTrie* trie, DfaTable* out) {

@@ -53,11 +53,7 @@ constexpr uint32_t kLdsRows = kLdsStride; // >= nstates (ebd_build_dfa checks)
 // Every byte >= 0x80 steps like 0x7f in every state (no class of the parser holds one;
 // build_dfa checks), so the image keeps 128 columns and a step reads column min(b, 127):
 // 25 KB of LDS instead of 50 KB, which k_fresh spends on a wider finalize staging.
-#ifdef EBD_STATE_MAJOR
-constexpr uint32_t kLdsCols = 256;
-#else
 constexpr uint32_t kLdsCols = 128;
-#endif
 constexpr uint32_t kLdsTableBytes = kLdsCols * kLdsStride;
 void build_lds_image(const DfaTable* t, uint8_t* out); // out: kLdsTableBytes
 

@@ -146,14 +146,12 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 		return kNone;
 	}
 	Slot* s = d.slots + idx;
-#ifndef EBD_EXP_AGG_NOATOMIC // experiment: probe only, no counter / first-arrival atomics
 	if (inc_int)
 		atomicAdd(&s->internal_clients, inc_int);
 	if (inc_ext)
 		atomicAdd(&s->external_clients, inc_ext);
 	if (first < seen_first)
 		atomicMin(&s->first, first);
-#endif
 	return idx;
 }
 
@@ -362,11 +360,7 @@ __device__ int sset_find(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid) 
 // Logical index (s << 8) | b into the LDS image (ebd_dfa.h: byte-major, kLdsStride).
 struct LdsTable {
 	const uint8_t* t;
-#ifdef EBD_STATE_MAJOR
-	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[i]; }
-#else
 	__device__ __forceinline__ uint32_t operator[](uint32_t i) const { return t[min(i & 0xffu, kLdsCols - 1) * kLdsStride + (i >> 8)]; }
-#endif
 };
 
 // One 16-byte chunk as 4 little-endian words.
@@ -409,16 +403,7 @@ constexpr int kFreshWaves = kFreshThreads / 64;
 // and endpoint bytes past the staged 64 B come from HBM): 10 scan + 6 finalize waves beat
 // 12 + 4 (2.74 vs 2.87 ms per 20 M config-3 events) and 11 + 5 or 9 + 7.
 constexpr int kScanWaves = EBD_SCAN_WAVES;
-#ifdef EBD_PREFETCH
-// one wave streams the workgroup's payload into L2 / the Infinity Cache ahead of the scan front
-constexpr int kPfWaves = 1;
-#ifndef EBD_PF_BYTES
-#define EBD_PF_BYTES 65536
-#endif
-constexpr uint64_t kPfBytes = EBD_PF_BYTES; // distance ahead of the scan front
-#else
 constexpr int kPfWaves = 0;
-#endif
 constexpr int kFinWaves = kFreshWaves - kScanWaves - kPfWaves;
 constexpr uint32_t kScanLanes = kScanWaves * 64, kFinLanes = kFinWaves * 64;
 #ifndef EBD_RING
@@ -432,11 +417,7 @@ static_assert(kRing >= 128 && (kRing & (kRing - 1)) == 0, "ring: a power of two 
 
 // LDS address of entry (s, byte k of word x): v_bfe (off the state chain) + v_mad_u32_u24.
 __device__ __forceinline__ uint32_t tab_index(uint32_t s, uint32_t x, int k) {
-#ifdef EBD_STATE_MAJOR // entry (s, b) at s * 256 + b: one v_perm_b32 builds the index
-	return __builtin_amdgcn_perm(s, x, 0x0c0c0400u | (uint32_t)(k & 3));
-#else
 	return min(__builtin_amdgcn_ubfe(x, 8 * (k & 3), 8), kLdsCols - 1) * kLdsStride + s;
-#endif
 }
 
 // Every byte of w in [0x20, 0x7e] (SWAR: no byte < 0x20, none >= 0x7f; exact tests).
@@ -448,61 +429,25 @@ __device__ __forceinline__ bool printable4(uint32_t w) {
 
 // 16 DFA steps over one chunk: s advances, m = the maximum next state, qs = the states at
 // the quarter starts (s0 | s4 << 8 | s8 << 16 | s12 << 24), qm = running maxima after 4, 8
-// and 12 steps (ebd_fresh.h chunk_update).  With EBD_SKIP, a quarter (one 4-byte word)
-// whose start state is a generic header-value state (di.vl0 / di.vl1: they step to
-// themselves on every byte in [0x20, 0x7e], checked when the table is built) and whose
-// bytes are all in that range leaves the state as it is and the lane skips its 4 table
-// reads.  The skip is exec-masked: the wave still waits for the lanes that step, and the
-// test costs more issue slots than the LDS reads it saves (20 M config-3 events: 2.87 ms
-// without, 2.92 ms with), so it is off by default.
-#ifdef EBD_EXP_DUAL
-#define DUAL_ARG , uint32_t& g_dual
-#define DUAL_PASS , dual
-#else
-#define DUAL_ARG
-#define DUAL_PASS
-#endif
-__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t vl0, uint32_t vl1, uint32_t& s,
-		uint32_t& m, uint32_t& qs, uint32_t& qm DUAL_ARG) {
+// and 12 steps (ebd_fresh.h chunk_update).  (Skipping a printable quarter in a generic
+// header-value state was measured slower: exec-masked, the wave still waits for the lanes
+// that step)
+__device__ __forceinline__ void scan_chunk(const uint8_t* T, const Chunk& w, uint32_t& s, uint32_t& m, uint32_t& qs, uint32_t& qm) {
 	qs = s;
 	m = 0;
 #pragma unroll
 	for (int q = 0; q < 4; q++) {
 		const uint32_t x = w.w[q];
-#ifdef EBD_SKIP
-		const bool skip = (s == vl0 || s == vl1) && printable4(x);
-#else
-		const bool skip = false;
-#endif
-		if (!skip) {
 #pragma unroll
-			for (int k = 0; k < 4; k++) {
-#ifdef EBD_EXP_DUAL // experiment: a second, independent chain over the same bytes (ILP probe)
-				g_dual = T[tab_index(g_dual, x, k)];
-#endif
-#ifndef EBD_EXP_FAKESTEP
-				s = T[tab_index(s, x, k)];
-#else // experiment: a VALU-only step in place of the LDS table read (results are wrong)
-				s = 64u | ((s * 5u + __builtin_amdgcn_ubfe(x, 8 * (k & 3), 8)) & 63u);
-#endif
-#ifndef EBD_EXP_LEAN
-				m = max(m, s);
-#endif
-			}
-		} else {
+		for (int k = 0; k < 4; k++) {
+			s = T[tab_index(s, x, k)];
 			m = max(m, s);
 		}
-#ifndef EBD_EXP_LEAN
 		if (q < 3) {
 			qs |= s << (8 * (q + 1));
 			qm = q == 0 ? m : (qm | (m << (8 * q)));
 		}
-#endif
 	}
-#ifdef EBD_EXP_LEAN // experiment: steps only, no chunk maximum or quarter states (results are wrong)
-	m = s;
-	qm = 0;
-#endif
 }
 
 // quad_perm DPP: the value of `v` held by quad lane P's pattern
@@ -619,23 +564,20 @@ enum : uint32_t {
 	R_LIM = R_QS + 5, // staged leading bytes that are valid
 	R_SRC,  // the source address (4 words): finalize classifies it (Aggregator.cpp:60-66, 85-88)
 	R_POS = R_SRC + 4, // ring position + 1 (checked by finalize)
+	R_TW,   // the 4 bytes the terminal tracker's rescan needs, from the scan lane's registers
 	R_WORDS
 };
-static_assert(R_WORDS == 20, "finalize record is 20 words");
+static_assert(R_WORDS == 21, "finalize record is 21 words");
 
 // Leading buffer bytes a scan lane stages (window 0), carried to finalize in LDS so that it
 // reads the request line and usually the Host header from LDS instead of reloading lines
 // that left L2 while the lane scanned the rest of the buffer.  Rows are structure of
 // arrays too: word j of the row of lane (or slot) l at [j * stride + l], one row of slack.
-#ifndef EBD_NO_STAGING
 #ifndef EBD_STAGE
 #define EBD_STAGE 96 // window 0 and the first half of window 1 (the request line and, mostly, Host)
 #endif
 constexpr uint32_t kStage = EBD_STAGE, kStageWords = kStage / 4;
 static_assert(kStage >= 64 && kStage <= 128 && kStage % 16 == 0, "staging: window 0 plus whole chunks of window 1");
-#else // experiment: finalize reads every byte from the buffer (no LDS staging)
-constexpr uint32_t kStage = 0, kStageWords = 1;
-#endif
 
 // Buffer bytes for fresh_finalize: offsets [0, lim) from the staged copy (word j at
 // s[j * kFinLanes]), the rest from the buffer in global memory.
@@ -643,10 +585,13 @@ struct StagedMem {
 	const uint8_t* p;
 	const uint32_t* s;
 	uint32_t lim;
+	uint32_t two, tw; // the word at buffer offset two, carried in the record (R_TW)
 	__device__ __forceinline__ uint32_t lds4(uint32_t o) const {
 		return __builtin_amdgcn_alignbyte(s[((o >> 2) + 1) * kFinLanes], s[(o >> 2) * kFinLanes], o & 3u);
 	}
 	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
+		if (o == two)
+			return tw;
 		if (o + 4 <= lim)
 			return lds4(o);
 		return *(const __attribute__((address_space(1))) u32a1*)(p + o);
@@ -699,8 +644,11 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	sr.cqm = q[R_CQM];
 	sr.cseen = (q[R_SF] >> 16) & 1u;
 	FreshResult fr;
-	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM]}, L, d.hkey,
-			q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
+	// the terminal tracker's word travels in the record: it lies at the end of the request,
+	// past the staged bytes, where a reload from HBM cost one line per event
+	const uint32_t two = 16 * sr.term.c + 4 * flip_quarter<RS_TERM>(d.di, sr.term, 0);
+	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM], two, q[R_TW]}, L,
+			d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 		if (!fr.cip) { // the client is the session's source address; a client-IP token is k_agg_fast's
@@ -709,10 +657,6 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 			fr.r.info = (uint8_t)(fr.r.info | (classify_source(*d.ifs, (uint8_t)(q[R_SF] >> 8), src) << EBD_INFO_CLASS_SHIFT));
 		}
 	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
-#ifdef EBD_EXP_LEAN
-		d.res[i] = fr.r;
-		return;
-#endif
 		// the session may be saved (Discovery.cpp:148-150): sequential path
 		const EventRec& ev = d.ev[i];
 		d.ev_slot[wave_add(&d.ctr[CTR_UNFINISHED], 1ull)] = i; // k_sset_build inserts its session
@@ -750,38 +694,6 @@ void k_fresh(Dev d) {
 	__syncthreads();
 	const DfaInfo& di = d.di;
 
-#ifdef EBD_PREFETCH
-	if (wave == kFreshWaves - 1) {
-		// ---- prefetcher: touches every 128-B line of the payload up to kPfBytes past the scan
-		// front (the buffer of the next event the scan lanes will take), 64 lines per load
-		// instruction, 8 instructions per round, so the lanes' window loads hit in L2 / MALL ----
-		const unsigned long long lo = rb < re ? d.off[rb] & ~127ull : 0, hi = rb < re ? d.off[re - 1] + d.len[re - 1] : 0;
-		unsigned long long upto = lo;
-		uint32_t sink = 0;
-		while (upto < hi) {
-			if (lds_load_acq(&sh.scan_done) == (uint32_t)kScanWaves)
-				break;
-			const uint32_t front = min(lds_load_acq(&sh.next_ev), re - 1);
-			const unsigned long long want = min(hi, d.off[front] + kPfBytes);
-			if (upto >= want) {
-				__builtin_amdgcn_s_sleep(8);
-				continue;
-			}
-			uint32_t acc = 0;
-#pragma unroll
-			for (uint32_t k = 0; k < 8; k++) {
-				const unsigned long long o = upto + k * 8192ull + lane * 128ull;
-				if (o < want)
-					acc ^= *(const volatile uint32_t*)(d.payload + o);
-			}
-			sink ^= acc;
-			upto = min(want, upto + 8 * 8192ull);
-		}
-		if (sink == 0x9e3779b9u && d.n == 0xffffffffu) // never: keeps the loads
-			set_error(d, EBD_ERR_INTERNAL);
-		return;
-	}
-#endif
 
 	if (wave >= kScanWaves) {
 		// ---- finalize waves: 64 records at a time, in position order ----
@@ -829,14 +741,12 @@ void k_fresh(Dev d) {
 					fs[j * kFinLanes] = sh.rdata[j * kRing + slot];
 				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
 			}
-#ifndef EBD_EXP_NOFIN // experiment: scan without finalize (results are wrong)
 			if (st == 1) {
 				if (q[R_POS] != pos + 1)
 					set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
 				else
 					finalize_rec(d, T, q, fs);
 			}
-#endif
 		}
 		return;
 	}
@@ -850,14 +760,11 @@ void k_fresh(Dev d) {
 	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
 	uint32_t w0 = 0; // e0's window to scan next
 	uint32_t s = di.init, live = 0, post = 0;
-#ifdef EBD_EXP_DUAL
-	uint32_t dual = di.init + 1;
-#endif
 	ScanRec sr;
 	rec_init(di, sr);
 
-	// Hands e0's scan record to the finalize waves when `done`.
-	auto push = [&](bool done) {
+	// Hands e0's scan record to the finalize waves when `done`; tw: the terminal tracker's word.
+	auto push = [&](bool done, uint32_t tw) {
 		const unsigned long long b = __ballot(done);
 		if (b == 0)
 			return;
@@ -895,14 +802,13 @@ void k_fresh(Dev d) {
 			t[R_SRC + 2] = e0.src.z;
 			t[R_SRC + 3] = e0.src.w;
 			t[R_POS] = pos + 1;
+			t[R_TW] = tw;
 #pragma unroll
 			for (uint32_t f = 0; f < R_WORDS; f++)
 				sh.ring[f * kRing + slot] = t[f];
-#ifndef EBD_NO_STAGING
 #pragma unroll
 			for (uint32_t j = 0; j < kStageWords; j++)
 				sh.rdata[j * kRing + slot] = stg[j * kScanLanes];
-#endif
 			lds_store_rel(&sh.ready[slot], pos + 1);
 		}
 	};
@@ -975,23 +881,16 @@ void k_fresh(Dev d) {
 			tw = nw;
 		}
 		transpose_quad(X, r);
-#ifdef EBD_EXP_XPOSE3 // experiment: two more transposes (an involution: results unchanged), to price one
-		transpose_quad(X, r);
-		transpose_quad(X, r);
-#endif
 		bool done = false;
 		if (valid) {
 			if (w0 == 0) {
 				post = (X[0].w[0] & 0xffu) == 'P' ? 1u : 0u;
-#ifndef EBD_NO_STAGING
 #pragma unroll
 				for (int k = 0; k < 4; k++) // window 0 into the lane's staging row
 #pragma unroll
 					for (int j = 0; j < 4; j++)
 						stg[(4 * k + j) * kScanLanes] = X[k].w[j];
-#endif
 			}
-#ifndef EBD_NO_STAGING
 			if (w0 == 1) {
 #pragma unroll
 				for (int k = 0; k < (int)(kStage - 64) / 16; k++) // window 1's first chunks
@@ -999,97 +898,36 @@ void k_fresh(Dev d) {
 					for (int j = 0; j < 4; j++)
 						stg[(16 + 4 * k + j) * kScanLanes] = X[k].w[j];
 			}
-#endif
-#if defined(EBD_EXP_SPLIT4) // experiment: every chunk its own chain (ILP probe; results are wrong)
-			{
-				uint32_t sx[4], m[4], qs[4], qm[4];
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					sx[k] = s ^ (uint32_t)k;
-					scan_chunk(T, X[k], di.vl0, di.vl1, sx[k], m[k], qs[k], qm[k]);
-				}
-				if (live) {
-#pragma unroll
-					for (int k = 0; k < 4; k++)
-						chunk_update(di, sr, 4 * w0 + k, s ^ (uint32_t)k, qs[k], qm[k], m[k]);
-					live = 64 * (w0 + 1) < e0.L ? 1u : 0u; // every byte of the buffer (no early end on garbage states)
-					s = sx[0] ^ sx[1] ^ sx[2] ^ sx[3];
-				}
-			}
-#elif defined(EBD_EXP_SPLIT) // experiment: chunks 0-1 and 2-3 as two independent chains (ILP probe; results are wrong)
-			{
-				uint32_t sa = s, sb = s ^ 1u, m0, qs0, qm0, m1, qs1, qm1;
-				scan_chunk(T, X[0], di.vl0, di.vl1, sa, m0, qs0, qm0);
-				scan_chunk(T, X[2], di.vl0, di.vl1, sb, m1, qs1, qm1);
-				if (live)
-					chunk_update(di, sr, 4 * w0 + 0, s, qs0, qm0, m0);
-				if (live)
-					chunk_update(di, sr, 4 * w0 + 2, s ^ 1u, qs1, qm1, m1);
-				const uint32_t sa1 = sa, sb1 = sb;
-				scan_chunk(T, X[1], di.vl0, di.vl1, sa, m0, qs0, qm0);
-				scan_chunk(T, X[3], di.vl0, di.vl1, sb, m1, qs1, qm1);
-				if (live) {
-					chunk_update(di, sr, 4 * w0 + 1, sa1, qs0, qm0, m0);
-					chunk_update(di, sr, 4 * w0 + 3, sb1, qs1, qm1, m1);
-					live = 64 * (w0 + 1) < e0.L ? 1u : 0u; // every byte of the buffer (no early end on garbage states)
-					s = sa ^ sb ^ s;
-				}
-			}
-#else
 #pragma unroll
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
-#ifndef EBD_EXP_NOSCAN
-				scan_chunk(T, X[k], di.vl0, di.vl1, sx, m, qs, qm DUAL_PASS);
-#else // experiment: the window stream alone, no DFA (results are wrong)
-				sx = (s ^ X[k].w[0] ^ X[k].w[1] ^ X[k].w[2] ^ X[k].w[3]) & 63u;
-				m = qs = qm = sx;
-#endif
+				scan_chunk(T, X[k], sx, m, qs, qm);
 				if (live) {
 					const uint32_t c = 4 * w0 + k;
-#ifndef EBD_EXP_NOTRACK // experiment: no crossing trackers (results are wrong)
-#ifndef EBD_EXP_LEAN
 					chunk_update(di, sr, c, s, qs, qm, m);
-#else // one select per tracker of (chunk | start state << 16)
-					{
-						const uint32_t pk = c | (s << 16);
-						sr.url.c = st_pred<RS_URL>(di, s) ? sr.url.c : pk;
-						sr.host.c = st_pred<RS_HOST>(di, s) ? sr.host.c : pk;
-						sr.hend.c = st_pred<RS_HEND>(di, s) ? sr.hend.c : pk;
-						sr.cip.c = sr.cseen ? sr.cip.c : pk;
-						sr.cseen |= s >= di.hvc0 ? 1u : 0u;
-						sr.term.c = c;
-					}
-#endif
-#endif
-#ifdef EBD_EXP_LENLIVE // experiment: scan every byte of the buffer (the SPLIT probes' baseline)
-					live = 16 * (c + 1) < e0.L ? 1u : 0u;
-#else
 					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
-#endif
 					s = sx;
 				}
 			}
-#endif
 			w0++;
 			done = !live;
 		}
-#ifndef EBD_EXP_NOPUSH // experiment: no records for finalize (results are wrong)
-		push(done);
-#else // every result NONE, so that the kernels after k_fresh follow no span of a parse it did not finish
-		if (done)
-			write_none(d, e0.idx);
-#endif
+		uint32_t tw = 0;
+		if (done) { // the last chunk scanned is the terminal tracker's, in this window's registers
+			const uint32_t k = sr.term.c & 3u, qt = flip_quarter<RS_TERM>(di, sr.term, 0);
+			uint32_t w4[4];
+#pragma unroll
+			for (int j = 0; j < 4; j++)
+				w4[j] = k == 0 ? X[0].w[j] : k == 1 ? X[1].w[j] : k == 2 ? X[2].w[j] : X[3].w[j];
+			tw = qt == 0 ? w4[0] : qt == 1 ? w4[1] : qt == 2 ? w4[2] : w4[3];
+		}
+		push(done, tw);
 		if (done) {
 			e0 = e1;
 			e1 = lane_ev(d, grab(), re);
 			resolve();
 		}
 	}
-#ifdef EBD_EXP_DUAL
-	if ((dual ^ d.n) == 0x7fffffffu) // never: keeps the second chain alive
-		set_error(d, EBD_ERR_INTERNAL);
-#endif
 	if (lane == 0)
 		atomicAdd(&sh.scan_done, 1u);
 }
@@ -2049,11 +1887,6 @@ struct AggShared {
 
 __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_event_result& r, uint32_t cls, AggShared& sh,
 		unsigned long long net) {
-#ifdef EBD_EXP_AGG_NOINSERT // experiment: classification only (results are wrong)
-	if (cls == 7)
-		atomicAdd(&sh.cn, 1u);
-	return;
-#endif
 	bool claimed;
 	const Hash128 key = d.keys[i];
 	const uint32_t slot = agg_insert(d, key, first_word(d.seq_base + i, (r.info & EBD_INFO_HTTPS) != 0, r.u.span.host_len),
@@ -2078,11 +1911,7 @@ __device__ __forceinline__ void agg_request(const Dev& d, uint32_t i, const ebd_
 __device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* row, AggShared& sh) {
 	ebd_event_result r = d.res[i];
 	unsigned long long net = 0;
-#ifndef EBD_EXP_AGG_NOCIP // experiment: no client-IP token parse (results are wrong)
 	const uint32_t cls = cip_classify(d, i, r, row, &net);
-#else
-	const uint32_t cls = CLS_INTERNAL;
-#endif
 	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
 	d.res[i] = r;
 	agg_request(d, i, r, cls, sh, net);
