@@ -238,11 +238,14 @@ class Context:
         self.h = h
         self.max_events = max_events
         self.network_counters = network_counters
+        self._held = []  # device tensors the queued work of the context reads or writes (_fence)
 
     def close(self):
         if getattr(self, "h", None):
-            lib().ebd_ctx_destroy(self.h)
+            lib().ebd_ctx_destroy(self.h)  # waits for the context's streams
             self.h = None
+            self._ext = None
+            self._held = []
 
     def __del__(self):
         self.close()
@@ -312,10 +315,10 @@ class Context:
         if getattr(self, "_ext", None) is None:
             self._ext = torch.cuda.ExternalStream(lib().ebd_ctx_stream(self.h), device=ts[0].device)
         self._ext.wait_stream(torch.cuda.current_stream(ts[0].device))
-        # and torch's caching allocator may not hand their memory out again before the work
-        # queued on the context stream by now (which reads or writes them) is done
-        for t in ts:
-            t.record_stream(self._ext)
+        # and the tensors stay referenced until the context's queued work is known done (sync,
+        # close): torch's caching allocator may not hand their memory out again before then.
+        # (record_stream on the context's stream would outlive it: ebd_ctx_destroy destroys it.)
+        self._held.extend(ts)
 
     def submit_device(self, events, lens, offs, payload, n, payload_bytes=None):
         """Device-resident batch (torch tensors on the context's device or raw pointers).
@@ -332,6 +335,7 @@ class Context:
 
     def sync(self):
         _check(lib().ebd_sync(self.h), "ebd_sync")
+        self._held = []
 
     def set_seq_base(self, seq):
         _check(lib().ebd_set_seq_base(self.h, seq), "ebd_set_seq_base")
@@ -432,7 +436,7 @@ class Context:
     def set_event_clock(self, times):
         """ebd_set_event_clock: per-event getCurrentTime readings (a device int64/uint64 tensor
         of the next batch's n events) or None.  The batch's kernels read it after submit
-        returns; _fence's record_stream keeps its memory from being reused before they ran."""
+        returns; _fence keeps it referenced until sync()."""
         self._ev_times = times
         if times is not None:
             self._fence(times)

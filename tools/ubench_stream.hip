@@ -11,6 +11,9 @@
 //            last window are shared with its neighbours)
 //   oct128   a lane per event; 8 lanes load 128-B line-aligned windows (one member's line per
 //            instruction: every instruction = 8 whole lines), 8x8 transpose, next line in flight
+//   oct128e  oct128 with event-relative windows (128 B from the event's 16-B aligned start:
+//            each spans two lines)
+//   +W       the same with the DFA's cost shape: 16 dependent LDS table steps per 16-B piece
 //   dma<L,D> L loader waves copy the workgroup's span into an LDS ring of 16-KiB slots by
 //            global_load_lds_dwordx4 (1 KiB per wave instruction), D slots in flight per
 //            loader; the other waves read each ready slot once (ds_read_b128) and free it
@@ -99,6 +102,29 @@ __device__ __forceinline__ void transpose_quad(v4u (&X)[4], uint32_t r) {
 		}
 }
 
+// The DFA's cost shape (WORK = 1): 16 dependent table steps per 16-B piece from a 128-column,
+// 196-row byte-major table in LDS (k_fresh's LdsTable layout), plus the running maximum.
+constexpr uint32_t kTabStride = 196, kTabBytes = 128 * kTabStride;
+__device__ __forceinline__ void load_tab(uint8_t* T) {
+	for (uint32_t k = threadIdx.x; k < kTabBytes; k += blockDim.x)
+		T[k] = (uint8_t)((k * 2654435761u) >> 24) % 190u;
+	__syncthreads();
+}
+template <int WORK>
+__device__ __forceinline__ void consume(const uint8_t* T, const v4u& v, uint32_t& s, uint32_t& acc) {
+	if (WORK) {
+#pragma unroll
+		for (int q = 0; q < 4; q++)
+#pragma unroll
+			for (int k = 0; k < 4; k++) {
+				s = T[min(__builtin_amdgcn_ubfe(v[q], 8 * k, 8), 127u) * kTabStride + s];
+				acc = max(acc, s);
+			}
+	} else {
+		acc ^= fold(v);
+	}
+}
+
 struct Ev {
 	uint32_t idx, L;
 	const uint8_t* p;
@@ -116,9 +142,14 @@ __device__ __forceinline__ Ev get_ev(const uint8_t* pay, const uint64_t* off, co
 	return e;
 }
 
+template <int WORK>
 __global__ __launch_bounds__(kThreads) void k_quad64(const uint8_t* pay, const uint64_t* off, const uint32_t* len, uint32_t n,
 		uint32_t* out) {
 	__shared__ uint32_t next;
+	__shared__ uint8_t T[WORK ? kTabBytes : 4];
+	if (WORK)
+		load_tab(T);
+	uint32_t s = 1;
 	uint32_t rb, re;
 	wg_range(n, rb, re);
 	if (threadIdx.x == 0)
@@ -161,7 +192,7 @@ __global__ __launch_bounds__(kThreads) void k_quad64(const uint8_t* pay, const u
 		if (valid) {
 #pragma unroll
 			for (int k = 0; k < 4; k++)
-				acc ^= fold(X[k]);
+				consume<WORK>(T, X[k], s, acc);
 			w0++;
 			if (w0 >= nwin) {
 				e0 = e1;
@@ -170,7 +201,7 @@ __global__ __launch_bounds__(kThreads) void k_quad64(const uint8_t* pay, const u
 			}
 		}
 	}
-	out[blockIdx.x * kThreads + threadIdx.x] = acc;
+	out[blockIdx.x * kThreads + threadIdx.x] = acc + s;
 }
 
 // ---- oct128: line-aligned 128-B windows, 8 lanes per instruction group ----
@@ -191,9 +222,14 @@ __device__ __forceinline__ void xstage(v4u (&X)[8], uint32_t r) {
 	}
 }
 
+template <int WORK, int LINE>
 __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const uint64_t* off, const uint32_t* len, uint32_t n,
 		uint32_t* out) {
 	__shared__ uint32_t next;
+	__shared__ uint8_t T[WORK ? kTabBytes : 4];
+	if (WORK)
+		load_tab(T);
+	uint32_t s = 1;
 	uint32_t rb, re;
 	wg_range(n, rb, re);
 	if (threadIdx.x == 0)
@@ -210,8 +246,9 @@ __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const u
 		e.idx = i;
 		if (i < re) {
 			const unsigned long long a = (unsigned long long)(uintptr_t)(pay + off[i]);
-			e.a0 = a & ~127ull;
-			e.nl = (uint32_t)(((a & 127ull) + len[i] + 127ull) >> 7);
+			const unsigned long long am = LINE ? 127ull : 15ull;
+			e.a0 = a & ~am;
+			e.nl = (uint32_t)(((a & am) + len[i] + 127ull) >> 7);
 		} else {
 			e.a0 = (unsigned long long)(uintptr_t)pay;
 			e.nl = 0;
@@ -250,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const u
 		if (valid) {
 #pragma unroll
 			for (int k = 0; k < 8; k++)
-				acc ^= fold(X[k]);
+				consume<WORK>(T, X[k], s, acc);
 			if (++w0 >= e0.nl) {
 				e0 = e1;
 				e1 = lev(atomicAdd(&next, 1u));
@@ -258,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const u
 			}
 		}
 	}
-	out[blockIdx.x * kThreads + threadIdx.x] = acc;
+	out[blockIdx.x * kThreads + threadIdx.x] = acc + s;
 }
 
 // quad64a: quad64 with 64-B windows aligned to 64 B (each a whole half line)
@@ -479,9 +516,13 @@ int main(int argc, char** argv) {
 	};
 	const dim3 g(cus), b(kThreads);
 	run("read", [&] { hipLaunchKernelGGL(k_read, g, b, 0, 0, dp, doff, dlen, n, dout); });
-	run("quad64", [&] { hipLaunchKernelGGL(k_quad64, g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("quad64", [&] { hipLaunchKernelGGL((k_quad64<0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("quad64a", [&] { hipLaunchKernelGGL(k_quad64a, g, b, 0, 0, dp, doff, dlen, n, dout); });
-	run("oct128", [&] { hipLaunchKernelGGL(k_oct128, g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("oct128", [&] { hipLaunchKernelGGL((k_oct128<0, 1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("oct128e", [&] { hipLaunchKernelGGL((k_oct128<0, 0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("quad64+W", [&] { hipLaunchKernelGGL((k_quad64<1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("oct128+W", [&] { hipLaunchKernelGGL((k_oct128<1, 1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("oct128e+W", [&] { hipLaunchKernelGGL((k_oct128<1, 0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("dma1x3", [&] { hipLaunchKernelGGL((k_dma<1, 3>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
 	run("dma2x2", [&] { hipLaunchKernelGGL((k_dma<2, 2>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
 	run("dma2x3", [&] { hipLaunchKernelGGL((k_dma<2, 3>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
