@@ -65,7 +65,13 @@ def _run(n, ev, ln, of, pay, keep=None):
         fin_total += int(fin.sum())
         cls_int += int((fin & (cls == ebd.CLASS_INTERNAL)).sum())
         cls_ext += int((fin & (cls == ebd.CLASS_EXTERNAL)).sum())
-        digests.append(hashlib.sha256(res.tobytes()).hexdigest())
+        # a session request's index into the cycle's request list is handed out by an atomic
+        # (its order is not part of the result): digest everything else
+        det = res.copy()
+        sess = (det["info"] & ebd.INFO_SESSION) != 0
+        for f in ("url_off", "url_len"):
+            det[f][sess] = 0
+        digests.append(hashlib.sha256(det.tobytes()).hexdigest())
         if keep is not None:
             sreq, sstr = ctx.session_requests()
             keep(c, a, z, res, sreq, sstr)
