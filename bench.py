@@ -389,6 +389,9 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, seed, args.cpu_seconds)
     peak_copy = copy_peak(dev)
+    # the measured read-stream peak: the faster of two read-only shapes
+    rb = ebd.read_bandwidth(local, 4 << 30, 10)
+    read_peak = max(rb.values())
     total_events = n_all * args.steps
     out = {
         "metric": "HTTP events parsed/s (device-resident)",
@@ -409,6 +412,8 @@ def main():
                                    else "1 GPU")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "measured_read_peak": read_peak, "frac_of_measured_read_peak": achieved / read_peak,
+                     "measured_read_shapes_gbps": rb,
                      "kernel": top, "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes,
                      "alg_bytes_def": "sum(consumed) + 40 B per data event (36-B DiscoveryEvent + 4-B length) + 36 B per "
                                       "close-only event" + (" (kernel time: all its launches in one step of %d poll "

@@ -143,6 +143,8 @@ _SIGS = {
     "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ebd_strerror": (C.c_char_p, [C.c_int]),
     "ebd_build_id": (C.c_char_p, []),
+    "ebd_measure_read_bandwidth": (C.c_int, [C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_double),
+                                             C.POINTER(C.c_double)]),
     "ebd_trace_size": (C.c_int, [C.POINTER(TraceConfig), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "ebd_trace_generate_host": (C.c_int, [C.POINTER(TraceConfig), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_uint64, C.c_void_p]),
@@ -187,6 +189,14 @@ def lib():
 
 def build_id():
     return lib().ebd_build_id().decode()
+
+
+def read_bandwidth(device=0, nbytes=4 << 30, reps=10):
+    """ebd_measure_read_bandwidth: the device's measured read-stream rates in GB/s,
+    {"plain": 16-B loads per lane, "dma": LDS-DMA tiles}."""
+    a, b = C.c_double(), C.c_double()
+    _check(lib().ebd_measure_read_bandwidth(device, nbytes, reps, C.byref(a), C.byref(b)), "ebd_measure_read_bandwidth")
+    return {"plain": a.value, "dma": b.value}
 
 
 class EbdError(RuntimeError):

@@ -406,6 +406,11 @@ int ebd_aggregate_requests(ebd_ctx* ctx, const ebd_request* reqs, uint32_t n, co
 
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
+/* The measured HBM read-stream peak of `device` over a `bytes` buffer (>= 16 MiB), `reps` timed
+ * passes each: plain 16-byte-per-lane loads and LDS-DMA (global_load_lds) tiles, in GB/s.  The
+ * roofline's second reference beside the 8 TB/s spec; allocates and frees its
+ * own buffer. */
+int ebd_measure_read_bandwidth(int device, uint64_t bytes, uint32_t reps, double* plain_gbps, double* dma_gbps);
 /* Hash of the sources this library was built from (profiles/ name the build they measured). */
 const char* ebd_build_id(void);
 

@@ -299,9 +299,14 @@ __global__ __launch_bounds__(kThreads) void k_oct128(const uint8_t* pay, const u
 }
 
 // quad64a: quad64 with 64-B windows aligned to 64 B (each a whole half line)
+template <int WORK>
 __global__ __launch_bounds__(kThreads) void k_quad64a(const uint8_t* pay, const uint64_t* off, const uint32_t* len, uint32_t n,
 		uint32_t* out) {
 	__shared__ uint32_t next;
+	__shared__ uint8_t T[WORK ? kTabBytes : 4];
+	if (WORK)
+		load_tab(T);
+	uint32_t s = 1;
 	uint32_t rb, re;
 	wg_range(n, rb, re);
 	if (threadIdx.x == 0)
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(kThreads) void k_quad64a(const uint8_t* pay, const 
 		if (valid) {
 #pragma unroll
 			for (int k = 0; k < 4; k++)
-				acc ^= fold(X[k]);
+				consume<WORK>(T, X[k], s, acc);
 			if (++w0 >= e0.nw) {
 				e0 = e1;
 				e1 = qev(atomicAdd(&next, 1u));
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(kThreads) void k_quad64a(const uint8_t* pay, const 
 			}
 		}
 	}
-	out[blockIdx.x * kThreads + threadIdx.x] = acc;
+	out[blockIdx.x * kThreads + threadIdx.x] = acc + s;
 }
 
 // ---- dma: LDS-DMA ring ----
@@ -517,10 +522,11 @@ int main(int argc, char** argv) {
 	const dim3 g(cus), b(kThreads);
 	run("read", [&] { hipLaunchKernelGGL(k_read, g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("quad64", [&] { hipLaunchKernelGGL((k_quad64<0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
-	run("quad64a", [&] { hipLaunchKernelGGL(k_quad64a, g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("quad64a", [&] { hipLaunchKernelGGL((k_quad64a<0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("oct128", [&] { hipLaunchKernelGGL((k_oct128<0, 1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("oct128e", [&] { hipLaunchKernelGGL((k_oct128<0, 0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("quad64+W", [&] { hipLaunchKernelGGL((k_quad64<1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
+	run("quad64a+W", [&] { hipLaunchKernelGGL((k_quad64a<1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("oct128+W", [&] { hipLaunchKernelGGL((k_oct128<1, 1>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("oct128e+W", [&] { hipLaunchKernelGGL((k_oct128<1, 0>), g, b, 0, 0, dp, doff, dlen, n, dout); });
 	run("dma1x3", [&] { hipLaunchKernelGGL((k_dma<1, 3>), g, b, 0, 0, dp, doff, dlen, n, dout, derr); });
