@@ -583,10 +583,9 @@ enum : uint32_t {
 	R_SRC,  // the source address (4 words): finalize classifies it (Aggregator.cpp:60-66, 85-88)
 	R_POS = R_SRC + 4, // ring position + 1 (checked by finalize)
 	R_TW,   // the 4 bytes the terminal tracker's rescan needs, from the scan lane's registers
-	R_CW,   // the same for the client-IP start tracker (when a client-IP value was seen)
 	R_WORDS
 };
-static_assert(R_WORDS == 22, "finalize record is 22 words");
+static_assert(R_WORDS == 21, "finalize record is 21 words");
 
 // Leading buffer bytes a scan lane stages (window 0), carried to finalize in LDS so that it
 // reads the request line and usually the Host header from LDS instead of reloading lines
@@ -604,16 +603,13 @@ struct StagedMem {
 	const uint8_t* p;
 	const uint32_t* s;
 	uint32_t lim;
-	uint32_t two, tw; // the words at buffer offsets two and cwo, carried in the record (R_TW, R_CW)
-	uint32_t cwo, cw;
+	uint32_t two, tw; // the word at buffer offset two, carried in the record (R_TW)
 	__device__ __forceinline__ uint32_t lds4(uint32_t o) const {
 		return __builtin_amdgcn_alignbyte(s[((o >> 2) + 1) * kFinLanes], s[(o >> 2) * kFinLanes], o & 3u);
 	}
 	__device__ __forceinline__ uint32_t ld4(uint32_t o) const {
 		if (o == two)
 			return tw;
-		if (o == cwo)
-			return cw;
 		if (o + 4 <= lim)
 			return lds4(o);
 		return *(const __attribute__((address_space(1))) u32a1*)(p + o);
@@ -669,9 +665,8 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 	// the terminal tracker's word travels in the record: it lies at the end of the request,
 	// past the staged bytes, where a reload from HBM cost one line per event
 	const uint32_t two = 16 * sr.term.c + 4 * flip_quarter<RS_TERM>(d.di, sr.term, 0);
-	const uint32_t cwo = sr.cseen ? 16 * sr.cip.c + 4 * flip_quarter<RS_CIP>(d.di, sr.cip, sr.cqm) : kNone;
-	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0,
-			StagedMem{p, fs, q[R_LIM], two, q[R_TW], cwo, q[R_CW]}, L, d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
+	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM], two, q[R_TW]}, L,
+			d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
 	if (fr.r.status == EBD_STATUS_FINISHED) {
 		d.keys[i] = fr.key;
 		if (!fr.cip) { // the client is the session's source address; a client-IP token is k_agg_fast's
@@ -782,7 +777,7 @@ void k_fresh(Dev d) {
 	LaneEv e0 = lane_ev(d, rb + sl, re);
 	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
 	uint32_t w0 = 0; // e0's window to scan next
-	uint32_t s = di.init, live = 0, cw = 0; // cw: the client-IP start tracker's word (R_CW)
+	uint32_t s = di.init, live = 0;
 	ScanRec sr;
 	rec_init(di, sr);
 
@@ -827,7 +822,6 @@ void k_fresh(Dev d) {
 			t[R_SRC + 3] = e0.src.w;
 			t[R_POS] = pos + 1;
 			t[R_TW] = tw;
-			t[R_CW] = cw;
 #pragma unroll
 			for (uint32_t f = 0; f < R_WORDS; f++)
 				sh.ring[f * kRing + slot] = t[f];
@@ -855,7 +849,6 @@ void k_fresh(Dev d) {
 		}
 		w0 = 0;
 		s = di.init;
-		cw = 0;
 		rec_init(di, sr);
 		live = e0.kind == EK_PARSE ? 1u : 0u;
 	};
@@ -922,12 +915,6 @@ void k_fresh(Dev d) {
 				const int ci = (int)(4 * w0 + k) - (int)e0.j0;
 				if (live && ci >= 0) {
 					const uint32_t c = (uint32_t)ci;
-					// the first chunk that reaches a client-IP value state holds the value's start:
-					// keep the word its rescan needs (it often lies past the staged bytes)
-					if (sr.cseen == 0 && m >= di.hvc0) {
-						const uint32_t qc = byte_of(qm, 0) >= di.hvc0 ? 0u : byte_of(qm, 1) >= di.hvc0 ? 1u : byte_of(qm, 2) >= di.hvc0 ? 2u : 3u;
-						cw = qc == 0 ? X[k].w[0] : qc == 1 ? X[k].w[1] : qc == 2 ? X[k].w[2] : X[k].w[3];
-					}
 					chunk_update(di, sr, c, s, qs, qm, m);
 					live = !st_terminal(di, sx) && 16 * (c + 1) < e0.L ? 1u : 0u;
 					s = sx;
