@@ -373,14 +373,17 @@ def main():
             merge_ms = (time.perf_counter() - tm) * 1e3
             where = "once after the timed steps (warm: the table of all steps), not in value"
         owned = ctx.stats()["services"]
-        tot = torch.tensor([n, owned, x["sent"], x["record_bytes"], x["string_bytes"]], dtype=torch.int64, device=dev)
+        tot = torch.tensor([n, owned, x["sent"], x["record_bytes"], x["string_bytes"], x["need_bytes"],
+                            x["string_bytes_one_round"]], dtype=torch.int64, device=dev)
         torch.distributed.all_reduce(tot)
         mt = torch.tensor([merge_ms], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(mt, op=torch.distributed.ReduceOp.MAX)
         n_all = int(tot[0])
         merge = {"merge_ms": float(mt.item()), "where": where, "services_merged": int(tot[1]),
                  "records_exchanged": int(tot[2]), "record_bytes_per_interval": int(tot[3]),
-                 "string_bytes_per_interval": int(tot[4]), "record_size": shard.REC.itemsize}
+                 "string_bytes_per_interval": int(tot[4]), "need_flag_bytes_per_interval": int(tot[5]),
+                 "string_bytes_if_one_round": int(tot[6]), "record_size": shard.REC.itemsize,
+                 "protocol": "two rounds: records, need flags back, endpoint bytes only for keys new to the owner"}
         if rank != 0:
             torch.distributed.destroy_process_group()
             return

@@ -56,6 +56,14 @@ hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsig
 hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
 		const unsigned long long* offs, hipStream_t st, int cus);
 hipError_t launch_agg_requests(const Dev& d, const ebd_request* rq, uint32_t n, const uint8_t* strings, hipStream_t st, int cus);
+hipError_t launch_merge_keys(const Dev& d, const ebd_wire_service* rec, uint32_t n, unsigned long long* dst, hipStream_t st, int cus);
+hipError_t launch_wire_bytes_needed(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		unsigned long long* nb, hipStream_t st, int cus);
+hipError_t launch_wire_compact(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* soff,
+		const unsigned long long* doff, const uint8_t* strings, unsigned long long strlen, uint8_t* out, unsigned long long outcap,
+		unsigned long long* ctr, hipStream_t st, int cus);
+hipError_t launch_merge_bytes(const Dev& d, const ebd_wire_service* rec, uint32_t n, const unsigned long long* dst,
+		const unsigned long long* offs, const uint8_t* strings, unsigned long long strlen, hipStream_t st, int cus);
 hipError_t launch_gen4_count(unsigned long long seed, uint32_t J, uint32_t* cnt, hipStream_t st);
 hipError_t launch_gen4_len(const GenTables* T, unsigned long long seed, uint32_t J, unsigned long long n, uint32_t align,
 		const uint32_t* stt, unsigned long long* alen, hipStream_t st);
@@ -1238,12 +1246,21 @@ int ebd_report_json(ebd_ctx* c, char* out, uint64_t cap, uint64_t* len) {
 	return ebd_format_services_json(svc.data(), n, str.data(), sl, out, cap, len);
 }
 
-// The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
-// are n entries, the scan's scratch is allocated on the stream.
-static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, unsigned long long* nb, unsigned long long* offs) {
-	hipError_t e = launch_wire_bytes(recs, n, nb, c->stream, c->cus);
-	if (e != hipSuccess)
-		return e;
+// Room to verify every merged record: each may race a claim.
+static int ensure_verify(ebd_ctx* c, uint32_t n) {
+	if (n <= c->verify_cap)
+		return 0;
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipFree(c->d_verify));
+	c->d_verify = nullptr;
+	HIP_TRY(hipMalloc(&c->d_verify, (size_t)n * sizeof(VerifyRec)));
+	c->verify_cap = n;
+	return 0;
+}
+
+// offs = the exclusive scan of nb (n entries); the scan's scratch is allocated on the stream.
+static hipError_t excl_scan(ebd_ctx* c, const unsigned long long* nb, unsigned long long* offs, uint32_t n) {
+	hipError_t e;
 	size_t tb = 0;
 	if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nb, offs, (int)n, c->stream)) != hipSuccess)
 		return e;
@@ -1253,6 +1270,13 @@ static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_
 	e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nb, offs, (int)n, c->stream);
 	const hipError_t f = hipFreeAsync(tmp, c->stream);
 	return e != hipSuccess ? e : f;
+}
+
+// The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
+// are n entries.
+static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, unsigned long long* nb, unsigned long long* offs) {
+	hipError_t e = launch_wire_bytes(recs, n, nb, c->stream, c->cus);
+	return e != hipSuccess ? e : excl_scan(c, nb, offs, n);
 }
 
 int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
@@ -1307,13 +1331,9 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
-	if (n > c->verify_cap) { // every merged record may race a claim: room to verify each
-		HIP_TRY(hipStreamSynchronize(c->stream));
-		HIP_TRY(hipFree(c->d_verify));
-		c->d_verify = nullptr;
-		HIP_TRY(hipMalloc(&c->d_verify, (size_t)n * sizeof(VerifyRec)));
-		c->verify_cap = n;
-	}
+	int rc = ensure_verify(c, n);
+	if (rc)
+		return rc;
 	Dev d = make_dev(c);
 	d.n = 0;
 	unsigned long long* tmp = nullptr; // nb, offs
@@ -1323,6 +1343,78 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_EVICTIONS, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_merge(d, recs, n, strings, strlen, tmp + n, c->stream, c->cus));
 	HIP_TRY(launch_verify(d, c->stream, c->cus));
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_merge_service_keys_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, uint64_t* dst) {
+	if (!c || (n && (!recs || !dst)))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (n == 0)
+		return 0;
+	int rc = ensure_verify(c, n);
+	if (rc)
+		return rc;
+	Dev d = make_dev(c);
+	d.n = 0;
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_merge_keys(d, recs, n, (unsigned long long*)dst, c->stream, c->cus));
+	HIP_TRY(launch_verify(d, c->stream, c->cus));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen,
+		const uint8_t* need, uint8_t* out, uint64_t outcap, uint64_t* out_len) {
+	if (!c || !out_len || (n && (!recs || !need || (!strings && strlen))))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	*out_len = 0;
+	if (n == 0)
+		return 0;
+	unsigned long long* tmp = nullptr; // nb, soff, nbn, doff
+	HIP_TRY(hipMallocAsync((void**)&tmp, 4 * (size_t)n * sizeof(unsigned long long), c->stream));
+	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
+	HIP_TRY(launch_wire_bytes_needed(recs, n, need, nullptr, tmp + 2 * (size_t)n, c->stream, c->cus));
+	HIP_TRY(excl_scan(c, tmp + 2 * (size_t)n, tmp + 3 * (size_t)n, n));
+	unsigned long long last[2] = {0, 0}; // the last record's needed bytes and offset: the total
+	HIP_TRY(hipMemcpyAsync(&last[0], tmp + 3 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(&last[1], tmp + 4 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	const uint64_t total = last[0] + last[1];
+	int rc = 0;
+	if (out) {
+		if (total > outcap)
+			rc = -ENOSPC;
+		else
+			HIP_TRY(launch_wire_compact(recs, n, need, tmp + n, tmp + 3 * (size_t)n, strings, strlen, out, outcap, c->d_ctr, c->stream,
+					c->cus));
+	}
+	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	*out_len = total;
+	return rc;
+}
+
+int ebd_merge_service_bytes_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint64_t* dst, const uint8_t* strings,
+		uint64_t strlen) {
+	if (!c || (n && (!recs || !dst || (!strings && strlen))))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	if (n == 0)
+		return 0;
+	Dev d = make_dev(c);
+	d.n = 0;
+	unsigned long long* tmp = nullptr; // nb, offs
+	HIP_TRY(hipMallocAsync((void**)&tmp, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_wire_bytes_needed(recs, n, nullptr, (const unsigned long long*)dst, tmp, c->stream, c->cus));
+	HIP_TRY(excl_scan(c, tmp, tmp + n, n));
+	HIP_TRY(launch_merge_bytes(d, recs, n, (const unsigned long long*)dst, tmp + n, strings, strlen, c->stream, c->cus));
 	HIP_TRY(hipFreeAsync(tmp, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;

@@ -507,10 +507,37 @@ struct LaneEv {
 	v4u src;          // the session's source address (DiscoverySockSourceIP), classified by finalize
 };
 
-__device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end) {
-	LaneEv e;
-	e.idx = i;
+// The next event as loaded: its words stay in flight until the lane first needs the event
+// (lane_ev), one or more windows later, so taking a new event never waits for memory.
+struct LaneRaw {
+	uint32_t idx, pf, flags, len; // flags bit 8: past the workgroup's range
+	unsigned long long off;
+	v4u src;
+};
+
+__device__ __forceinline__ LaneRaw lane_load(const Dev& d, uint32_t i, uint32_t end) {
+	LaneRaw r;
+	r.idx = i;
 	if (i >= end) {
+		r.pf = r.len = 0;
+		r.flags = 0x100u;
+		r.off = 0;
+		r.src = v4u{0u, 0u, 0u, 0u};
+		return r;
+	}
+	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	r.flags = evb[32];
+	r.pf = *(const uint32_t*)evb;
+	r.src = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // 4-byte aligned, beside pid and flags
+	r.len = d.len[i];
+	r.off = d.off[i];
+	return r;
+}
+
+__device__ __forceinline__ LaneEv lane_ev(const Dev& d, const LaneRaw& r) {
+	LaneEv e;
+	e.idx = r.idx;
+	if (r.flags & 0x100u) {
 		e.kind = EK_NONE;
 		e.L = 0;
 		e.pf = e.flags = 0;
@@ -520,13 +547,12 @@ __device__ __forceinline__ LaneEv lane_ev(const Dev& d, uint32_t i, uint32_t end
 		e.src = v4u{0u, 0u, 0u, 0u};
 		return e;
 	}
-	const uint8_t* evb = (const uint8_t*)(d.ev + i);
-	const uint32_t flags = evb[32];
-	e.pf = *(const uint32_t*)evb;
-	e.src = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // 4-byte aligned, beside pid and flags
+	const uint32_t flags = r.flags;
+	e.pf = r.pf;
+	e.src = r.src;
 	e.flags = flags;
-	const uint32_t L = d.len[i];
-	const uint64_t off = d.off[i];
+	const uint32_t L = r.len;
+	const uint64_t off = r.off;
 	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : !buf_in(d, L, off) ? EK_BAD : EK_PARSE;
 	e.L = e.kind == EK_PARSE ? L : 0;
 	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
@@ -774,8 +800,8 @@ void k_fresh(Dev d) {
 	uint32_t* stg = sh.stage + sl;        // this lane's staging row (word j at stg[j * kScanLanes])
 	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
 	// the lane's current event (e0) and the next one (e1, whose record arrives early)
-	LaneEv e0 = lane_ev(d, rb + sl, re);
-	LaneEv e1 = lane_ev(d, rb + kScanLanes + sl, re);
+	LaneEv e0 = lane_ev(d, lane_load(d, rb + sl, re));
+	LaneRaw e1 = lane_load(d, rb + kScanLanes + sl, re);
 	uint32_t w0 = 0; // e0's window to scan next
 	uint32_t s = di.init, live = 0;
 	ScanRec sr;
@@ -844,8 +870,8 @@ void k_fresh(Dev d) {
 			} else {
 				break;
 			}
-			e0 = e1;
-			e1 = lane_ev(d, grab(), re);
+			e0 = lane_ev(d, e1);
+			e1 = lane_load(d, grab(), re);
 		}
 		w0 = 0;
 		s = di.init;
@@ -890,7 +916,8 @@ void k_fresh(Dev d) {
 			} else if (w0 + 1 < nwin(e0)) {
 				na = e0.base, nl = e0.lastp, ni = e0.idx, nw = w0 + 1;
 			} else {
-				na = e1.base, nl = e1.lastp, ni = e1.idx, nw = 0;
+				const LaneEv n1 = lane_ev(d, e1);
+				na = n1.base, nl = n1.lastp, ni = n1.idx, nw = 0;
 			}
 			issue(na, nl, nw);
 			tidx = ni;
@@ -934,8 +961,8 @@ void k_fresh(Dev d) {
 		}
 		push(done, tw);
 		if (done) {
-			e0 = e1;
-			e1 = lane_ev(d, grab(), re);
+			e0 = lane_ev(d, e1);
+			e1 = lane_load(d, grab(), re);
 			resolve();
 		}
 	}
@@ -2553,6 +2580,96 @@ __global__ void k_merge(Dev d, const ebd_wire_service* rec, uint32_t n, const ui
 	}
 }
 
+// Two-round merge (ebd_merge_service_keys_device / ebd_merge_service_bytes_device): the key
+// round inserts the records as k_merge does, but the claimer of a new service only reserves
+// its list entry and arena bytes: dst[k] = the reserved arena offset (~0: record k's bytes are
+// not needed, the owner already has the key or the source had none).  The sources then send
+// the bytes of exactly the records with dst != ~0 (k_wire_compact), in record order, and
+// k_merge_bytes copies them to their reserved places.
+__global__ void k_merge_keys(Dev d, const ebd_wire_service* rec, uint32_t n, unsigned long long* dst) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const ebd_wire_service v = rec[k];
+		const uint32_t len = v.endpoint_len & ~EBD_WIRE_NO_BYTES;
+		unsigned long long at = ~0ull;
+		if (len > 0xffffu) { // not what an export writes
+			set_error(d, EBD_ERR_INTERNAL);
+			dst[k] = at;
+			continue;
+		}
+		bool claimed;
+		const uint32_t slot = agg_insert(d, Hash128{v.key_lo, v.key_hi}, v.first, v.internal_clients, v.external_clients, &claimed);
+		if (claimed) {
+			const unsigned long long list_at = atomicAdd(&d.ctr[CTR_SERVICES], 1ull);
+			if (list_at >= d.new_cap) {
+				set_error(d, EBD_ERR_TABLE_FULL);
+			} else {
+				if (v.endpoint_len & EBD_WIRE_NO_BYTES) {
+					set_error(d, EBD_ERR_ARENA_FULL); // the source had no bytes: none here either
+				} else {
+					const unsigned long long ep = atomicAdd(&d.ctr[CTR_SARENA], (unsigned long long)((len + 7u) & ~7u));
+					if (ep + len <= d.sarena_cap)
+						at = ep;
+					else
+						set_error(d, EBD_ERR_ARENA_FULL);
+				}
+				d.new_slots[list_at] = slot;
+				d.list_ep[list_at] = at;
+				d.list_pl[list_at] = (unsigned long long)v.pid | ((unsigned long long)len << 32);
+			}
+		}
+		dst[k] = at;
+	}
+}
+
+// Bytes each record sends in the bytes round: its endpoint's (8-padded) when needed, else 0.
+__global__ void k_wire_bytes_needed(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		unsigned long long* nb) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const bool on = need ? need[k] != 0 : dst[k] != ~0ull;
+		nb[k] = on ? EBD_WIRE_BYTES(rec[k].endpoint_len) : 0ull;
+	}
+}
+
+// Source side: the needed records' bytes (at soff[k] in the export's strings) packed in record
+// order at doff[k] (the scan of k_wire_bytes_needed).
+__global__ void k_wire_compact(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* soff,
+		const unsigned long long* doff, const uint8_t* strings, unsigned long long strlen, uint8_t* out, unsigned long long outcap,
+		unsigned long long* ctr) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		if (!need[k])
+			continue;
+		const uint32_t nb = EBD_WIRE_BYTES(rec[k].endpoint_len);
+		if (soff[k] + nb > strlen || doff[k] + nb > outcap) {
+			atomicOr(&ctr[CTR_ERRORS], (unsigned long long)EBD_ERR_INTERNAL);
+			continue;
+		}
+		const unsigned long long* src = (const unsigned long long*)(strings + soff[k]);
+		unsigned long long* o = (unsigned long long*)(out + doff[k]);
+		for (uint32_t b = 0; b < nb / 8; b++)
+			o[b] = src[b];
+	}
+}
+
+// Owner side: received bytes (at offs[k], the scan of k_wire_bytes_needed over dst) to the
+// arena offsets the key round reserved.
+__global__ void k_merge_bytes(Dev d, const ebd_wire_service* rec, uint32_t n, const unsigned long long* dst, const unsigned long long* offs,
+		const uint8_t* strings, unsigned long long strlen) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const unsigned long long at = dst[k];
+		if (at == ~0ull)
+			continue;
+		const uint32_t nb = EBD_WIRE_BYTES(rec[k].endpoint_len);
+		if (offs[k] + nb > strlen || at + nb > d.sarena_cap + 64) {
+			set_error(d, EBD_ERR_INTERNAL);
+			continue;
+		}
+		const unsigned long long* src = (const unsigned long long*)(strings + offs[k]);
+		unsigned long long* o = (unsigned long long*)(d.sarena + at);
+		for (uint32_t b = 0; b < nb / 8; b++)
+			o[b] = src[b];
+	}
+}
+
 // service::Aggregator::newRequest (Aggregator.cpp:155-168) for requests parsed elsewhere
 // (ebd_aggregate_requests): the service key over (pid, host + url), the client class of
 // clientIp.front() or of the session's source address (Aggregator.cpp:50-88), the
@@ -2861,6 +2978,27 @@ hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsig
 }
 hipError_t launch_agg_requests(const Dev& d, const ebd_request* rq, uint32_t n, const uint8_t* strings, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_agg_requests, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rq, n, strings);
+	return hipGetLastError();
+}
+hipError_t launch_merge_keys(const Dev& d, const ebd_wire_service* rec, uint32_t n, unsigned long long* dst, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_merge_keys, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n, dst);
+	return hipGetLastError();
+}
+hipError_t launch_wire_bytes_needed(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		unsigned long long* nb, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_bytes_needed, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, need, dst, nb);
+	return hipGetLastError();
+}
+hipError_t launch_wire_compact(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* soff,
+		const unsigned long long* doff, const uint8_t* strings, unsigned long long strlen, uint8_t* out, unsigned long long outcap,
+		unsigned long long* ctr, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_compact, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, need, soff, doff, strings, strlen, out,
+			outcap, ctr);
+	return hipGetLastError();
+}
+hipError_t launch_merge_bytes(const Dev& d, const ebd_wire_service* rec, uint32_t n, const unsigned long long* dst,
+		const unsigned long long* offs, const uint8_t* strings, unsigned long long strlen, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_merge_bytes, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, d, rec, n, dst, offs, strings, strlen);
 	return hipGetLastError();
 }
 hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,

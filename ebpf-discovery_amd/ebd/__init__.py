@@ -139,6 +139,10 @@ _SIGS = {
     "ebd_export_services_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.c_void_p, C.c_void_p]),
     "ebd_merge_services_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "ebd_merge_service_keys_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "ebd_wire_compact_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                          C.c_uint64, C.POINTER(C.c_uint64)]),
+    "ebd_merge_service_bytes_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]),
     "ebd_aggregate_requests": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "ebd_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "ebd_strerror": (C.c_char_p, [C.c_int]),
@@ -501,6 +505,49 @@ class Context:
         _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
                                                C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                strings.numel()), "ebd_merge_services_device")
+
+    def merge_service_keys_device(self, recs, dst):
+        """Key round of the two-round merge: wire records (device uint8 tensor) into this
+        table; dst (device int64 tensor, one per record) gets the arena offset reserved for
+        each record whose bytes are needed, -1 for the others."""
+        n = recs.numel() // WIRE_DTYPE.itemsize
+        assert dst.dtype == __import__("torch").int64 and dst.numel() == n
+        if n == 0:
+            return
+        self._fence(recs, dst)
+        _check(lib().ebd_merge_service_keys_device(self.h, C.c_void_p(recs.data_ptr()), n, C.c_void_p(dst.data_ptr())),
+               "ebd_merge_service_keys_device")
+
+    def wire_compact_device(self, recs, strings, need):
+        """Source side of the bytes round: the endpoint bytes of the exported records whose
+        need byte is set, packed in record order (a device uint8 tensor)."""
+        import torch
+        n = recs.numel() // WIRE_DTYPE.itemsize
+        assert need.dtype == torch.uint8 and need.numel() == n
+        if n == 0:
+            return torch.empty(0, dtype=torch.uint8, device=recs.device)
+        self._fence(recs, strings, need)
+        ln = C.c_uint64(0)
+        sp = C.c_void_p(strings.data_ptr()) if strings.numel() else None
+        _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
+                                             C.c_void_p(need.data_ptr()), None, 0, C.byref(ln)), "ebd_wire_compact_device")
+        out = torch.empty(max(int(ln.value), 8), dtype=torch.uint8, device=recs.device)
+        self._fence(out)
+        _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
+                                             C.c_void_p(need.data_ptr()), C.c_void_p(out.data_ptr()), out.numel(),
+                                             C.byref(ln)), "ebd_wire_compact_device")
+        return out[:int(ln.value)]
+
+    def merge_service_bytes_device(self, recs, dst, strings):
+        """Bytes round of the two-round merge: the received bytes (device uint8, in the order
+        of the records with dst >= 0, readable 8 bytes past their end) to their places."""
+        n = recs.numel() // WIRE_DTYPE.itemsize
+        if n == 0:
+            return
+        self._fence(recs, dst, strings)
+        _check(lib().ebd_merge_service_bytes_device(self.h, C.c_void_p(recs.data_ptr()), n, C.c_void_p(dst.data_ptr()),
+                                                    C.c_void_p(strings.data_ptr()) if strings.numel() else None,
+                                                    strings.numel()), "ebd_merge_service_bytes_device")
 
     def aggregate_requests(self, reqs):
         """ebd_aggregate_requests: Aggregator::newRequest for requests parsed elsewhere, in order.

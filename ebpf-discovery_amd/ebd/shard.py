@@ -14,6 +14,11 @@ collective.  The one exchange is at the end, the Aggregator merge:
     of endpoint bytes ship each service to its owner, over RCCL (xGMI) on GPU tensors.  A
     record's bytes follow the previous record's (8-byte padded), so the received segments
     concatenate into one addressable table with no offsets to rebase;
+  * endpoint bytes cross once per key the owner lacks (two rounds): the records go first,
+    alone; the owner merges them (its own records first) and answers each source with one
+    byte per record, set where that record created a service whose bytes it needs; the
+    sources then send exactly those records' bytes (ebd_merge_service_keys_device,
+    ebd_wire_compact_device, ebd_merge_service_bytes_device);
   * the owner merges on the device (ebd_merge_services_device): counters add modulo 2^32
     (Service.h:53-54 are uint32), the earliest first request fixes domain and scheme
     (Aggregator.cpp:155-168: the first request of a key creates the service, later ones
@@ -249,18 +254,96 @@ def exchange(recs, strings, counts, scounts, group=None):
     return out_r, out_s
 
 
-def exchange_merge(table, device="cpu", group=None):
+def exchange_merge(table, device="cpu", group=None, two_round=True, stats=None):
     """CPU path: owner-partitioned exchange of a ServiceTable, merged by the numpy rule on
-    each owner.  Returns this rank's owned part of the merged table."""
+    each owner.  Returns this rank's owned part of the merged table.  two_round: the key
+    round, the owner's need flags, then only the needed bytes (device_exchange_merge's
+    protocol, with claimers() in place of the device claims); stats gets the bytes sent."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
     rec, strings, counts, scounts = table.merged().to_wire(world)
     r = torch.from_numpy(rec.view(np.uint8).reshape(-1).copy()).to(device)
-    s = torch.from_numpy(strings.copy()).to(device)
-    out_r, out_s = exchange(r, s, counts, scounts, group)
-    mine = ServiceTable.from_wire(out_r.cpu().numpy().view(REC).copy(), out_s.cpu().numpy()[:out_s.numel() - STR_SLACK])
-    return mine.merged().packed()
+    if not two_round:
+        s = torch.from_numpy(strings.copy()).to(device)
+        out_r, out_s = exchange(r, s, counts, scounts, group)
+        mine = ServiceTable.from_wire(out_r.cpu().numpy().view(REC).copy(), out_s.cpu().numpy()[:out_s.numel() - STR_SLACK])
+        if stats is not None:
+            stats.update(record_bytes=rec.nbytes, string_bytes=int(strings.size), need_bytes=0)
+        return mine.merged().packed()
+    out_r, rc = exchange_counts(r, counts, REC.itemsize, group)
+    got = out_r.cpu().numpy().view(REC).copy()
+    need = claimers(got, rc, rank)
+    back, _ = exchange_counts(torch.from_numpy(need.astype(np.uint8)).to(device), rc, 1, group)
+    mask = back.cpu().numpy().astype(bool)
+    nb = wire_bytes(rec["endpoint_len"])
+    soff = np.zeros(nb.size, np.int64)
+    soff[1:] = np.cumsum(nb.astype(np.int64))[:-1]
+    sel = np.flatnonzero(mask)
+    sent = np.concatenate([strings[soff[k]:soff[k] + int(nb[k])] for k in sel]) if sel.size else np.zeros(0, np.uint8)
+    owner = np.repeat(np.arange(world), counts.astype(np.int64))
+    bc = np.bincount(owner[sel], weights=nb[sel].astype(np.float64), minlength=world).astype(np.int64)
+    out_s, _ = exchange_counts(torch.from_numpy(sent.astype(np.uint8)).to(device), bc, 1, group)
+    if stats is not None:
+        stats.update(record_bytes=rec.nbytes, string_bytes=int(sent.size), need_bytes=int(need.size),
+                     string_bytes_one_round=int(strings.size))
+    return merged_with_bytes(got, need, out_s.cpu().numpy())
+
+
+def claimers(w, rc, rank):
+    """The records whose bytes an owner asks for (received records w, rc[s] from source s in
+    source order): per key, the first record that has bytes, the owner's own records first,
+    then in source order.  The device path claims in the same spirit (own records merged
+    first); which sender's copy it takes does not matter, every copy of a key is the same."""
+    n = w.size
+    need = np.zeros(n, np.uint8)
+    if n == 0:
+        return need
+    starts = np.concatenate([[0], np.cumsum(rc)[:-1]]).astype(np.int64)
+    pref = np.ones(n, np.int64)
+    pref[starts[rank]:starts[rank] + int(rc[rank])] = 0
+    has = (w["endpoint_len"] & np.uint32(WIRE_NO_BYTES)) == 0
+    order = np.lexsort((np.arange(n), pref, ~has, w["key_hi"], w["key_lo"]))
+    kl, kh = w["key_lo"][order], w["key_hi"][order]
+    head = np.ones(n, bool)
+    head[1:] = (kl[1:] != kl[:-1]) | (kh[1:] != kh[:-1])
+    first = order[head]
+    need[first[has[first]]] = 1
+    return need
+
+
+def merged_with_bytes(w, need, strings):
+    """The owner's table from received records and the bytes of the needed ones (in record
+    order): one record per key, counters summed mod 2^32, the earliest first request's fields,
+    the endpoint from whichever record carried it, the domain from the earliest host length."""
+    nb = wire_bytes(w["endpoint_len"]) * need.astype(np.uint64)
+    offs = np.zeros(w.size, np.uint64)
+    if w.size:
+        offs[1:] = np.cumsum(nb)[:-1]
+    t = ServiceTable.from_wire(w, np.zeros(0, np.uint8))
+    r = t.rec
+    r["endpoint_off"] = np.where(need.astype(bool), offs, NO_OFF)
+    if r.size == 0:
+        return ServiceTable(r, np.zeros(0, np.uint8))
+    order = np.lexsort((r["first_seq"], r["key_hi"], r["key_lo"]))
+    r = r[order]
+    head = np.ones(r.size, bool)
+    head[1:] = (r["key_lo"][1:] != r["key_lo"][:-1]) | (r["key_hi"][1:] != r["key_hi"][:-1])
+    starts = np.flatnonzero(head)
+    out = r[starts].copy()
+    for f in ("internal", "external"):
+        out[f] = (np.add.reduceat(r[f].astype(np.uint64), starts) & M32).astype(np.uint32)
+    out["endpoint_off"] = np.minimum.reduceat(r["endpoint_off"], starts)  # the one carried copy (NO_OFF: none)
+    s = strings.tobytes()
+    for k in range(out.size):
+        o = out["endpoint_off"][k]
+        if o == NO_OFF:
+            out["domain_off"][k] = out["domain_len"][k] = 0
+            continue
+        o = int(o)
+        hl = min(int(out["host_len"][k]), int(out["endpoint_len"][k]))
+        out["domain_off"][k], out["domain_len"][k] = host_domain(s[o:o + hl])
+    return ServiceTable(out, np.frombuffer(s, np.uint8).copy() if s else np.zeros(0, np.uint8)).packed()
 
 
 def gather_rows(table, group=None):
@@ -274,16 +357,19 @@ def gather_rows(table, group=None):
     return rows
 
 
-def device_exchange_merge(ctx, device, group=None, map_first=None):
+def device_exchange_merge(ctx, device, group=None, map_first=None, two_round=True):
     """GPU path: export by owner on the device, exchange over RCCL, merge on the device into
-    this rank's context (reset first).  With network counters the services' network-map
+    this rank's context (reset first).  two_round (default): records alone, the owner's need
+    flags back, then only the needed endpoint bytes (module docstring); else one round of
+    records and every record's bytes.  With network counters the services' network-map
     entries follow their services to the owner (one more all_to_all of 32-byte records) and
     merge into its maps (union, later last-seen time).  map_first(first_seq int64 tensor) ->
     trace positions, applied before the exchange.  Returns {sent, received, record_bytes,
-    string_bytes, net_sent, net_received}: this rank's records out and in, and the bytes it
-    sent."""
+    string_bytes, need_bytes, string_bytes_one_round, net_sent, net_received}: this rank's
+    records out and in, and the bytes it sent."""
+    import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
     check_same_hash_key(ctx, device, group)
     recs, strs, counts, scounts = ctx.export_services_device(world, device)
     if map_first is not None:
@@ -291,17 +377,54 @@ def device_exchange_merge(ctx, device, group=None, map_first=None):
     nets = ncounts = None
     if getattr(ctx, "network_counters", False):
         nets, ncounts = group_by_owner(ctx.networks_device(device), NET_REC_BYTES, world)
-    out_r, out_s = exchange(recs, strs, counts, scounts, group)
-    ctx.reset_services()
-    ctx.merge_services_device(out_r, out_s)
+    if not two_round:
+        out_r, out_s = exchange(recs, strs, counts, scounts, group)
+        ctx.reset_services()
+        ctx.merge_services_device(out_r, out_s)
+        sent_bytes, need_bytes = strs.numel(), 0
+    else:
+        out_r, rc = exchange_counts(recs, counts, REC.itemsize, group)
+        ctx.reset_services()
+        n_in = out_r.numel() // REC.itemsize
+        dst = torch.empty(n_in, dtype=torch.int64, device=device)
+        a = int(np.sum(rc[:rank]))
+        b = a + int(rc[rank])
+        rb = REC.itemsize
+        # the owner's own records first: they create its services, and their bytes stay local
+        ctx.merge_service_keys_device(out_r[a * rb:b * rb], dst[a:b])
+        ctx.merge_service_keys_device(out_r[:a * rb], dst[:a])
+        ctx.merge_service_keys_device(out_r[b * rb:], dst[b:])
+        need_in = (dst >= 0).to(torch.uint8)
+        need, _ = exchange_counts(need_in, rc, 1, group)  # one flag per record this rank sent
+        sbytes = ctx.wire_compact_device(recs, strs, need)
+        bc = owner_byte_counts(recs, need, counts, world)
+        out_s, _ = exchange_counts(sbytes, bc, 1, group, slack=STR_SLACK)
+        ctx.merge_service_bytes_device(out_r, dst, out_s)
+        sent_bytes, need_bytes = sbytes.numel(), need_in.numel()
     out_n = None
     if nets is not None:
         out_n = exchange_fixed(nets, ncounts, NET_REC_BYTES, group)
         ctx.merge_networks_device(out_n)
     return {"sent": int(counts.sum()), "received": out_r.numel() // REC.itemsize,
-            "record_bytes": recs.numel(), "string_bytes": strs.numel(),
+            "record_bytes": recs.numel(), "string_bytes": sent_bytes, "need_bytes": need_bytes,
+            "string_bytes_one_round": strs.numel(),
             "net_sent": int(ncounts.sum()) if ncounts is not None else 0,
             "net_received": out_n.numel() // NET_REC_BYTES if out_n is not None else 0}
+
+
+def owner_byte_counts(recs, need, counts, world):
+    """Per owner, the endpoint bytes of the needed records (device wire records grouped by
+    owner, counts[w] each; need: one uint8 flag per record) as a numpy int64 array."""
+    import torch
+    n = recs.numel() // REC.itemsize
+    if n == 0:
+        return np.zeros(world, np.int64)
+    ln = recs.view(torch.int32).view(n, REC.itemsize // 4)[:, 9].to(torch.int64) & 0xFFFFFFFF  # endpoint_len
+    nb = torch.where((ln & WIRE_NO_BYTES) != 0, torch.zeros_like(ln), (ln + 7) & ~7) * need.to(torch.int64)
+    own = torch.repeat_interleave(torch.arange(world, device=recs.device),
+                                  torch.tensor(np.asarray(counts, np.int64), device=recs.device))
+    bc = torch.zeros(world, dtype=torch.int64, device=recs.device).index_add_(0, own, nb)
+    return bc.cpu().numpy()
 
 
 NET_REC_BYTES = 32  # ebd_service_net
@@ -330,6 +453,23 @@ def group_by_owner(recs, size, world):
     order = torch.argsort(own, stable=True)
     out = recs.view(n, size)[order].reshape(-1)
     return out, torch.bincount(own, minlength=world).cpu().numpy().astype(np.int64)
+
+
+def exchange_counts(recs, counts, size, group=None, slack=0):
+    """exchange_fixed that also returns the counts received from each source (numpy int64);
+    the output has `slack` zero bytes past the received ones."""
+    import torch
+    import torch.distributed as dist
+    dev = recs.device
+    sizes = torch.tensor(np.asarray(counts, np.int64), device=dev)
+    rsizes = torch.empty_like(sizes)
+    dist.all_to_all_single(rsizes, sizes, group=group)
+    rc = rsizes.cpu().numpy().astype(np.int64)
+    nout = int(rc.sum()) * size
+    out = torch.zeros(nout + slack, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(out[:nout], recs, output_split_sizes=[int(c) * size for c in rc],
+                           input_split_sizes=[int(c) * size for c in counts], group=group)
+    return (out if slack else out[:nout]), rc
 
 
 def exchange_fixed(recs, counts, size, group=None):

@@ -381,6 +381,22 @@ int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_wire_service* r
  * and reported as EBD_ERR_INTERNAL. */
 int ebd_merge_services_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings,
 		uint64_t strlen);
+/* The same merge in two rounds, so that endpoint bytes cross the fabric once per key the owner
+ * lacks ("ship endpoint strings once per new key"), not once per sender:
+ *  1. keys: the owner merges the records alone (counters, first word) into its table.  A record
+ *     that creates a service reserves the service's arena bytes: dst[k] (DEVICE, n entries) =
+ *     the reserved offset, or ~0 when record k's bytes are not needed (the key was there, or
+ *     the source had none).  Merge the owner's own records first and theirs are the creators.
+ *  2. the owner returns need[k] = (dst[k] != ~0) to each record's source;
+ *     ebd_wire_compact_device packs the bytes of the needed records (need: DEVICE, one byte per
+ *     exported record) in record order; out == NULL: *out_len only;
+ *  3. ebd_merge_service_bytes_device copies the received bytes (in the order of the records
+ *     with dst != ~0, readable 8 bytes past strlen) to the reserved places. */
+int ebd_merge_service_keys_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, uint64_t* dst);
+int ebd_wire_compact_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen,
+		const uint8_t* need, uint8_t* out, uint64_t outcap, uint64_t* out_len);
+int ebd_merge_service_bytes_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint64_t* dst,
+		const uint8_t* strings, uint64_t strlen);
 /* --- requests parsed elsewhere (service::Aggregator::newRequest, Aggregator.h:56) -------
  * One httpparser::HttpRequest with its DiscoverySessionMeta (Aggregator.h:40-44): what
  * Aggregator::newRequest reads of them (Aggregator.cpp:44-130, 155-168).  Its strings lie at

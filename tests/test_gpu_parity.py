@@ -267,6 +267,73 @@ def test_device_export_by_owner_and_merge_equals_whole_trace():
         assert rows == want
 
 
+def test_device_two_round_merge_ships_bytes_once_per_new_key():
+    """The two-round merge's device half on one GPU (what device_exchange_merge runs across
+    GPUs): W shard contexts export by owner; each owner merges its own records' keys first,
+    then the others' (ebd_merge_service_keys_device); the need flags go back to the sources,
+    which pack just those records' bytes (ebd_wire_compact_device); the owner copies them in
+    (ebd_merge_service_bytes_device).  The owners' tables equal the oracle over the whole trace,
+    and fewer endpoint bytes move than the one-round export holds."""
+    import torch
+    from ebd import shard
+    dev = torch.device("cuda:0")
+    W = 3
+    ev, lens, offs, payload = ebd.generate_host(3, 21, 0, 30000)
+    src = []  # per shard: (ctx, recs, strs, counts)
+    for idx in shard.shard_indices(ev, W):
+        ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size, hash_key=ebd.TEST_HASH_KEY)
+        ctx.submit(ev[idx], lens[idx], offs[idx], payload)
+        recs, strs, counts, scounts = ctx.export_services_device(W, dev)
+        gpos = torch.tensor(idx.astype(np.int64), device=dev)
+        shard.map_wire_first(recs, lambda f: gpos[f])
+        src.append((ctx, recs, strs, counts))
+    RB = shard.REC.itemsize
+
+    def seg(s, w):  # source s's records for owner w
+        c = src[s][3].astype(np.int64)
+        a = int(c[:w].sum())
+        return src[s][1][a * RB:(a + int(c[w])) * RB]
+
+    owners, need_for = [], [[None] * W for _ in range(W)]
+    for w in range(W):
+        m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY)
+        parts = [seg(s, w) for s in range(W)]
+        dsts = [torch.empty(p.numel() // RB, dtype=torch.int64, device=dev) for p in parts]
+        for s in [w] + [s for s in range(W) if s != w]:  # the owner's own records first
+            m.merge_service_keys_device(parts[s], dsts[s])
+        for s in range(W):
+            need_for[s][w] = (dsts[s] >= 0).to(torch.uint8)
+            if s != w:  # a key the owner had is never asked of another shard
+                own_keys = set(map(tuple, parts[w].view(torch.int64).view(-1, 5)[:, :2].cpu().numpy().tolist()))
+                keys = parts[s].view(torch.int64).view(-1, 5)[:, :2].cpu().numpy().tolist()
+                asked = need_for[s][w].cpu().numpy()
+                assert not any(a and tuple(k) in own_keys for a, k in zip(asked, keys))
+        owners.append((m, parts, dsts))
+    sent = 0
+    got = [[] for _ in range(W)]
+    for s in range(W):
+        ctx, recs, strs, counts = src[s]
+        need = torch.cat([need_for[s][w] for w in range(W)])
+        packed = ctx.wire_compact_device(recs, strs, need)
+        bc = shard.owner_byte_counts(recs, need, counts, W)
+        assert int(bc.sum()) == packed.numel()
+        sent += packed.numel()
+        a = 0
+        for w in range(W):
+            got[w].append(packed[a:a + int(bc[w])])
+            a += int(bc[w])
+    rows = []
+    for w, (m, parts, dsts) in enumerate(owners):
+        strs = torch.cat(got[w] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8, device=dev)])
+        m.merge_service_bytes_device(torch.cat(parts), torch.cat(dsts), strs)
+        assert m.stats()["errors"] == 0
+        rows += m.services()
+    rows.sort(key=lambda t: (t[0], t[1]))
+    _, want, _ = run_oracle(ev, lens, offs, payload)
+    assert rows == want
+    assert 0 < sent < sum(src[s][2].numel() for s in range(W))
+
+
 def test_device_exchange_merge_over_rccl_world1():
     """shard.device_exchange_merge end to end through RCCL (a world-1 nccl group): export,
     all_to_all_single on GPU tensors, device merge; the table is unchanged."""

@@ -46,7 +46,7 @@ def _shard_table(ev, lens, offs, payload, idx):
     return shard.ServiceTable.from_rows(rows, keys)
 
 
-def _worker(rank, world, port, kind, out_path):
+def _worker(rank, world, port, kind, out_path, two_round=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=120))
@@ -57,16 +57,29 @@ def _worker(rank, world, port, kind, out_path):
             sev, sl, so, sp, gidx = ebd.generate_host(5, 5, 0, 6000, shard=(world, rank), with_gidx=True)
             assert np.array_equal(gidx, idx) and np.array_equal(sev, ev[idx])
         table = _shard_table(ev, lens, offs, payload, idx)
-        mine = shard.exchange_merge(table, device="cpu")
+        stats = {}
+        mine = shard.exchange_merge(table, device="cpu", two_round=two_round, stats=stats)
         owner = shard.owner_np(mine.rec["key_lo"], world)
         assert np.all(owner == rank)  # every merged service is on its owner
         rows = shard.gather_rows(mine)
+        parts = [None] * world
+        dist.all_gather_object(parts, stats)
         if rank == 0:
             with open(out_path, "w") as f:
-                json.dump([[p, ep.decode("latin-1"), dom.decode("latin-1"), sch.decode(), i, e]
-                           for (p, ep, dom, sch, i, e) in rows], f)
+                json.dump({"rows": [[p, ep.decode("latin-1"), dom.decode("latin-1"), sch.decode(), i, e]
+                                    for (p, ep, dom, sch, i, e) in rows], "stats": parts}, f)
     finally:
         dist.destroy_process_group()
+
+
+def _run_merge(kind, tmp_path, two_round=True, world=2):
+    out_path = str(tmp_path / f"merged_{kind}_{int(two_round)}.json")
+    mp.start_processes(_worker, args=(world, _free_port(), kind, out_path, two_round), nprocs=world, join=True,
+                       start_method="spawn")
+    with open(out_path) as f:
+        got = json.load(f)
+    rows = [(p, ep.encode("latin-1"), dom.encode("latin-1"), sch.encode(), i, e) for p, ep, dom, sch, i, e in got["rows"]]
+    return rows, got["stats"]
 
 
 def _free_port():
@@ -77,17 +90,28 @@ def _free_port():
 
 @pytest.mark.parametrize("kind", ["config3", "config5", "fragmented"])
 def test_two_rank_merge_equals_whole_trace(kind, tmp_path):
-    out_path = str(tmp_path / "merged.json")
-    mp.start_processes(_worker, args=(2, _free_port(), kind, out_path), nprocs=2, join=True, start_method="spawn")
-    with open(out_path) as f:
-        merged = [(p, ep.encode("latin-1"), dom.encode("latin-1"), sch.encode(), i, e) for p, ep, dom, sch, i, e in
-                  json.load(f)]
+    merged, _ = _run_merge(kind, tmp_path)
     ev, lens, offs, payload = _trace(kind)
     o = O.Oracle()
     o.process(ev, lens, offs, payload)
     want = sorted(o.services(), key=lambda t: (t[0], t[1]))
     assert len(merged) == len(want)
     assert merged == want
+
+
+def test_two_round_exchange_ships_bytes_once_per_new_key(tmp_path):
+    """The key round, the owners' need flags and the bytes round give the one-round table,
+    and endpoint bytes cross only for keys their owner lacked: fewer bytes than one round
+    (config 3's Zipf keys recur across shards), at most one copy per merged key."""
+    two, st2 = _run_merge("config3", tmp_path, two_round=True)
+    one, st1 = _run_merge("config3", tmp_path, two_round=False)
+    assert two == one
+    sent2 = sum(s["string_bytes"] for s in st2)
+    sent1 = sum(s["string_bytes"] for s in st1)
+    assert sent1 == sum(s["string_bytes_one_round"] for s in st2)
+    assert 0 < sent2 < sent1
+    # at most one copy of each merged key's endpoint (8-byte padded)
+    assert sent2 <= sum((len(ep) + 7) // 8 * 8 for (_, ep, _, _, _, _) in two)
 
 
 def test_shards_keep_connections_and_order():

@@ -82,20 +82,25 @@ def main():
 		if (done) { // the last chunk""")
     s = sub(s, """		push(done, tw);
 		if (done) {
-			e0 = e1;
-			e1 = lane_ev(d, grab(), re);
+			e0 = lane_ev(d, e1);
+			e1 = lane_load(d, grab(), re);
 			resolve();
 		}
-	}""", """		push(done, tw);
+	}
+	if (lane == 0)
+		atomicAdd(&sh.scan_done, 1u);""", """		push(done, tw);
 		unsigned long long Q4 = clock64();
 		S_push += Q4 - Q3;
 		if (done) {
-			e0 = e1;
-			e1 = lane_ev(d, grab(), re);
+			e0 = lane_ev(d, e1);
+			e1 = lane_load(d, grab(), re);
 			resolve();
 		}
 		S_res += clock64() - Q4;
 	}
+	if (lane == 0)
+		atomicAdd(&sh.scan_done, 1u);
+	// after the finalize waves were released: the print's cost is outside every stamp
 	if (lane == 0 && blockIdx.x < 8)
 		printf("STAMP scan %u %u %llu %llu %llu %llu %llu %llu %llu\\n", blockIdx.x, wave, S_it, S_val, S_wait, S_issue, S_scan, S_push, S_res);""")
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
