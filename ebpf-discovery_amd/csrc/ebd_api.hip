@@ -30,6 +30,10 @@ hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* m
 hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
 		uint32_t cap, hipStream_t st, int cus);
 size_t sess_state_bytes();
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, hipStream_t st, int cus);
+hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus);
+hipError_t launch_walk_heads(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, hipStream_t st, int cus);
+size_t lru_scan_blocks(uint32_t n);
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
@@ -83,7 +87,7 @@ using namespace ebd;
 
 // the layouts the Python binding (ebd/__init__.py) and tests/test_abi.py assume
 static_assert(sizeof(ebd_config) == 64, "ebd_config layout");
-static_assert(sizeof(ebd_stats) == 88, "ebd_stats layout");
+static_assert(sizeof(ebd_stats) == 104, "ebd_stats layout");
 static_assert(sizeof(ebd_event_result) == 16 && sizeof(ebd_service) == 80 && sizeof(ebd_service_net) == 32, "result layouts");
 static_assert(sizeof(ebd_request) == 40 && sizeof(ebd_device_batch) == 48, "request / batch layouts");
 
@@ -168,6 +172,10 @@ struct ebd_ctx {
 	void* d_lru_sess = nullptr;
 	uint32_t* d_lru_live = nullptr;
 	uint64_t lru_batches_exact = 0;
+	uint64_t lru_rounds = 0, lru_sequential = 0;
+	LruRound lr{};              // the exact-LRU rounds' scratch (allocated on first need)
+	void* lr_mem = nullptr;
+	unsigned long long* h_lr = nullptr; // pinned: a round's counters
 	// network counters (EBD_CFG_NETWORK_COUNTERS): map entries (two tables: a clear rebuilds
 	// into the other), the v6 prefix dictionary, and the network-counter clear's scratch
 	int net_on = 0;
@@ -348,6 +356,10 @@ static void ctx_free(ebd_ctx* c) {
 		(void)hipHostFree(c->h_ctr);
 	if (c->h_end)
 		(void)hipHostFree(c->h_end);
+	if (c->lr_mem)
+		(void)hipFree(c->lr_mem);
+	if (c->h_lr)
+		(void)hipHostFree(c->h_lr);
 	for (int k = 0; k < 2; k++) {
 		auto& g = c->stg[k];
 		void* sp[] = {g.ev, g.len, g.off, g.payload};
@@ -594,6 +606,87 @@ static int finish_pending(ebd_ctx* c) {
 	return 0;
 }
 
+// The exact-LRU rounds' scratch, one allocation carved into LruRound's arrays.
+static int lru_alloc(ebd_ctx* c) {
+	if (c->lr_mem)
+		return 0;
+	const size_t n = c->max_events, cc = c->carry_cap, nb = lru_scan_blocks(c->max_events) + 1;
+	const size_t sizes[] = {n, n, 4 * n, n, 4 * (n + cc), 4 * (n + cc), 4 * n, 4 * cc, 4 * cc, n, n, cc, cc, 16 * nb, 4 * nb, 8 * nb, 4 * nb,
+			4 * nb, 4 * nb, 16, 4 * n, 4 * n, 32};
+	size_t total = 0;
+	for (size_t z : sizes)
+		total += (z + 255) & ~(size_t)255;
+	HIP_TRY(hipMalloc(&c->lr_mem, total));
+	if (!c->h_lr)
+		HIP_TRY(hipHostMalloc(&c->h_lr, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+	uint8_t* p = (uint8_t*)c->lr_mem;
+	void* ptrs[23];
+	for (int k = 0; k < 23; k++) {
+		ptrs[k] = p;
+		p += (sizes[k] + 255) & ~(size_t)255;
+	}
+	LruRound& w = c->lr;
+	w.ops = (uint8_t*)ptrs[0];
+	w.opt = (uint8_t*)ptrs[1];
+	w.mend = (uint32_t*)ptrs[2];
+	w.evt = (uint8_t*)ptrs[3];
+	w.mk_ref = (uint32_t*)ptrs[4];
+	w.mk_e = (uint32_t*)ptrs[5];
+	w.ev_t = (uint32_t*)ptrs[6];
+	w.cm_end = (uint32_t*)ptrs[7];
+	w.cm_head = (uint32_t*)ptrs[8];
+	w.f[0] = (uint8_t*)ptrs[9];
+	w.f[1] = (uint8_t*)ptrs[10];
+	w.cf[0] = (uint8_t*)ptrs[11];
+	w.cf[1] = (uint8_t*)ptrs[12];
+	w.bf = ptrs[13];
+	w.bm = (uint32_t*)ptrs[14];
+	w.lst = (long long*)ptrs[15];
+	w.moff = (uint32_t*)ptrs[16];
+	w.be = (uint32_t*)ptrs[17];
+	w.eoff = (uint32_t*)ptrs[18];
+	w.tot = (uint32_t*)ptrs[19];
+	w.jpos = (uint32_t*)ptrs[20];
+	w.head = (uint32_t*)ptrs[21];
+	w.cnt = (unsigned long long*)ptrs[22];
+	return 0;
+}
+
+// The exact LRU in rounds (ebd_kernels.hip k_lru_*): walk the sessions in a world of
+// evictions without output, derive the evictions the walk's LRU operations imply, repeat
+// until the world derived is the world walked; then the walk with output.  Returns 1 when
+// the rounds did not settle (the caller replays the batch sequentially instead).
+static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled) {
+	*settled = 0;
+	if (int rc = lru_alloc(c))
+		return rc;
+	LruRound& w = c->lr;
+	HIP_TRY(hipMemsetAsync(w.jpos, 0xff, (size_t)d.n * sizeof(uint32_t), c->stream));
+	HIP_TRY(launch_walk_heads(d, nslow, w.jpos, w.head, c->stream, c->cus));
+	HIP_TRY(hipMemsetAsync(w.f[0], 0, nslow, c->stream));
+	HIP_TRY(hipMemsetAsync(w.cf[0], 0, c->carry_cap, c->stream));
+	int cur = 0;
+	const int max_rounds = 256;
+	for (int r = 0; r < max_rounds; r++) {
+		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, c->stream, c->cus); }));
+		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		c->lru_rounds++;
+		if (c->h_lr[1]) // operations with a full cache and no victim: not a world to walk on
+			return 0;
+		if (c->h_lr[2] == 0) { // the world derived is the world walked
+			*settled = 1;
+			break;
+		}
+		cur ^= 1;
+	}
+	if (!*settled)
+		return 0;
+	HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk_flags(d, nslow, w.f[cur], w.cf[cur], c->stream, c->cus); }));
+	HIP_TRY(hipMemcpyAsync(c->d_ctr + CTR_EVICTIONS, w.cnt, sizeof(unsigned long long), hipMemcpyDeviceToDevice, c->stream));
+	return 0;
+}
+
 // One poll cycle on the context stream.  The host waits once, for the counters after the
 // fresh pass (is there session work?), while k_agg_fast already runs; a batch without session
 // work returns with its kernels still queued, and a batch with some returns once the session
@@ -677,8 +770,14 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 			const long long peak = pk ? (long long)pk - (1ll << 31) : 0;
 			exact = (long long)c->n_carry + peak > (long long)c->carry_cap;
 		}
+		int settled = 0;
 		if (exact) {
 			c->lru_batches_exact++;
+			if (int rc = run_lru_rounds(c, d, (uint32_t)nslow, &settled))
+				return rc;
+		}
+		if (exact && !settled) {
+			c->lru_sequential++;
 			if (!c->d_lru_jpos) {
 				HIP_TRY(hipMalloc(&c->d_lru_jpos, (size_t)c->max_events * sizeof(uint32_t)));
 				HIP_TRY(hipMalloc(&c->d_lru_head, (size_t)c->max_events * sizeof(uint32_t)));
@@ -690,7 +789,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 				return launch_walk_lru(d, (uint32_t)nslow, c->d_lru_jpos, c->d_lru_head, (SessState*)c->d_lru_sess, c->d_lru_live,
 						c->carry_cap, c->stream, c->cus);
 			}));
-		} else {
+		} else if (!exact) {
 			HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk(d, (uint32_t)nslow, c->stream, c->cus); }));
 			if (c->n_carry)
 				HIP_TRY(timed(c, KT_CARRY_PASS, [&] { return launch_carry_pass(d, c->stream); }));
@@ -1482,6 +1581,8 @@ int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 	s->hash_collisions = c->h_ctr[CTR_COLLISIONS];
 	s->lru_evictions = c->h_ctr[CTR_EVICTIONS_TOTAL];
 	s->lru_exact_batches = c->lru_batches_exact;
+	s->lru_rounds = c->lru_rounds;
+	s->lru_sequential = c->lru_sequential;
 	s->services = c->h_ctr[CTR_SERVICES];
 	s->errors = c->h_ctr[CTR_ERRORS];
 	return 0;

@@ -124,6 +124,33 @@ struct ClaimRec {
 };
 static_assert(sizeof(ClaimRec) == 24, "claim record is 24 bytes");
 
+// Scratch of the exact-LRU rounds (k_lru_*, ebd_api.hip run_batch): per event (ops by sorted
+// position, opt by event, marker ends, eviction flags), the compacted markers and eviction
+// times, per carried session, the two worlds of eviction flags, per scan block.
+struct LruRound {
+	uint8_t* ops;
+	uint8_t* opt;
+	uint32_t* mend;
+	uint8_t* evt;
+	uint32_t* mk_ref;
+	uint32_t* mk_e;
+	uint32_t* ev_t;
+	uint32_t* cm_end;
+	uint32_t* cm_head;
+	uint8_t* f[2];
+	uint8_t* cf[2];
+	void* bf; // LFn per scan block
+	uint32_t* bm;
+	long long* lst;
+	uint32_t* moff;
+	uint32_t* be;
+	uint32_t* eoff;
+	uint32_t* tot;
+	uint32_t* jpos;
+	uint32_t* head;
+	unsigned long long* cnt;
+};
+
 struct Dev {
 	// immutable tables
 	const uint8_t* dfa;

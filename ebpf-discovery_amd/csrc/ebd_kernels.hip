@@ -1355,7 +1355,10 @@ struct SessState {
 	uint32_t li; // position in the exact walker's live list
 };
 
-enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2 };
+// The LRU operation of one event (the exact-LRU rounds record them, k_lru_*): none (no find:
+// no buffer to parse, or the session is not saved), insert (saveSession), erase (close or a
+// saved session's INVALID), access (a saved session's buffer: find touched it, it stays).
+enum : uint32_t { OP_NONE = 0, OP_INSERT = 1, OP_ERASE = 2, OP_ACCESS = 3 };
 
 // Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
 // session's state in S.  Returns the LRU operation it implies; an insert (saveSession,
@@ -1392,6 +1395,7 @@ __device__ __forceinline__ bool ev_begin(const Dev& d, SessState& S, uint32_t jj
 // kernel-side delete (INVALID of a saved session), the close.  Returns the LRU operation
 // it implies; an insert (saveSession, Discovery.cpp:148-150) is left to the caller, which
 // may have to evict first.
+template <bool DRY = false>
 __device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvCtx& e, uint32_t c) {
 	ebd_event_result r;
 	r.consumed = 0;
@@ -1404,14 +1408,17 @@ __device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvC
 		r.consumed = (uint16_t)c;
 		if (e.flags & EV_EXISTING) {
 			r.info |= EBD_INFO_EXISTING;
+			op = OP_ACCESS;
 			if (S.g.state == ST_INVALID) {
 				r.status = EBD_STATUS_INVALID;
-				atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
+				if (!DRY)
+					atomicAdd(&d.ctr[CTR_KDELETES], 1ull); // bpfDiscoveryDeleteSession
 				S.live = 0;
 				op = OP_ERASE;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-				defer_emit(d, S.w, e.jj, S.g, e.i, r);
+				if (!DRY)
+					defer_emit(d, S.w, e.jj, S.g, e.i, r);
 				gp_reset(S.g); // session.reset(); stays saved
 				S.w = Walk{nullptr, 0, e.jj + 1};
 			} else {
@@ -1422,7 +1429,8 @@ __device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvC
 				r.status = EBD_STATUS_INVALID;
 			} else if (S.g.state == ST_FINISHED) {
 				r.status = EBD_STATUS_FINISHED;
-				defer_emit(d, S.w, e.jj, S.g, e.i, r);
+				if (!DRY)
+					defer_emit(d, S.w, e.jj, S.g, e.i, r);
 			} else {
 				r.status = EBD_STATUS_UNFINISHED;
 				if (!(e.flags & FLAG_END))
@@ -1434,7 +1442,8 @@ __device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvC
 		S.live = 0;
 		op = OP_ERASE;
 	}
-	d.res[e.i] = r;
+	if (!DRY)
+		d.res[e.i] = r;
 	return op;
 }
 
@@ -1497,9 +1506,13 @@ __device__ __forceinline__ void session_carry_out(const Dev& d, const SessState&
 
 // The parallel session path: one lane per session (k_walk_heads lists them), events in
 // order.  Exact while no LRU eviction can happen (run_batch checks an upper bound of the
-// live sessions first).  The header-key trie and the byte classes sit in LDS: the walk
-// reads them once per byte.
-__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
+// live sessions first), or with the evictions the exact-LRU rounds derived: evf[j] bit 0 =
+// the session was evicted before its event j (it parses that buffer as a new session), bit 1
+// at a session's first position = evicted after its last event (not carried out).  DRY (the
+// rounds' walks): no outputs, only each event's LRU operation in ops[j].  The header-key trie
+// and the byte classes sit in LDS: the walk reads them once per byte.
+template <bool DRY>
+__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, uint8_t* ops) {
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
 		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
@@ -1532,11 +1545,15 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 		if (busy == 0 || __popcll(wait) >= kWalkRefill) {
 			if (ended) {
 				const uint32_t c = dfa_walk_store(d.di, w, pos0, ne, e.L, (uint8_t)e.flags, S.g);
-				if (ev_end(d, S, e, c) == OP_INSERT) {
+				const uint32_t op = ev_end<DRY>(d, S, e, c);
+				if (op == OP_INSERT) {
 					S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
 					S.stamp = d.seq_base + e.i;
-					wave_add(&d.ctr[CTR_INSERTS], 1ull);
+					if (!DRY)
+						wave_add(&d.ctr[CTR_INSERTS], 1ull);
 				}
+				if (DRY)
+					ops[e.jj] = (uint8_t)op;
 				ended = false;
 			}
 			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
@@ -1567,6 +1584,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 							pf_off = d.off[pf_i];
 						}
 					}
+					if (evf && (evf[jj] & 1u))
+						S.live = 0; // evicted since its previous event: find() misses
 					if (ev_begin(d, S, jj, i, fl, L, off, e)) {
 						dfa_walk_load(S.g, A[S.g.ds], w);
 						pos0 = w.pos;
@@ -1580,11 +1599,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d) {
 							cur = *(const uint4*)b0;
 						in_ev = true;
 					} else {
-						ev_end(d, S, e, 0);
+						const uint32_t op = ev_end<DRY>(d, S, e, 0);
+						if (DRY)
+							ops[jj] = (uint8_t)op;
 					}
 					jj++;
 				} else {
-					if (S.live)
+					if (!DRY && S.live && !(evf && (evf[jhead] & 2u)))
 						session_carry_out(d, S, jhead, jj - 1);
 					have = false;
 					h += stride;
@@ -1616,8 +1637,10 @@ __global__ void k_sess_tally(Dev d) {
 }
 
 // Saved sessions with no event in this batch stay saved unchanged.
-__global__ void k_carry_pass(Dev d) {
+__global__ void k_carry_pass(Dev d, const uint8_t* cevf) {
 	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < d.n_carry_in; c += gridDim.x * blockDim.x) {
+		if (cevf && cevf[c])
+			continue; // evicted (the exact-LRU rounds)
 		const Carry& cr = d.carry_in[c];
 		const int slot = sset_find(d, cr.pid, cr.fd, cr.sid);
 		if (slot >= 0 && d.sset[slot].visited)
@@ -1894,6 +1917,305 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 			jl++;
 		session_carry_out(d, S[h], h, jl);
 	}
+}
+
+// ---------------------------------------------------------------------------------
+// Exact LRU in rounds (the parallel form of k_walk_lru).  A world is a set of evictions, as
+// flags on the session events at which a session finds itself evicted (k_walk's evf).  Each
+// round walks every session in the current world without output (k_walk<true>), which gives
+// every session event its LRU operation, then derives the evictions those operations imply:
+//  * the LRU's size after each event follows from the operation types alone: an insert makes
+//    it min(cap, L + 1) (a full cache evicts first, LRUCache.h:54-60), an erase L - 1.  Maps
+//    x -> min(a, x + b) compose within their family, so the sizes come from a scan over event
+//    order (k_lru_scan_*), and an insert evicts exactly when the size before it is cap;
+//  * an eviction removes the least recently used session.  Every insert or access starts a
+//    "marker" (the session's recency) that lasts until the session's next operation; the
+//    evicted session is the oldest marker still alive, and since evictions only ever take the
+//    oldest, they take markers in position order: one merge of the markers (carried sessions
+//    first, by recency) with the eviction times (k_lru_greedy).
+// The victim's next find (the first event at which its absence shows) gets the eviction flag.
+// When a round derives the world it walked, that world is the sequential execution.  If the
+// walked flags first differ from the sequential ones at event T, the operations before T are
+// the sequential ones, so are the evictions before T and their victims, and so every derived
+// flag up to T: each round settles at least one more event (tests/test_lru_rounds.py restates
+// the rounds and checks them against a sequential LRU).
+// ---------------------------------------------------------------------------------
+constexpr int kLsT = 256, kLsPer = 16;
+constexpr uint32_t kLsBlk = kLsT * kLsPer; // events per scan block
+constexpr long long kLInf = 1ll << 60;
+struct LFn {
+	long long a, b; // x -> min(a, x + b)
+};
+__device__ __forceinline__ LFn lfn_id() { return LFn{kLInf, 0}; }
+__device__ __forceinline__ LFn lfn_op(uint32_t op, uint32_t cap) {
+	return op == OP_INSERT ? LFn{(long long)cap, 1} : op == OP_ERASE ? LFn{kLInf, -1} : lfn_id();
+}
+__device__ __forceinline__ LFn lfn_then(LFn f, LFn g) { return LFn{min(g.a, f.a + g.b), f.b + g.b}; } // g after f
+__device__ __forceinline__ long long lfn_apply(LFn f, long long x) { return min(f.a, x + f.b); }
+__device__ __forceinline__ bool op_marks(uint32_t op) { return op == OP_INSERT || op == OP_ACCESS; }
+
+// Event-ordered operations (opt, zeroed before), each marker's end, and per carried session
+// its first marker's end and its first sorted position (cm_end, cm_head: kNone before).  A
+// marker ends at its session's next find (Discovery.cpp:114 for a buffer, :195 for a close),
+// whatever that event did in the world walked: a session evicted before it misses there.
+__global__ void k_lru_mark(Dev d, uint32_t nslow, const uint8_t* ops, uint8_t* opt, uint32_t* mend, uint32_t* cm_end,
+		uint32_t* cm_head) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
+		const unsigned long long key = d.slow_keys[j];
+		const uint32_t grp = (uint32_t)(key >> 32), i = (uint32_t)key, op = ops[j];
+		opt[i] = (uint8_t)op;
+		auto next_find = [&](uint32_t from) {
+			for (uint32_t q = from; q < nslow && (uint32_t)(d.slow_keys[q] >> 32) == grp; q++) {
+				const uint32_t iq = (uint32_t)d.slow_keys[q], fl = d.ev[iq].flags, L = d.len[iq];
+				if ((fl & FLAG_END) || ((fl & FLAG_NEW) && L != EBD_NO_BUFFER && buf_in(d, L, d.off[iq])))
+					return iq;
+			}
+			return kNone;
+		};
+		if (op_marks(op))
+			mend[i] = next_find(j + 1);
+		const bool headj = j == 0 || (uint32_t)(d.slow_keys[j - 1] >> 32) != grp;
+		if (headj && grp < d.carry_cap) { // a carried session (its group is its carry index)
+			cm_head[grp] = j;
+			cm_end[grp] = next_find(j);
+		}
+	}
+}
+
+// The carried sessions' markers, least recently used first (stamps are unique event positions).
+__global__ void k_lru_carry_rank(Dev d, const uint32_t* cm_end, uint32_t* mk_ref, uint32_t* mk_e) {
+	const uint32_t nc = d.n_carry_in;
+	for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += gridDim.x * blockDim.x) {
+		const unsigned long long st = d.carry_in[c].stamp;
+		uint32_t rank = 0;
+		for (uint32_t o = 0; o < nc; o++) {
+			const unsigned long long so = d.carry_in[o].stamp;
+			rank += (so < st || (so == st && o < c)) ? 1u : 0u;
+		}
+		mk_ref[rank] = 0x80000000u | c;
+		mk_e[rank] = cm_end[c];
+	}
+}
+
+// Phase 1: each block's composed size map and its marker count.
+__global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint32_t n, uint32_t cap, LFn* bf, uint32_t* bm) {
+	__shared__ LFn F[kLsT];
+	__shared__ uint32_t M[kLsT];
+	const uint32_t t = threadIdx.x;
+	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
+	LFn f = lfn_id();
+	uint32_t m = 0;
+	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
+		const unsigned long long i = base + k;
+		const uint32_t op = i < n ? opt[i] : OP_NONE;
+		f = lfn_then(f, lfn_op(op, cap));
+		m += op_marks(op) ? 1u : 0u;
+	}
+	F[t] = f;
+	M[t] = m;
+	__syncthreads();
+	for (uint32_t s = 1; s < (uint32_t)kLsT; s <<= 1) { // in-order tree: F[t] = F[t] then F[t + s]
+		if ((t & (2 * s - 1)) == 0) {
+			F[t] = lfn_then(F[t], F[t + s]);
+			M[t] += M[t + s];
+		}
+		__syncthreads();
+	}
+	if (t == 0) {
+		bf[blockIdx.x] = F[0];
+		bm[blockIdx.x] = M[0];
+	}
+}
+
+// Phase 2 (one thread): each block's starting size from the context's carried sessions, and
+// its first marker's index (after the carried ones).
+__global__ void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0, long long* lst,
+		uint32_t* moff, uint32_t* tot) {
+	if (blockIdx.x || threadIdx.x)
+		return;
+	long long x = l0;
+	uint32_t m = m0;
+	for (uint32_t b = 0; b < nb; b++) {
+		lst[b] = x;
+		moff[b] = m;
+		x = lfn_apply(bf[b], x);
+		m += bm[b];
+	}
+	tot[0] = m; // markers, carried ones included
+}
+
+// Block-wide exclusive scan of the threads' maps (in order), by Hillis-Steele in LDS.
+__device__ __forceinline__ LFn lfn_block_excl(LFn f, LFn* F) {
+	const uint32_t t = threadIdx.x;
+	F[t] = f;
+	__syncthreads();
+	for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) {
+		const LFn g = t >= o ? lfn_then(F[t - o], F[t]) : F[t];
+		__syncthreads();
+		F[t] = g;
+		__syncthreads();
+	}
+	const LFn r = t ? F[t - 1] : lfn_id();
+	__syncthreads();
+	return r;
+}
+__device__ __forceinline__ uint32_t u32_block_excl(uint32_t x, uint32_t* S, uint32_t* total) {
+	const uint32_t t = threadIdx.x;
+	S[t] = x;
+	__syncthreads();
+	for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) {
+		const uint32_t g = t >= o ? S[t - o] + S[t] : S[t];
+		__syncthreads();
+		S[t] = g;
+		__syncthreads();
+	}
+	const uint32_t r = t ? S[t - 1] : 0u;
+	*total = S[kLsT - 1];
+	__syncthreads();
+	return r;
+}
+
+// Phase 3: each event's size before it; evt[i] = 1 where an insert finds the cache full.
+__global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uint32_t n, uint32_t cap, const long long* lst,
+		uint8_t* evt, uint32_t* be) {
+	__shared__ LFn F[kLsT];
+	__shared__ uint32_t S[kLsT];
+	const uint32_t t = threadIdx.x;
+	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
+	LFn f = lfn_id();
+	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
+		const unsigned long long i = base + k;
+		f = lfn_then(f, lfn_op(i < n ? opt[i] : OP_NONE, cap));
+	}
+	long long x = lfn_apply(lfn_block_excl(f, F), lst[blockIdx.x]);
+	uint32_t ne = 0;
+	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
+		const unsigned long long i = base + k;
+		if (i >= n)
+			break;
+		const uint32_t op = opt[i];
+		const bool ev = op == OP_INSERT && x >= (long long)cap;
+		evt[i] = ev ? 1 : 0;
+		ne += ev ? 1u : 0u;
+		x = lfn_apply(lfn_op(op, cap), x);
+	}
+	uint32_t tot;
+	(void)u32_block_excl(ne, S, &tot);
+	if (t == 0)
+		be[blockIdx.x] = tot;
+}
+
+// Phase 4 (one thread): each block's first eviction index.
+__global__ void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot) {
+	if (blockIdx.x || threadIdx.x)
+		return;
+	uint32_t e = 0;
+	for (uint32_t b = 0; b < nb; b++) {
+		eoff[b] = e;
+		e += be[b];
+	}
+	tot[1] = e;
+}
+
+// Phase 5: the markers (event position, end) and the eviction times, in event order.
+__global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const uint32_t* mend, const uint8_t* evt, uint32_t n,
+		const uint32_t* moff, const uint32_t* eoff, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t) {
+	__shared__ uint32_t S[kLsT];
+	const uint32_t t = threadIdx.x;
+	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
+	uint32_t nm = 0, ne = 0;
+	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
+		const unsigned long long i = base + k;
+		if (i >= n)
+			break;
+		nm += op_marks(opt[i]) ? 1u : 0u;
+		ne += evt[i];
+	}
+	uint32_t tot;
+	uint32_t m = moff[blockIdx.x] + u32_block_excl(nm, S, &tot);
+	uint32_t e = eoff[blockIdx.x] + u32_block_excl(ne, S, &tot);
+	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
+		const unsigned long long i = base + k;
+		if (i >= n)
+			break;
+		if (op_marks(opt[i])) {
+			mk_ref[m] = (uint32_t)i;
+			mk_e[m] = mend[i];
+			m++;
+		}
+		if (evt[i])
+			ev_t[e++] = (uint32_t)i;
+	}
+}
+
+// Phase 6 (one wave): each eviction takes the oldest marker alive at its time; the victim's
+// next event (or its session's end, or its carry entry) gets the eviction flag.  cnt[0] =
+// evictions, cnt[1] = 1 when the operations are inconsistent (a full cache with no victim).
+__global__ __launch_bounds__(64) void k_lru_greedy(const uint32_t* mk_ref, const uint32_t* mk_e, const uint32_t* tot,
+		const uint32_t* ev_t, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head, uint8_t* nf, uint8_t* ncf,
+		unsigned long long* cnt) {
+	const uint32_t lane = threadIdx.x;
+	const uint32_t nmk = tot[0], nev = tot[1];
+	uint32_t wb = 0, qf = 0; // window base (markers [wb, wb + 64) in registers), queue front
+	uint32_t r = lane < nmk ? mk_ref[lane] : 0u, e = lane < nmk ? mk_e[lane] : 0u;
+	uint32_t bad = 0;
+	for (uint32_t j0 = 0; j0 < nev && !bad; j0 += 64) {
+		const uint32_t tv = j0 + lane < nev ? ev_t[j0 + lane] : 0u;
+		const uint32_t nj = min(64u, nev - j0);
+		for (uint32_t jl = 0; jl < nj && !bad; jl++) {
+			const uint32_t t = __shfl(tv, (int)jl);
+			for (;;) {
+				const bool live = wb + lane >= qf && wb + lane < nmk && (e == kNone || e > t);
+				const unsigned long long b = __ballot(live);
+				if (b == 0) {
+					wb += 64;
+					if (wb >= nmk) {
+						bad = 1;
+						break;
+					}
+					qf = wb;
+					r = wb + lane < nmk ? mk_ref[wb + lane] : 0u;
+					e = wb + lane < nmk ? mk_e[wb + lane] : 0u;
+					continue;
+				}
+				const uint32_t k = (uint32_t)__builtin_ctzll(b);
+				const uint32_t vr = __shfl(r, (int)k), ve = __shfl(e, (int)k);
+				qf = wb + k + 1;
+				if (!(vr & 0x80000000u) && vr >= t) { // the oldest live marker is not older than the insert
+					bad = 1;
+					break;
+				}
+				if (lane == 0) {
+					if (ve != kNone) {
+						nf[jpos[ve]] |= 1u; // find() misses at the session's next operation
+					} else if (vr & 0x80000000u) {
+						const uint32_t c = vr & 0x7fffffffu;
+						if (cm_head[c] != kNone)
+							nf[cm_head[c]] |= 2u;
+						else
+							ncf[c] = 1;
+					} else {
+						nf[head[jpos[vr]]] |= 2u; // after the session's last event: not carried out
+					}
+				}
+				break;
+			}
+		}
+	}
+	if (lane == 0) {
+		cnt[0] = bad ? 0ull : (unsigned long long)nev;
+		cnt[1] = bad;
+	}
+}
+
+// Phase 7: how many flags the round changed.
+__global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, const uint8_t* cf, const uint8_t* ncf, uint32_t n2,
+		unsigned long long* cnt) {
+	uint32_t x = 0;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x)
+		x += k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
+	if (__any(x != 0))
+		wave_add(&cnt[2], (unsigned long long)x);
 }
 
 // Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
@@ -2858,12 +3180,63 @@ hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
 }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
-	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d);
+	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d,
+			(const uint8_t*)nullptr, (uint8_t*)nullptr);
 
 	return hipGetLastError();
 }
+// One exact-LRU round (k_lru_* above) after a dry walk in the world of flags f / cf: the
+// derived world in nf / ncf (zeroed here), cnt[0] evictions, cnt[1] inconsistency, cnt[2] the
+// flags that changed.  scratch: LruRound's arrays.
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, hipStream_t st, int cus) {
+	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
+	const uint8_t* f = w.f[cur];
+	uint8_t* nf = w.f[cur ^ 1];
+	const uint8_t* cf = w.cf[cur];
+	uint8_t* ncf = w.cf[cur ^ 1];
+	hipLaunchKernelGGL(k_walk<true>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f, w.ops);
+	hipError_t e;
+	if ((e = hipMemsetAsync(w.opt, 0, n, st)) != hipSuccess || (e = hipMemsetAsync(w.cm_end, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
+			(e = hipMemsetAsync(nf, 0, nslow, st)) != hipSuccess || (e = hipMemsetAsync(ncf, 0, d.carry_cap, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cnt, 0, 4 * sizeof(unsigned long long), st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_lru_mark, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.ops, w.opt, w.mend,
+			w.cm_end, w.cm_head);
+	if (nc)
+		hipLaunchKernelGGL(k_lru_carry_rank, dim3(grid_for(nc, 256, cus * 4)), dim3(256), 0, st, d, (const uint32_t*)w.cm_end, w.mk_ref,
+				w.mk_e);
+	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm);
+	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(1), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
+			w.moff, w.tot);
+	hipLaunchKernelGGL(k_lru_scan_apply, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (const long long*)w.lst,
+			w.evt, w.be);
+	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(1), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
+	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
+			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, w.mk_ref, w.mk_e, w.ev_t);
+	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(64), 0, st, (const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.tot,
+			(const uint32_t*)w.ev_t, (const uint32_t*)w.jpos, (const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf, w.cnt);
+	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(nslow + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, f, (const uint8_t*)nf, nslow, cf,
+			(const uint8_t*)ncf, d.carry_cap, w.cnt);
+	return hipGetLastError();
+}
+// The final walk of the exact path in the converged world (with output), then the carried
+// sessions it did not meet.
+hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f,
+			(uint8_t*)nullptr);
+	if (d.n_carry_in)
+		hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, cf);
+	return hipGetLastError();
+}
+hipError_t launch_walk_heads(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
+	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, jpos, head);
+	return hipGetLastError();
+}
+size_t lru_scan_blocks(uint32_t n) { return (n + kLsBlk - 1) / kLsBlk; }
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
-	hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d);
+	hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, (const uint8_t*)nullptr);
 	return hipGetLastError();
 }
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {

@@ -79,7 +79,8 @@ class Stats(C.Structure):
     _fields_ = [("events", C.c_uint64), ("requests", C.c_uint64), ("session_events", C.c_uint64),
                 ("kernel_deletes", C.c_uint64), ("live_sessions", C.c_uint64), ("max_live_sessions", C.c_uint64),
                 ("services", C.c_uint64), ("hash_collisions", C.c_uint64), ("errors", C.c_uint64),
-                ("lru_evictions", C.c_uint64), ("lru_exact_batches", C.c_uint64)]
+                ("lru_evictions", C.c_uint64), ("lru_exact_batches", C.c_uint64),
+                ("lru_rounds", C.c_uint64), ("lru_sequential", C.c_uint64)]
 
 
 class KernelTime(C.Structure):

@@ -178,7 +178,9 @@ typedef struct ebd_stats {
 	uint64_t hash_collisions;   /* 64-bit slot tag matched but the 128-bit key did not */
 	uint64_t errors;            /* bitmask of EBD_ERR_* conditions seen */
 	uint64_t lru_evictions;     /* sessions evicted from the full LRU (LRUCache.h:56-58) */
-	uint64_t lru_exact_batches; /* batches whose session events ran through the exact LRU walker */
+	uint64_t lru_exact_batches; /* batches whose session events ran through the exact LRU path */
+	uint64_t lru_rounds;        /* walk-and-derive rounds the exact LRU path took (all batches) */
+	uint64_t lru_sequential;    /* exact batches that fell back to the one-lane replay (k_walk_lru) */
 } ebd_stats;
 
 #define EBD_ERR_TABLE_FULL 1u      /* service table probe limit reached */

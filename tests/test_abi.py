@@ -37,7 +37,7 @@ def test_struct_layouts_match_header():
     assert ebd.SESSION_REQ_DTYPE.itemsize == 32
     assert ebd.SERVICE_DTYPE.itemsize == 80
     assert C.sizeof(ebd.Config) == 64  # static_assert in ebd_api.hip
-    assert C.sizeof(ebd.Stats) == 88
+    assert C.sizeof(ebd.Stats) == 104
 
 
 def test_strerror():

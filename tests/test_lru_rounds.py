@@ -1,0 +1,158 @@
+"""The exact LRU in rounds (ebd_kernels.hip k_lru_*, ebd_api.hip run_lru_rounds), restated in
+Python and checked against a plain sequential LRU (LRUCache.h:50-89 as Discovery.cpp:92-198
+drives it) on random session traces.  The GPU path itself is checked against the oracle by
+test_gpu_parity.py::test_lru_eviction_exact; this pins the algorithm: the size scan, the
+marker merge, the victim flags and the convergence of the rounds to the sequential result.
+
+Session model (what the walker's parse decides, reduced to the LRU): an event of a saved
+session touches it (find) and keeps it (ACCESS) or drops it (ERASE: INVALID); an event of an
+unsaved session inserts it (saveSession after an UNFINISHED fresh parse) or does nothing;
+a close (DATA_END) erases a saved session; an event without a buffer does nothing.
+"""
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+
+NONE, INSERT, ERASE, ACCESS = 0, 1, 2, 3
+
+
+def make_trace(rng, n_sessions, n_events, n_carried):
+    """Events (session, has_buffer, op if saved, op if not saved, close) in time order, and the
+    carried sessions least recently used first."""
+    ev = []
+    for _ in range(n_events):
+        s = int(rng.integers(0, n_sessions))
+        buf = rng.random() < 0.95
+        ex_op = ERASE if rng.random() < 0.05 else ACCESS
+        new_op = INSERT if rng.random() < 0.6 else NONE
+        close = rng.random() < 0.08
+        ev.append((s, buf, ex_op, new_op, close))
+    carried = [int(x) for x in rng.permutation(n_sessions)[:n_carried]]
+    return ev, carried
+
+
+def sequential(ev, carried, cap):
+    """Discovery's loop with a real LRU: per-event operation, evictions, sessions left."""
+    lru = OrderedDict((s, True) for s in carried)  # first = least recently used
+    ops, evicted = [], 0
+    for (s, buf, ex_op, new_op, close) in ev:
+        op = NONE
+        if buf:
+            if s in lru:
+                lru.move_to_end(s)  # find touches
+                op = ex_op
+                if op == ERASE:
+                    del lru[s]
+            elif new_op == INSERT and not close:
+                if len(lru) >= cap:
+                    lru.popitem(last=False)
+                    evicted += 1
+                lru[s] = True
+                op = INSERT
+        if close and s in lru:
+            del lru[s]
+            op = ERASE
+        ops.append(op)
+    return ops, evicted, list(lru)
+
+
+def walk(ev, carried, flags, tail, cflag):
+    """The dry walk in a world of evictions: flags[t] = the event's session was evicted before
+    it; tail[s] / cflag[s]: evicted after its last event.  Per-event operations, and the
+    sessions saved at the end."""
+    live = {s: True for s in carried}
+    ops = []
+    for t, (s, buf, ex_op, new_op, close) in enumerate(ev):
+        if flags[t]:
+            live.pop(s, None)
+        op = NONE
+        if buf:
+            if s in live:
+                op = ex_op
+                if op == ERASE:
+                    del live[s]
+            elif new_op == INSERT and not close:
+                live[s] = True
+                op = INSERT
+        if close and s in live:
+            del live[s]
+            op = ERASE
+        ops.append(op)
+    left = [s for s in live if not tail.get(s) and not cflag.get(s)]
+    return ops, left
+
+
+def derive(ev, carried, ops, cap):
+    """k_lru_mark / scan / compact / greedy: the evictions the operations imply, as flags."""
+    n = len(ev)
+    # marker ends: the session's next find (an event with a buffer, or a close), whatever it
+    # did in this world (a find of an evicted session misses and does nothing)
+    nxt, last = [None] * n, {}
+    for t in range(n - 1, -1, -1):
+        s, buf, _, _, close = ev[t]
+        nxt[t] = last.get(s)
+        if buf or close:
+            last[s] = t
+    first_op = {s: last.get(s) for s in carried}
+    # the size scan: min(cap, L + 1) per insert, L - 1 per erase (composed maps)
+    fns = [(cap, 1) if o == INSERT else (1 << 60, -1) if o == ERASE else (1 << 60, 0) for o in ops]
+    L = len(carried)
+    evictions = []
+    for t, (a, b) in enumerate(fns):
+        if ops[t] == INSERT and L >= cap:
+            evictions.append(t)
+        L = min(a, L + b)
+    # markers, carried ones (least recently used first) before the batch's
+    markers = [(-1, first_op[s], s) for s in carried]
+    markers += [(t, nxt[t], ev[t][0]) for t in range(n) if ops[t] in (INSERT, ACCESS)]
+    flags, tail, cflag = [False] * n, {}, {}
+    q = 0
+    for t in evictions:
+        while q < len(markers) and not (markers[q][1] is None or markers[q][1] > t):
+            q += 1
+        assert q < len(markers) and markers[q][0] < t
+        pos, end, s = markers[q]
+        q += 1
+        if end is not None:
+            flags[end] = True
+        elif pos < 0:
+            cflag[s] = True
+        else:
+            tail[s] = True
+    return flags, tail, cflag, len(evictions)
+
+
+def rounds(ev, carried, cap, max_rounds=500):
+    flags, tail, cflag = [False] * len(ev), {}, {}
+    for r in range(1, max_rounds + 1):
+        ops, left = walk(ev, carried, flags, tail, cflag)
+        nf, nt, nc, nev = derive(ev, carried, ops, cap)
+        if nf == flags and nt == tail and nc == cflag:
+            return ops, nev, left, r
+        flags, tail, cflag = nf, nt, nc
+    raise AssertionError("rounds did not settle")
+
+
+@pytest.mark.parametrize("seed,cap,sessions,carried", [(1, 8, 40, 0), (2, 16, 100, 10), (3, 64, 500, 64), (4, 5, 30, 5),
+                                                        (5, 128, 3000, 100), (6, 2, 10, 2)])
+def test_rounds_equal_sequential_lru(seed, cap, sessions, carried):
+    rng = np.random.default_rng(seed)
+    ev, car = make_trace(rng, sessions, 4000, carried)
+    want_ops, want_ev, want_left = sequential(ev, car, cap)
+    ops, nev, left, r = rounds(ev, car, cap)
+    assert ops == want_ops
+    assert nev == want_ev
+    assert sorted(left) == sorted(want_left)
+    assert want_ev > 0 or cap >= sessions
+
+
+def test_rounds_settle_quickly_on_a_keepalive_trace():
+    """Many live sessions and steady inserts (config 4 over a small LRU, as in the GPU test):
+    the rounds settle in far fewer rounds than there are evictions."""
+    rng = np.random.default_rng(9)
+    ev, car = make_trace(rng, 2000, 20000, 50)
+    want_ops, want_ev, _ = sequential(ev, car, 100)
+    ops, nev, _, r = rounds(ev, car, 100)
+    assert ops == want_ops and nev == want_ev
+    assert want_ev > 1000 and r < 50

@@ -34,16 +34,22 @@ def main():
     ctx = ebd.Context(max_events=E, service_capacity=1 << max(20, int(np.ceil(np.log2(E / 3.2 * 0.8)))),
                       string_arena=max(256 << 20, E * 16), timing=True, lru_capacity=args.lru)
     ev, ln, of, pay, gidx, n, size = bench.generate_shard(ctx, 4, 4, E, 1, 0, dev)
+    import time
     for k in range(args.reps):
         ctx.clear()
         ctx.reset_kernel_times()
         ctx.set_seq_base(k * n)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
         ctx.submit_device(ev, ln, of, pay, n)
         ctx.sync()
+        dt = time.perf_counter() - t
     kt = ctx.kernel_times()
     st = ctx.stats()
-    print(json.dumps({"lib": os.path.basename(ebd.LIB_PATH), "events": n, "payload": size,
-                      "kernel_ms": {k: v[1] / v[0] for k, v in kt.items() if v[0]}, "stats": st}))
+    print(json.dumps({"lib": os.path.basename(ebd.LIB_PATH), "events": n, "payload": size, "batch_ms": dt * 1e3,
+                      "events_per_s": n / dt, "kernel_ms": {k: v[1] / v[0] for k, v in kt.items() if v[0]},
+                      "kernel_total_ms": {k: v[1] for k, v in kt.items() if v[0]},
+                      "launches": {k: v[0] for k, v in kt.items() if v[0]}, "stats": st}))
 
 
 if __name__ == "__main__":
