@@ -30,9 +30,10 @@ hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* m
 hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
 		uint32_t cap, hipStream_t st, int cus);
 size_t sess_state_bytes();
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, hipStream_t st, int cus);
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t nwalk, uint32_t front, uint32_t window,
+		hipStream_t st, int cus);
+hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus);
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus);
-hipError_t launch_walk_heads(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, hipStream_t st, int cus);
 size_t lru_scan_blocks(uint32_t n);
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
@@ -612,16 +613,16 @@ static int lru_alloc(ebd_ctx* c) {
 		return 0;
 	const size_t n = c->max_events, cc = c->carry_cap, nb = lru_scan_blocks(c->max_events) + 1;
 	const size_t sizes[] = {n, n, 4 * n, n, 4 * (n + cc), 4 * (n + cc), 4 * n, 4 * cc, 4 * cc, n, n, cc, cc, 16 * nb, 4 * nb, 8 * nb, 4 * nb,
-			4 * nb, 4 * nb, 16, 4 * n, 4 * n, 32};
+			4 * nb, 4 * nb, 32, 4 * n, 4 * n, 32, n, 4 * (n + cc), n, 4 * n, 4 * (n + 1), 4 * (n + 1)};
 	size_t total = 0;
 	for (size_t z : sizes)
 		total += (z + 255) & ~(size_t)255;
 	HIP_TRY(hipMalloc(&c->lr_mem, total));
 	if (!c->h_lr)
-		HIP_TRY(hipHostMalloc(&c->h_lr, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc(&c->h_lr, 6 * sizeof(unsigned long long), hipHostMallocDefault));
 	uint8_t* p = (uint8_t*)c->lr_mem;
-	void* ptrs[23];
-	for (int k = 0; k < 23; k++) {
+	void* ptrs[29];
+	for (int k = 0; k < 29; k++) {
 		ptrs[k] = p;
 		p += (sizes[k] + 255) & ~(size_t)255;
 	}
@@ -649,36 +650,57 @@ static int lru_alloc(ebd_ctx* c) {
 	w.jpos = (uint32_t*)ptrs[20];
 	w.head = (uint32_t*)ptrs[21];
 	w.cnt = (unsigned long long*)ptrs[22];
+	w.nf_t = (uint8_t*)ptrs[23];
+	w.vic = (uint32_t*)ptrs[24];
+	w.rmark = (uint8_t*)ptrs[25];
+	w.rlist = (uint32_t*)ptrs[26];
+	w.vict = (uint32_t*)ptrs[27];
+	w.qfe = (uint32_t*)ptrs[28];
+	HIP_TRY(hipMemset(w.rmark, 0, n)); // k_lru_rlist clears what it lists
 	return 0;
 }
 
 // The exact LRU in rounds (ebd_kernels.hip k_lru_*): walk the sessions in a world of
 // evictions without output, derive the evictions the walk's LRU operations imply, repeat
-// until the world derived is the world walked; then the walk with output.  Returns 1 when
-// the rounds did not settle (the caller replays the batch sequentially instead).
+// until the world derived is the world walked; then the walk with output.  Events before the
+// frontier are settled; a round derives the evictions of [front, front + window) (and keeps
+// the earlier ones) and walks again only the sessions whose flags changed.  *settled = 0: the
+// rounds did not settle (the caller replays the batch sequentially instead).
 static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled) {
 	*settled = 0;
 	if (int rc = lru_alloc(c))
 		return rc;
 	LruRound& w = c->lr;
-	HIP_TRY(hipMemsetAsync(w.jpos, 0xff, (size_t)d.n * sizeof(uint32_t), c->stream));
-	HIP_TRY(launch_walk_heads(d, nslow, w.jpos, w.head, c->stream, c->cus));
-	HIP_TRY(hipMemsetAsync(w.f[0], 0, nslow, c->stream));
-	HIP_TRY(hipMemsetAsync(w.cf[0], 0, c->carry_cap, c->stream));
+	HIP_TRY(launch_lru_init(d, nslow, w, c->stream, c->cus));
+	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
+	const uint32_t window = 1u << 16;
 	int cur = 0;
-	const int max_rounds = 256;
+	uint32_t nwalk = kNone, front = 0; // the first round walks every session
+	const int max_rounds = 4096;
 	for (int r = 0; r < max_rounds; r++) {
-		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, c->stream, c->cus); }));
-		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, nwalk, front, window, c->stream, c->cus); }));
+		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(hipMemcpyAsync(c->h_lr + 4, w.tot, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
 		HIP_TRY(hipStreamSynchronize(c->stream));
 		c->lru_rounds++;
+		const uint32_t* tot = (const uint32_t*)(c->h_lr + 4);
+		const unsigned long long changed = c->h_lr[2], first = c->h_lr[3];
+		const unsigned long long wend = (unsigned long long)front + window;
+		if (lru_trace)
+			std::fprintf(stderr, "ebd lru round %d: front %u, evictions %u (window to %u), flags changed %llu, first at %lld, walked %u\n", r,
+					front, tot[1], tot[2], changed, first == ~0ull ? -1ll : (long long)first, nwalk == kNone ? nslow : nwalk);
 		if (c->h_lr[1]) // operations with a full cache and no victim: not a world to walk on
 			return 0;
-		if (c->h_lr[2] == 0) { // the world derived is the world walked
+		if (changed == 0 && wend >= d.n) { // the world derived is the world walked, to the batch's end
 			*settled = 1;
 			break;
 		}
+		if (changed == 0)
+			front = (uint32_t)wend;
+		else if (first != ~0ull) // events before the first changed flag (and the window's end) are settled
+			front = (uint32_t)(first < wend ? first : wend);
 		cur ^= 1;
+		nwalk = tot[3];
 	}
 	if (!*settled)
 		return 0;

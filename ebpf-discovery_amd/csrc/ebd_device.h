@@ -145,10 +145,16 @@ struct LruRound {
 	uint32_t* moff;
 	uint32_t* be;
 	uint32_t* eoff;
-	uint32_t* tot;
+	uint32_t* tot; // 0 markers, 1 evictions, 2 window end, 3 next walk list, 4 listed victims, 5 evictions before the frontier
 	uint32_t* jpos;
 	uint32_t* head;
 	unsigned long long* cnt;
+	uint8_t* nf_t; // the round's eviction flags by event
+	uint32_t* vic; // victims with no later find
+	uint32_t* vict; // per eviction: its victim marker
+	uint32_t* qfe;  // per eviction: the marker queue's front before it
+	uint8_t* rmark; // sessions (by first sorted position) whose flags changed
+	uint32_t* rlist; // the same as a list: the next round's walk
 };
 
 struct Dev {

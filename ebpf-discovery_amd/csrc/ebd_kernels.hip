@@ -507,8 +507,9 @@ struct LaneEv {
 	v4u src;          // the session's source address (DiscoverySockSourceIP), classified by finalize
 };
 
-// The next event as loaded: its words stay in flight until the lane first needs the event
-// (lane_ev), one or more windows later, so taking a new event never waits for memory.
+// An event's words as loaded (lane_ev decodes them).  Decoding the next event only where it
+// is first needed (a window later) was measured slower: 3.02 against 2.90 ms per 20 M config-3
+// events, same box.
 struct LaneRaw {
 	uint32_t idx, pf, flags, len; // flags bit 8: past the workgroup's range
 	unsigned long long off;
@@ -801,7 +802,7 @@ void k_fresh(Dev d) {
 	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
 	// the lane's current event (e0) and the next one (e1, whose record arrives early)
 	LaneEv e0 = lane_ev(d, lane_load(d, rb + sl, re));
-	LaneRaw e1 = lane_load(d, rb + kScanLanes + sl, re);
+	LaneEv e1 = lane_ev(d, lane_load(d, rb + kScanLanes + sl, re));
 	uint32_t w0 = 0; // e0's window to scan next
 	uint32_t s = di.init, live = 0;
 	ScanRec sr;
@@ -870,8 +871,8 @@ void k_fresh(Dev d) {
 			} else {
 				break;
 			}
-			e0 = lane_ev(d, e1);
-			e1 = lane_load(d, grab(), re);
+			e0 = e1;
+			e1 = lane_ev(d, lane_load(d, grab(), re));
 		}
 		w0 = 0;
 		s = di.init;
@@ -916,8 +917,7 @@ void k_fresh(Dev d) {
 			} else if (w0 + 1 < nwin(e0)) {
 				na = e0.base, nl = e0.lastp, ni = e0.idx, nw = w0 + 1;
 			} else {
-				const LaneEv n1 = lane_ev(d, e1);
-				na = n1.base, nl = n1.lastp, ni = n1.idx, nw = 0;
+				na = e1.base, nl = e1.lastp, ni = e1.idx, nw = 0;
 			}
 			issue(na, nl, nw);
 			tidx = ni;
@@ -961,8 +961,8 @@ void k_fresh(Dev d) {
 		}
 		push(done, tw);
 		if (done) {
-			e0 = lane_ev(d, e1);
-			e1 = lane_load(d, grab(), re);
+			e0 = e1;
+			e1 = lane_ev(d, lane_load(d, grab(), re));
 			resolve();
 		}
 	}
@@ -1512,14 +1512,17 @@ __device__ __forceinline__ void session_carry_out(const Dev& d, const SessState&
 // rounds' walks): no outputs, only each event's LRU operation in ops[j].  The header-key trie
 // and the byte classes sit in LDS: the walk reads them once per byte.
 template <bool DRY>
-__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, uint8_t* ops) {
+__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, uint8_t* ops, const uint32_t* hlist,
+		const uint32_t* hcount) {
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
 		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
 	__syncthreads();
 	const LdsTable T{tabs};
 	const ByteTab A{tabs + kLdsTableBytes};
-	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
+	// the sessions to walk: every one (k_walk_heads), or the list an exact-LRU round changed
+	const uint32_t* heads = hlist ? hlist : d.heads;
+	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	const uint32_t stride = gridDim.x * kWalkThreads;
 	// A lane walks its sessions one 16-byte block per iteration.  A lane whose event ended
 	// waits until 60 of the 64 lanes have (or none is still parsing); then the wave ends those
@@ -1558,7 +1561,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 			}
 			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
 				if (!have) {
-					jhead = jj = d.heads[h];
+					jhead = jj = heads[h];
 					grp = (uint32_t)(d.slow_keys[jj] >> 32);
 					session_begin(d, S, jj, d.ev_slot[slow_event(d, jj)]);
 					have = true;
@@ -1921,24 +1924,27 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 
 // ---------------------------------------------------------------------------------
 // Exact LRU in rounds (the parallel form of k_walk_lru).  A world is a set of evictions, as
-// flags on the session events at which a session finds itself evicted (k_walk's evf).  Each
-// round walks every session in the current world without output (k_walk<true>), which gives
-// every session event its LRU operation, then derives the evictions those operations imply:
+// flags on the session events at which a session finds itself evicted (k_walk's evf).  A
+// round walks sessions in the current world without output (k_walk<true>), which gives every
+// session event its LRU operation, then derives the evictions those operations imply:
 //  * the LRU's size after each event follows from the operation types alone: an insert makes
 //    it min(cap, L + 1) (a full cache evicts first, LRUCache.h:54-60), an erase L - 1.  Maps
 //    x -> min(a, x + b) compose within their family, so the sizes come from a scan over event
 //    order (k_lru_scan_*), and an insert evicts exactly when the size before it is cap;
 //  * an eviction removes the least recently used session.  Every insert or access starts a
-//    "marker" (the session's recency) that lasts until the session's next operation; the
-//    evicted session is the oldest marker still alive, and since evictions only ever take the
-//    oldest, they take markers in position order: one merge of the markers (carried sessions
-//    first, by recency) with the eviction times (k_lru_greedy).
-// The victim's next find (the first event at which its absence shows) gets the eviction flag.
-// When a round derives the world it walked, that world is the sequential execution.  If the
-// walked flags first differ from the sequential ones at event T, the operations before T are
-// the sequential ones, so are the evictions before T and their victims, and so every derived
-// flag up to T: each round settles at least one more event (tests/test_lru_rounds.py restates
-// the rounds and checks them against a sequential LRU).
+//    "marker" (the session's recency) that lasts until the session's next find; the evicted
+//    session is the oldest marker still alive, and since evictions only ever take the oldest,
+//    they take markers in position order: one merge of the markers (carried sessions first,
+//    by recency) with the eviction times (k_lru_greedy).
+// The victim's next find (where its absence shows) gets the eviction flag.  If the walked
+// flags first differ from the sequential ones at event T, the operations before T are the
+// sequential ones, so are the evictions before T, their victims, and every derived flag up
+// to T: each round settles at least one more event, and a round that derives the world it
+// walked has found the sequential execution (tests/test_lru_rounds.py restates the rounds and
+// checks them against a sequential LRU).  A victim's absence shows at its next find, about one
+// inter-event gap of a session later, so that is how far a round moves the settled frontier F.
+// A round therefore only derives the evictions in a window [F, F + H) (the greedy resumes at
+// F from its saved state) and only walks again the sessions whose flags changed.
 // ---------------------------------------------------------------------------------
 constexpr int kLsT = 256, kLsPer = 16;
 constexpr uint32_t kLsBlk = kLsT * kLsPer; // events per scan block
@@ -1954,16 +1960,13 @@ __device__ __forceinline__ LFn lfn_then(LFn f, LFn g) { return LFn{min(g.a, f.a 
 __device__ __forceinline__ long long lfn_apply(LFn f, long long x) { return min(f.a, x + f.b); }
 __device__ __forceinline__ bool op_marks(uint32_t op) { return op == OP_INSERT || op == OP_ACCESS; }
 
-// Event-ordered operations (opt, zeroed before), each marker's end, and per carried session
-// its first marker's end and its first sorted position (cm_end, cm_head: kNone before).  A
-// marker ends at its session's next find (Discovery.cpp:114 for a buffer, :195 for a close),
-// whatever that event did in the world walked: a session evicted before it misses there.
-__global__ void k_lru_mark(Dev d, uint32_t nslow, const uint8_t* ops, uint8_t* opt, uint32_t* mend, uint32_t* cm_end,
-		uint32_t* cm_head) {
+// Once per batch: each session event's next find (Discovery.cpp:114 for a buffer, :195 for a
+// close) in mend (by event), and per carried session its first find and first sorted
+// position (cm_end, cm_head: kNone before).
+__global__ void k_lru_static(Dev d, uint32_t nslow, uint32_t* mend, uint32_t* cm_end, uint32_t* cm_head) {
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x) {
 		const unsigned long long key = d.slow_keys[j];
-		const uint32_t grp = (uint32_t)(key >> 32), i = (uint32_t)key, op = ops[j];
-		opt[i] = (uint8_t)op;
+		const uint32_t grp = (uint32_t)(key >> 32), i = (uint32_t)key;
 		auto next_find = [&](uint32_t from) {
 			for (uint32_t q = from; q < nslow && (uint32_t)(d.slow_keys[q] >> 32) == grp; q++) {
 				const uint32_t iq = (uint32_t)d.slow_keys[q], fl = d.ev[iq].flags, L = d.len[iq];
@@ -1972,8 +1975,7 @@ __global__ void k_lru_mark(Dev d, uint32_t nslow, const uint8_t* ops, uint8_t* o
 			}
 			return kNone;
 		};
-		if (op_marks(op))
-			mend[i] = next_find(j + 1);
+		mend[i] = next_find(j + 1);
 		const bool headj = j == 0 || (uint32_t)(d.slow_keys[j - 1] >> 32) != grp;
 		if (headj && grp < d.carry_cap) { // a carried session (its group is its carry index)
 			cm_head[grp] = j;
@@ -1994,6 +1996,21 @@ __global__ void k_lru_carry_rank(Dev d, const uint32_t* cm_end, uint32_t* mk_ref
 		}
 		mk_ref[rank] = 0x80000000u | c;
 		mk_e[rank] = cm_end[c];
+	}
+}
+
+// The walked sessions' operations by event (opt): every session (hlist == nullptr) or the list.
+__global__ void k_lru_opt(Dev d, uint32_t nslow, const uint8_t* ops, const uint32_t* hlist, const uint32_t* hcount, uint8_t* opt) {
+	if (!hlist) {
+		for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
+			opt[(uint32_t)d.slow_keys[j]] = ops[j];
+		return;
+	}
+	const uint32_t nh = *hcount;
+	for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
+		const uint32_t j0 = hlist[h], grp = (uint32_t)(d.slow_keys[j0] >> 32);
+		for (uint32_t j = j0; j < nslow && (uint32_t)(d.slow_keys[j] >> 32) == grp; j++)
+			opt[(uint32_t)d.slow_keys[j]] = ops[j];
 	}
 }
 
@@ -2105,7 +2122,8 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uin
 		be[blockIdx.x] = tot;
 }
 
-// Phase 4 (one thread): each block's first eviction index.
+// Phase 4 (one thread): each block's first eviction index; tot[5] = the evictions before the
+// frontier (k_lru_compact sets it when the frontier lies inside the batch).
 __global__ void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot) {
 	if (blockIdx.x || threadIdx.x)
 		return;
@@ -2115,11 +2133,12 @@ __global__ void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff,
 		e += be[b];
 	}
 	tot[1] = e;
+	tot[5] = e;
 }
 
 // Phase 5: the markers (event position, end) and the eviction times, in event order.
 __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const uint32_t* mend, const uint8_t* evt, uint32_t n,
-		const uint32_t* moff, const uint32_t* eoff, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t) {
+		const uint32_t* moff, const uint32_t* eoff, uint32_t front, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* tot) {
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
 	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
@@ -2131,13 +2150,15 @@ __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const 
 		nm += op_marks(opt[i]) ? 1u : 0u;
 		ne += evt[i];
 	}
-	uint32_t tot;
-	uint32_t m = moff[blockIdx.x] + u32_block_excl(nm, S, &tot);
-	uint32_t e = eoff[blockIdx.x] + u32_block_excl(ne, S, &tot);
+	uint32_t tot_;
+	uint32_t m = moff[blockIdx.x] + u32_block_excl(nm, S, &tot_);
+	uint32_t e = eoff[blockIdx.x] + u32_block_excl(ne, S, &tot_);
 	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
 		const unsigned long long i = base + k;
 		if (i >= n)
 			break;
+		if (i == front)
+			tot[5] = e; // evictions before the frontier
 		if (op_marks(opt[i])) {
 			mk_ref[m] = (uint32_t)i;
 			mk_e[m] = mend[i];
@@ -2148,74 +2169,171 @@ __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const 
 	}
 }
 
-// Phase 6 (one wave): each eviction takes the oldest marker alive at its time; the victim's
-// next event (or its session's end, or its carry entry) gets the eviction flag.  cnt[0] =
-// evictions, cnt[1] = 1 when the operations are inconsistent (a full cache with no victim).
-__global__ __launch_bounds__(64) void k_lru_greedy(const uint32_t* mk_ref, const uint32_t* mk_e, const uint32_t* tot,
-		const uint32_t* ev_t, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head, uint8_t* nf, uint8_t* ncf,
-		unsigned long long* cnt) {
-	const uint32_t lane = threadIdx.x;
-	const uint32_t nmk = tot[0], nev = tot[1];
-	uint32_t wb = 0, qf = 0; // window base (markers [wb, wb + 64) in registers), queue front
-	uint32_t r = lane < nmk ? mk_ref[lane] : 0u, e = lane < nmk ? mk_e[lane] : 0u;
-	uint32_t bad = 0;
-	for (uint32_t j0 = 0; j0 < nev && !bad; j0 += 64) {
-		const uint32_t tv = j0 + lane < nev ? ev_t[j0 + lane] : 0u;
-		const uint32_t nj = min(64u, nev - j0);
-		for (uint32_t jl = 0; jl < nj && !bad; jl++) {
-			const uint32_t t = __shfl(tv, (int)jl);
-			for (;;) {
-				const bool live = wb + lane >= qf && wb + lane < nmk && (e == kNone || e > t);
-				const unsigned long long b = __ballot(live);
-				if (b == 0) {
-					wb += 64;
-					if (wb >= nmk) {
-						bad = 1;
-						break;
-					}
-					qf = wb;
-					r = wb + lane < nmk ? mk_ref[wb + lane] : 0u;
-					e = wb + lane < nmk ? mk_e[wb + lane] : 0u;
-					continue;
-				}
-				const uint32_t k = (uint32_t)__builtin_ctzll(b);
-				const uint32_t vr = __shfl(r, (int)k), ve = __shfl(e, (int)k);
-				qf = wb + k + 1;
-				if (!(vr & 0x80000000u) && vr >= t) { // the oldest live marker is not older than the insert
-					bad = 1;
+// Phase 6 (one workgroup): the evictions of the window [front, tend), from eviction tot[5] on,
+// each take the oldest marker alive at their time.  The queue front after the evictions
+// before j is qfe[j] (kept from the round that processed them: the evictions and markers
+// before the frontier do not change), so the merge resumes there.  All threads stage the
+// markers' ends and the eviction times in LDS; wave 0 merges, 64 evictions at a time: one
+// ballot per eviction gives the LDS window's markers alive at its time (a lane keeps the mask
+// of its eviction), then the victims follow one another in scalar registers (each is the
+// first alive marker after the previous victim).  vict[j] = eviction j's marker; tot[2] = the
+// window's end (first eviction not processed).  cnt[1] = 1: the operations are inconsistent
+// (a full cache with no victim).
+constexpr uint32_t kGrM = 8192, kGrE = 2048; // markers / evictions staged in LDS at a time
+__global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const uint32_t* ev_t, uint32_t* tot, uint32_t tend,
+		uint32_t* vict, uint32_t* qfe, unsigned long long* cnt) {
+	__shared__ uint32_t se[kGrM], sv[kGrE];
+	__shared__ uint32_t s_qf, s_j, s_more, s_bad;
+	const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+	const uint32_t nmk = tot[0], nev = tot[1], j0 = tot[5];
+	if (t == 0) {
+		s_qf = j0 ? qfe[j0] : 0u;
+		s_j = j0;
+		s_bad = 0;
+		s_more = j0 < nev;
+	}
+	__syncthreads();
+	while (s_more) {
+		const uint32_t mb = s_qf & ~63u, eb = s_j; // stage markers from the front's window, evictions from s_j
+		for (uint32_t k = t; k < kGrM; k += 256)
+			se[k] = mb + k < nmk ? mk_e[mb + k] : 0u;
+		for (uint32_t k = t; k < kGrE; k += 256)
+			sv[k] = eb + k < nev ? ev_t[eb + k] : ~0u;
+		__syncthreads();
+		if (wave == 0) {
+			uint32_t qf = s_qf, j = eb, bad = 0, restage = 0, stop = 0;
+			const uint32_t jlim = min(nev, eb + kGrE);
+			while (j < jlim && !bad && !restage && !stop) {
+				const uint32_t nj0 = min(64u, jlim - j);
+				const uint32_t tv = lane < nj0 ? sv[j - eb + lane] : ~0u;
+				const uint32_t nj = (uint32_t)__popcll(__ballot(lane < nj0 && tv < tend)); // times ascend
+				if (nj == 0) {
+					stop = 1; // the window ends at eviction j
 					break;
 				}
-				if (lane == 0) {
-					if (ve != kNone) {
-						nf[jpos[ve]] |= 1u; // find() misses at the session's next operation
-					} else if (vr & 0x80000000u) {
-						const uint32_t c = vr & 0x7fffffffu;
-						if (cm_head[c] != kNone)
-							nf[cm_head[c]] |= 2u;
-						else
-							ncf[c] = 1;
-					} else {
-						nf[head[jpos[vr]]] |= 2u; // after the session's last event: not carried out
+				uint32_t k = 0;
+				while (k < nj) {
+					const uint32_t wb = qf & ~63u;
+					if (wb >= nmk) {
+						bad = 1; // a full cache and no live marker
+						break;
 					}
+					if (wb + 64 > mb + kGrM) {
+						restage = 1; // the staged markers are used up
+						break;
+					}
+					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
+					unsigned long long mine = 0; // the alive mask of this lane's eviction (lanes k .. nj-1)
+					for (uint32_t jl = k; jl < nj; jl++) {
+						const uint32_t tt = __shfl(tv, (int)jl);
+						const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt));
+						mine = lane == jl ? m : mine;
+					}
+					uint32_t p = qf - wb, jl = k;
+					for (; jl < nj; jl++) {
+						const unsigned long long m = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, (int)jl) |
+								((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), (int)jl) << 32);
+						const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
+						if (avail == 0)
+							break;
+						const uint32_t v = (uint32_t)__builtin_ctzll(avail);
+						if (lane == jl) {
+							vict[j + jl] = wb + v;
+							qfe[j + jl] = wb + p; // the front before this eviction
+						}
+						p = v + 1;
+					}
+					// eviction jl finds no live marker in this window: none of its markers lives
+					// on for it or any later eviction, so the front moves to the next window
+					qf = jl < nj ? wb + 64 : wb + p;
+					k = jl;
 				}
-				break;
+				j += k;
+			}
+			if (lane == 0) {
+				s_qf = qf;
+				s_j = j;
+				s_bad = bad;
+				s_more = !bad && !stop && j < nev;
 			}
 		}
+		__syncthreads();
 	}
-	if (lane == 0) {
-		cnt[0] = bad ? 0ull : (unsigned long long)nev;
-		cnt[1] = bad;
+	if (t == 0) {
+		qfe[s_j] = s_qf; // the front after the window: where the next window resumes
+		tot[2] = s_j;
+		cnt[0] = nev;
+		if (s_bad)
+			atomicOr((uint32_t*)&cnt[1], 1u);
 	}
 }
 
-// Phase 7: how many flags the round changed.
+// Phase 6b: the world the evictions before the window's end imply, by event (nf_t zeroed
+// before): the victim's next find, or the victims with none (tot[4] of them) in vic.
+__global__ void k_lru_victims(const uint32_t* tot, const uint32_t* vict, const uint32_t* mk_ref, const uint32_t* mk_e,
+		const uint32_t* ev_t, uint8_t* nf_t, uint32_t* vic, uint32_t* vtot, unsigned long long* cnt) {
+	const uint32_t ne = tot[2];
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
+		const uint32_t q = vict[j], vr = mk_ref[q], ve = mk_e[q];
+		if (!(vr & 0x80000000u) && vr >= ev_t[j])
+			atomicOr((uint32_t*)&cnt[1], 1u); // the oldest live marker is not older than the insert
+		if (ve != kNone)
+			nf_t[ve] = 1; // find() misses at the session's next find
+		else
+			vic[atomicAdd(vtot, 1u)] = vr;
+	}
+}
+
+// Phase 6c: the round's flags by sorted position: bit 0 from nf_t, then bit 1 (after the
+// session's last event) or the carry flag for the listed victims (ncf zeroed before).
+__global__ void k_lru_flags(Dev d, uint32_t nslow, const uint8_t* nf_t, uint8_t* nf) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
+		nf[j] = nf_t[(uint32_t)d.slow_keys[j]];
+}
+__global__ void k_lru_tails(const uint32_t* vtot, const uint32_t* vic, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head,
+		uint8_t* nf, uint8_t* ncf) {
+	const uint32_t nv = *vtot;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nv; k += gridDim.x * blockDim.x) {
+		const uint32_t vr = vic[k];
+		if (vr & 0x80000000u) {
+			const uint32_t c = vr & 0x7fffffffu;
+			if (cm_head[c] != kNone)
+				nf[cm_head[c]] |= 2u;
+			else
+				ncf[c] = 1;
+		} else {
+			nf[head[jpos[vr]]] |= 2u; // after the session's last event: not carried out
+		}
+	}
+}
+
+// Phase 7: how many flags the round changed (cnt[2]), the first event whose eviction bit
+// changed (cnt[3]: the new frontier), and the sessions the next round walks again (rmark).
 __global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, const uint8_t* cf, const uint8_t* ncf, uint32_t n2,
-		unsigned long long* cnt) {
-	uint32_t x = 0;
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x)
-		x += k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
+		const unsigned long long* keys, const uint32_t* head, uint8_t* rmark, unsigned long long* cnt) {
+	uint32_t x = 0, first = kNone;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x) {
+		const bool dk = k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
+		x += dk ? 1u : 0u;
+		if (k < n1 && ((f[k] ^ nf[k]) & 1u)) { // the walk changes only with bit 0
+			rmark[head[k]] = 1;
+			const uint32_t tk = (uint32_t)keys[k];
+			first = tk < first ? tk : first;
+		}
+	}
 	if (__any(x != 0))
 		wave_add(&cnt[2], (unsigned long long)x);
+	if (first != kNone)
+		atomicMin(&cnt[3], (unsigned long long)first);
+}
+
+// The sessions the next round walks again (rmark, by first sorted position; cleared here).
+__global__ void k_lru_rlist(uint32_t nslow, uint8_t* rmark, uint32_t* rlist, uint32_t* tot) {
+	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
+		if (rmark[j]) {
+			rmark[j] = 0;
+			rlist[atomicAdd(&tot[3], 1u)] = j;
+		}
 }
 
 // Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
@@ -3181,31 +3299,54 @@ hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d,
-			(const uint8_t*)nullptr, (uint8_t*)nullptr);
+			(const uint8_t*)nullptr, (uint8_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 
 	return hipGetLastError();
 }
-// One exact-LRU round (k_lru_* above) after a dry walk in the world of flags f / cf: the
-// derived world in nf / ncf (zeroed here), cnt[0] evictions, cnt[1] inconsistency, cnt[2] the
-// flags that changed.  scratch: LruRound's arrays.
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, hipStream_t st, int cus) {
+// The exact-LRU rounds' once-per-batch part: heads, event -> sorted position, next finds,
+// carried markers, empty operations.
+hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus) {
+	hipError_t e;
+	if ((e = hipMemsetAsync(w.jpos, 0xff, (size_t)d.n * sizeof(uint32_t), st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cm_end, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.opt, 0, d.n, st)) != hipSuccess || (e = hipMemsetAsync(w.f[0], 0, nslow, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
+	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.jpos, w.head);
+	hipLaunchKernelGGL(k_lru_static, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.mend, w.cm_end, w.cm_head);
+	if (d.n_carry_in)
+		hipLaunchKernelGGL(k_lru_carry_rank, dim3(grid_for(d.n_carry_in, 256, cus * 4)), dim3(256), 0, st, d, (const uint32_t*)w.cm_end,
+				w.mk_ref, w.mk_e);
+	return hipGetLastError();
+}
+
+// One exact-LRU round after a dry walk in the world f / cf (every session when nwalk ==
+// kNone, else the nwalk sessions of the last round's list): the world the evictions of
+// [front, front + window) and all earlier ones imply in nf / ncf; cnt[1] inconsistency,
+// cnt[2] flags changed, cnt[3] the new frontier.
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t nwalk, uint32_t front, uint32_t window,
+		hipStream_t st, int cus) {
 	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
 	const uint8_t* f = w.f[cur];
 	uint8_t* nf = w.f[cur ^ 1];
 	const uint8_t* cf = w.cf[cur];
 	uint8_t* ncf = w.cf[cur ^ 1];
-	hipLaunchKernelGGL(k_walk<true>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f, w.ops);
+	const bool all = nwalk == kNone;
+	if (all || nwalk) {
+		const uint32_t g = grid_for(all ? nslow : nwalk, kWalkThreads, cus * EBD_WALK_BLOCKS);
+		hipLaunchKernelGGL(k_walk<true>, dim3(g), dim3(kWalkThreads), 0, st, d, f, w.ops, all ? (const uint32_t*)nullptr : (const uint32_t*)w.rlist,
+				(const uint32_t*)(w.tot + 3));
+		hipLaunchKernelGGL(k_lru_opt, dim3(grid_for(all ? nslow : nwalk, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.ops,
+				all ? (const uint32_t*)nullptr : (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3), w.opt);
+	}
 	hipError_t e;
-	if ((e = hipMemsetAsync(w.opt, 0, n, st)) != hipSuccess || (e = hipMemsetAsync(w.cm_end, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
-			(e = hipMemsetAsync(nf, 0, nslow, st)) != hipSuccess || (e = hipMemsetAsync(ncf, 0, d.carry_cap, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cnt, 0, 4 * sizeof(unsigned long long), st)) != hipSuccess)
+	if ((e = hipMemsetAsync(ncf, 0, d.carry_cap, st)) != hipSuccess || (e = hipMemsetAsync(w.nf_t, 0, n, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.tot + 4, 0, sizeof(uint32_t), st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cnt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cnt + 3, 0xff, sizeof(unsigned long long), st)) != hipSuccess)
 		return e;
-	hipLaunchKernelGGL(k_lru_mark, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.ops, w.opt, w.mend,
-			w.cm_end, w.cm_head);
-	if (nc)
-		hipLaunchKernelGGL(k_lru_carry_rank, dim3(grid_for(nc, 256, cus * 4)), dim3(256), 0, st, d, (const uint32_t*)w.cm_end, w.mk_ref,
-				w.mk_e);
 	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm);
 	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(1), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
 			w.moff, w.tot);
@@ -3213,25 +3354,29 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 			w.evt, w.be);
 	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(1), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
 	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
-			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, w.mk_ref, w.mk_e, w.ev_t);
-	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(64), 0, st, (const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.tot,
-			(const uint32_t*)w.ev_t, (const uint32_t*)w.jpos, (const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf, w.cnt);
+			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, front, w.mk_ref, w.mk_e, w.ev_t, w.tot);
+	const unsigned long long tend = (unsigned long long)front + window;
+	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot,
+			(uint32_t)(tend < 0xffffffffull ? tend : 0xffffffffull), w.vict, w.qfe, w.cnt);
+	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
+			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.nf_t, w.vic, w.tot + 4, w.cnt);
+	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.nf_t, nf);
+	hipLaunchKernelGGL(k_lru_tails, dim3(cus), dim3(256), 0, st, (const uint32_t*)(w.tot + 4), (const uint32_t*)w.vic, (const uint32_t*)w.jpos,
+			(const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf);
 	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(nslow + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, f, (const uint8_t*)nf, nslow, cf,
-			(const uint8_t*)ncf, d.carry_cap, w.cnt);
+			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.rmark, w.cnt);
+	if ((e = hipMemsetAsync(w.tot + 3, 0, sizeof(uint32_t), st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_lru_rlist, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, nslow, w.rmark, w.rlist, w.tot);
 	return hipGetLastError();
 }
 // The final walk of the exact path in the converged world (with output), then the carried
 // sessions it did not meet.
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f,
-			(uint8_t*)nullptr);
+			(uint8_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 	if (d.n_carry_in)
 		hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, cf);
-	return hipGetLastError();
-}
-hipError_t launch_walk_heads(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
-	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, jpos, head);
 	return hipGetLastError();
 }
 size_t lru_scan_blocks(uint32_t n) { return (n + kLsBlk - 1) / kLsBlk; }

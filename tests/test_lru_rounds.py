@@ -83,8 +83,9 @@ def walk(ev, carried, flags, tail, cflag):
     return ops, left
 
 
-def derive(ev, carried, ops, cap):
-    """k_lru_mark / scan / compact / greedy: the evictions the operations imply, as flags."""
+def derive(ev, carried, ops, cap, tend=None):
+    """k_lru_static / scan / compact / greedy / victims: the evictions the operations imply
+    (those before tend, when given), as flags."""
     n = len(ev)
     # marker ends: the session's next find (an event with a buffer, or a close), whatever it
     # did in this world (a find of an evicted session misses and does nothing)
@@ -109,6 +110,8 @@ def derive(ev, carried, ops, cap):
     flags, tail, cflag = [False] * n, {}, {}
     q = 0
     for t in evictions:
+        if tend is not None and t >= tend:
+            break
         while q < len(markers) and not (markers[q][1] is None or markers[q][1] > t):
             q += 1
         assert q < len(markers) and markers[q][0] < t
@@ -132,6 +135,42 @@ def rounds(ev, carried, cap, max_rounds=500):
             return ops, nev, left, r
         flags, tail, cflag = nf, nt, nc
     raise AssertionError("rounds did not settle")
+
+
+def rounds_windowed(ev, carried, cap, window, max_rounds=20000):
+    """run_lru_rounds' schedule: events before the frontier are settled; a round derives the
+    evictions before front + window and moves the frontier to the first changed flag (or past
+    the window when nothing changed)."""
+    n = len(ev)
+    flags, tail, cflag = [False] * n, {}, {}
+    front = 0
+    for r in range(1, max_rounds + 1):
+        ops, left = walk(ev, carried, flags, tail, cflag)
+        wend = front + window
+        nf, nt, nc, nev = derive(ev, carried, ops, cap, tend=wend)
+        changed = nf != flags or nt != tail or nc != cflag
+        if not changed and wend >= n:
+            return ops, nev, left, r
+        if not changed:
+            front = wend
+        else:
+            first = next((t for t in range(n) if nf[t] != flags[t]), None)
+            if first is not None:
+                assert first >= front  # settled events never change
+                front = min(first, wend)
+        flags, tail, cflag = nf, nt, nc
+    raise AssertionError("rounds did not settle")
+
+
+@pytest.mark.parametrize("seed,cap,sessions,window", [(1, 8, 40, 50), (2, 16, 100, 300), (3, 64, 500, 1000), (7, 5, 30, 7)])
+def test_windowed_rounds_equal_sequential_lru(seed, cap, sessions, window):
+    rng = np.random.default_rng(seed)
+    ev, car = make_trace(rng, sessions, 3000, min(cap, 5))
+    want_ops, want_ev, want_left = sequential(ev, car, cap)
+    ops, nev, left, r = rounds_windowed(ev, car, cap, window)
+    assert ops == want_ops
+    assert nev == want_ev
+    assert sorted(left) == sorted(want_left)
 
 
 @pytest.mark.parametrize("seed,cap,sessions,carried", [(1, 8, 40, 0), (2, 16, 100, 10), (3, 64, 500, 64), (4, 5, 30, 5),

@@ -3,11 +3,13 @@
 
   python tools/pmc_fetch_json.py --fetch <dir> [--write <dir>] --events N --config C --out profiles/x.json
 
-FETCH_SIZE and WRITE_SIZE are rocprofv3's derived counters in KiB.  The guide's gfx950 x2
-correction (MI355X_MICROARCH.md, HBM / rocprofv3) is calibrated for wide coalesced streaming
-reads; it does not hold for k_fresh's access pattern: the scan-only build (EBD_EXP_NOFIN)
-reports a raw FETCH_SIZE equal to the bytes it must read (payload + event metadata), so the
-default scale here is 1 (--fetch-scale 2 applies the guide's correction).
+FETCH_SIZE and WRITE_SIZE are rocprofv3's derived counters in KiB.  How many bytes a FETCH_SIZE
+KiB stands for depends on the load shape (profiles/r04_fetch_calibration.json: streams of known
+bytes, tools/ubench_stream under one --pmc FETCH_SIZE pass): x1.99 for 16 B per lane over
+consecutive addresses and x2.09 for LDS-DMA tiles (the guide's x2 rule, MI355X_MICROARCH.md HBM /
+rocprofv3), x1.25 for k_fresh's shape (a quad's 64-byte windows on the 64-byte grid, no work),
+x1.19 for the same with the DFA-like work, x1.03 for buffer-relative 64-byte windows.  The
+default scale is therefore 1.25 (round 3 used 1, from a round-1 scan-only build).
 """
 import argparse
 import collections
@@ -35,7 +37,7 @@ def main():
     ap.add_argument("--config", type=int, required=True)
     ap.add_argument("--kernel", default="k_fresh")
     ap.add_argument("--out", required=True)
-    ap.add_argument("--fetch-scale", type=float, default=1.0)
+    ap.add_argument("--fetch-scale", type=float, default=1.25)
     ap.add_argument("--build-id", required=True, help="ebd.build_id() of the library the passes measured")
     a = ap.parse_args()
     fkib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
@@ -49,8 +51,9 @@ def main():
         out["hbm_write_bytes_per_launch"] = wkib * 1024
         total += wkib * 1024
     out["hbm_bytes_per_launch"] = total
-    out["note"] = ("FETCH_SIZE x 1024 x fetch_scale + WRITE_SIZE x 1024, averaged over the launches; scale 1 is "
-                   "calibrated on this kernel: the scan-only build's raw FETCH_SIZE equals its payload + metadata bytes")
+    out["note"] = ("FETCH_SIZE x 1024 x fetch_scale + WRITE_SIZE x 1024, averaged over the launches; fetch_scale is "
+                   "measured on a stream of k_fresh's load shape with known bytes (profiles/r04_fetch_calibration.json: "
+                   "x1.25; x2 for plain 16-B-per-lane streams, the guide's rule)")
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))

@@ -82,8 +82,8 @@ def main():
 		if (done) { // the last chunk""")
     s = sub(s, """		push(done, tw);
 		if (done) {
-			e0 = lane_ev(d, e1);
-			e1 = lane_load(d, grab(), re);
+			e0 = e1;
+			e1 = lane_ev(d, lane_load(d, grab(), re));
 			resolve();
 		}
 	}
@@ -92,8 +92,8 @@ def main():
 		unsigned long long Q4 = clock64();
 		S_push += Q4 - Q3;
 		if (done) {
-			e0 = lane_ev(d, e1);
-			e1 = lane_load(d, grab(), re);
+			e0 = e1;
+			e1 = lane_ev(d, lane_load(d, grab(), re));
 			resolve();
 		}
 		S_res += clock64() - Q4;
