@@ -619,7 +619,7 @@ static int lru_alloc(ebd_ctx* c) {
 		total += (z + 255) & ~(size_t)255;
 	HIP_TRY(hipMalloc(&c->lr_mem, total));
 	if (!c->h_lr)
-		HIP_TRY(hipHostMalloc(&c->h_lr, 6 * sizeof(unsigned long long), hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc(&c->h_lr, 8 * sizeof(unsigned long long), hipHostMallocDefault));
 	uint8_t* p = (uint8_t*)c->lr_mem;
 	void* ptrs[29];
 	for (int k = 0; k < 29; k++) {
@@ -673,7 +673,7 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	LruRound& w = c->lr;
 	HIP_TRY(launch_lru_init(d, nslow, w, c->stream, c->cus));
 	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
-	const uint32_t window = 1u << 16;
+	const uint32_t window = 1u << 14; // a round settles about one session inter-event gap (config 4: ~4 k events)
 	int cur = 0;
 	uint32_t nwalk = kNone, front = 0; // the first round walks every session
 	const int max_rounds = 4096;

@@ -1538,7 +1538,9 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 	DfaWalk w;
 	uint32_t pos0 = 0, ne = 0, k0 = 0, nb = 0, bi = 0;
 	uintptr_t b0 = 0;
-	uint4 cur = uint4{0u, 0u, 0u, 0u};
+	// the event's next four 16-byte blocks: a block's walk is far shorter than a load's latency,
+	// so one block in flight left every block of a fragment paying the full latency
+	uint4 cur = uint4{0u, 0u, 0u, 0u}, n1 = cur, n2 = cur, n3 = cur;
 	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
 	unsigned long long pf_off = 0;
 	for (;;) {
@@ -1598,8 +1600,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 						k0 = (uint32_t)(p & 15u);
 						nb = ne ? (k0 + ne + 15u) >> 4 : 0u;
 						bi = 0;
-						if (nb)
+						if (nb) {
 							cur = *(const uint4*)b0;
+							n1 = nb > 1 ? *(const uint4*)(b0 + 16u) : cur;
+							n2 = nb > 2 ? *(const uint4*)(b0 + 32u) : cur;
+							n3 = nb > 3 ? *(const uint4*)(b0 + 48u) : cur;
+						}
 						in_ev = true;
 					} else {
 						const uint32_t op = ev_end<DRY>(d, S, e, 0);
@@ -1617,11 +1623,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 		}
 		if (in_ev) {
 			if (bi < nb) { // one block (dfa_parse_dev's)
-				const uint4 nx = bi + 1 < nb ? *(const uint4*)(b0 + 16u * (bi + 1)) : cur;
+				const uint4 nx = bi + 4 < nb ? *(const uint4*)(b0 + 16u * (bi + 4)) : cur;
 				const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
 				const uint32_t base = 16u * bi - k0;
 				dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
-				cur = nx;
+				cur = n1;
+				n1 = n2;
+				n2 = n3;
+				n3 = nx;
 				bi++;
 			}
 			if (bi >= nb || w.tpos != kNone) {
@@ -2173,22 +2182,22 @@ __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const 
 // each take the oldest marker alive at their time.  The queue front after the evictions
 // before j is qfe[j] (kept from the round that processed them: the evictions and markers
 // before the frontier do not change), so the merge resumes there.  All threads stage the
-// markers' ends and the eviction times in LDS; wave 0 merges, 64 evictions at a time: one
-// ballot per eviction gives the LDS window's markers alive at its time (a lane keeps the mask
-// of its eviction), then the victims follow one another in scalar registers (each is the
-// first alive marker after the previous victim).  vict[j] = eviction j's marker; tot[2] = the
+// markers' ends and the eviction times in LDS; wave 0 merges: one ballot per eviction gives
+// the 64-marker window's markers alive at its time, and the victim is the first of them after
+// the previous victim (a window with none moves the front on by 64).  vict[j] = eviction j's marker; tot[2] = the
 // window's end (first eviction not processed).  cnt[1] = 1: the operations are inconsistent
 // (a full cache with no victim).
 constexpr uint32_t kGrM = 8192, kGrE = 2048; // markers / evictions staged in LDS at a time
 __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const uint32_t* ev_t, uint32_t* tot, uint32_t tend,
 		uint32_t* vict, uint32_t* qfe, unsigned long long* cnt) {
 	__shared__ uint32_t se[kGrM], sv[kGrE];
-	__shared__ uint32_t s_qf, s_j, s_more, s_bad;
+	__shared__ uint32_t s_qf, s_j, s_more, s_bad, s_rec;
 	const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
 	const uint32_t nmk = tot[0], nev = tot[1], j0 = tot[5];
 	if (t == 0) {
 		s_qf = j0 ? qfe[j0] : 0u;
 		s_j = j0;
+		s_rec = j0; // evictions before s_rec have their front recorded
 		s_bad = 0;
 		s_more = j0 < nev;
 	}
@@ -2201,7 +2210,7 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 			sv[k] = eb + k < nev ? ev_t[eb + k] : ~0u;
 		__syncthreads();
 		if (wave == 0) {
-			uint32_t qf = s_qf, j = eb, bad = 0, restage = 0, stop = 0;
+			uint32_t qf = s_qf, j = eb, bad = 0, restage = 0, stop = 0, rec = s_rec;
 			const uint32_t jlim = min(nev, eb + kGrE);
 			while (j < jlim && !bad && !restage && !stop) {
 				const uint32_t nj0 = min(64u, jlim - j);
@@ -2223,24 +2232,23 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 						break;
 					}
 					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
-					unsigned long long mine = 0; // the alive mask of this lane's eviction (lanes k .. nj-1)
-					for (uint32_t jl = k; jl < nj; jl++) {
-						const uint32_t tt = __shfl(tv, (int)jl);
-						const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt));
-						mine = lane == jl ? m : mine;
-					}
 					uint32_t p = qf - wb, jl = k;
 					for (; jl < nj; jl++) {
-						const unsigned long long m = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, (int)jl) |
-								((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), (int)jl) << 32);
+						// the front after eviction jl - 1, before any window this eviction skips: a
+						// later round resumes there, and its eviction jl may come earlier
+						if (j + jl >= rec) { // once per eviction, also across a restaging
+							if (lane == jl)
+								qfe[j + jl] = wb + p;
+							rec = j + jl + 1;
+						}
+						const uint32_t tt = __shfl(tv, (int)jl);
+						const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt)); // alive at tt
 						const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
 						if (avail == 0)
 							break;
 						const uint32_t v = (uint32_t)__builtin_ctzll(avail);
-						if (lane == jl) {
+						if (lane == jl)
 							vict[j + jl] = wb + v;
-							qfe[j + jl] = wb + p; // the front before this eviction
-						}
 						p = v + 1;
 					}
 					// eviction jl finds no live marker in this window: none of its markers lives
@@ -2253,6 +2261,7 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 			if (lane == 0) {
 				s_qf = qf;
 				s_j = j;
+				s_rec = rec;
 				s_bad = bad;
 				s_more = !bad && !stop && j < nev;
 			}
