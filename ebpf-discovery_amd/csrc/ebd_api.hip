@@ -30,8 +30,8 @@ hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* m
 hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
 		uint32_t cap, hipStream_t st, int cus);
 size_t sess_state_bytes();
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t nwalk, uint32_t front, uint32_t window,
-		hipStream_t st, int cus);
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t front, uint32_t window, hipStream_t st,
+		int cus);
 hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus);
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus);
 size_t lru_scan_blocks(uint32_t n);
@@ -612,51 +612,28 @@ static int lru_alloc(ebd_ctx* c) {
 	if (c->lr_mem)
 		return 0;
 	const size_t n = c->max_events, cc = c->carry_cap, nb = lru_scan_blocks(c->max_events) + 1;
-	const size_t sizes[] = {n, n, 4 * n, n, 4 * (n + cc), 4 * (n + cc), 4 * n, 4 * cc, 4 * cc, n, n, cc, cc, 16 * nb, 4 * nb, 8 * nb, 4 * nb,
-			4 * nb, 4 * nb, 32, 4 * n, 4 * n, 32, n, 4 * (n + cc), n, 4 * n, 4 * (n + 1), 4 * (n + 1)};
+	LruRound& w = c->lr;
+	struct Part {
+		void** p;
+		size_t bytes;
+	} parts[] = {{(void**)&w.opt, n}, {(void**)&w.mend, 4 * n}, {(void**)&w.evt, n}, {(void**)&w.mk_ref, 4 * (n + cc)},
+			{(void**)&w.mk_e, 4 * (n + cc)}, {(void**)&w.ev_t, 4 * n}, {(void**)&w.cm_end, 4 * cc}, {(void**)&w.cm_head, 4 * cc},
+			{(void**)&w.f[0], n}, {(void**)&w.f[1], n}, {(void**)&w.cf[0], cc}, {(void**)&w.cf[1], cc}, {(void**)&w.bf, 16 * nb},
+			{(void**)&w.bm, 4 * nb}, {(void**)&w.lst, 8 * nb}, {(void**)&w.moff, 4 * nb}, {(void**)&w.be, 4 * nb}, {(void**)&w.eoff, 4 * nb},
+			{(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32}, {(void**)&w.nf_t, n},
+			{(void**)&w.vic, 4 * (n + cc)}, {(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
+			{(void**)&w.qfe, 4 * (n + 1)}, {(void**)&w.wto, 4 * n}, {(void**)&w.snap, sess_state_bytes() * n}};
 	size_t total = 0;
-	for (size_t z : sizes)
-		total += (z + 255) & ~(size_t)255;
+	for (const Part& q : parts)
+		total += (q.bytes + 255) & ~(size_t)255;
 	HIP_TRY(hipMalloc(&c->lr_mem, total));
 	if (!c->h_lr)
 		HIP_TRY(hipHostMalloc(&c->h_lr, 8 * sizeof(unsigned long long), hipHostMallocDefault));
 	uint8_t* p = (uint8_t*)c->lr_mem;
-	void* ptrs[29];
-	for (int k = 0; k < 29; k++) {
-		ptrs[k] = p;
-		p += (sizes[k] + 255) & ~(size_t)255;
+	for (const Part& q : parts) {
+		*q.p = p;
+		p += (q.bytes + 255) & ~(size_t)255;
 	}
-	LruRound& w = c->lr;
-	w.ops = (uint8_t*)ptrs[0];
-	w.opt = (uint8_t*)ptrs[1];
-	w.mend = (uint32_t*)ptrs[2];
-	w.evt = (uint8_t*)ptrs[3];
-	w.mk_ref = (uint32_t*)ptrs[4];
-	w.mk_e = (uint32_t*)ptrs[5];
-	w.ev_t = (uint32_t*)ptrs[6];
-	w.cm_end = (uint32_t*)ptrs[7];
-	w.cm_head = (uint32_t*)ptrs[8];
-	w.f[0] = (uint8_t*)ptrs[9];
-	w.f[1] = (uint8_t*)ptrs[10];
-	w.cf[0] = (uint8_t*)ptrs[11];
-	w.cf[1] = (uint8_t*)ptrs[12];
-	w.bf = ptrs[13];
-	w.bm = (uint32_t*)ptrs[14];
-	w.lst = (long long*)ptrs[15];
-	w.moff = (uint32_t*)ptrs[16];
-	w.be = (uint32_t*)ptrs[17];
-	w.eoff = (uint32_t*)ptrs[18];
-	w.tot = (uint32_t*)ptrs[19];
-	w.jpos = (uint32_t*)ptrs[20];
-	w.head = (uint32_t*)ptrs[21];
-	w.cnt = (unsigned long long*)ptrs[22];
-	w.nf_t = (uint8_t*)ptrs[23];
-	w.vic = (uint32_t*)ptrs[24];
-	w.rmark = (uint8_t*)ptrs[25];
-	w.rlist = (uint32_t*)ptrs[26];
-	w.vict = (uint32_t*)ptrs[27];
-	w.qfe = (uint32_t*)ptrs[28];
-	HIP_TRY(hipMemset(w.rmark, 0, n)); // k_lru_rlist clears what it lists
 	return 0;
 }
 
@@ -675,10 +652,10 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
 	const uint32_t window = 1u << 14; // a round settles about one session inter-event gap (config 4: ~4 k events)
 	int cur = 0;
-	uint32_t nwalk = kNone, front = 0; // the first round walks every session
+	uint32_t front = 0;
 	const int max_rounds = 4096;
 	for (int r = 0; r < max_rounds; r++) {
-		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, nwalk, front, window, c->stream, c->cus); }));
+		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, front, window, c->stream, c->cus); }));
 		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 		HIP_TRY(hipMemcpyAsync(c->h_lr + 4, w.tot, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
 		HIP_TRY(hipStreamSynchronize(c->stream));
@@ -688,7 +665,7 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 		const unsigned long long wend = (unsigned long long)front + window;
 		if (lru_trace)
 			std::fprintf(stderr, "ebd lru round %d: front %u, evictions %u (window to %u), flags changed %llu, first at %lld, walked %u\n", r,
-					front, tot[1], tot[2], changed, first == ~0ull ? -1ll : (long long)first, nwalk == kNone ? nslow : nwalk);
+					front, tot[1], tot[2], changed, first == ~0ull ? -1ll : (long long)first, tot[3]);
 		if (c->h_lr[1]) // operations with a full cache and no victim: not a world to walk on
 			return 0;
 		if (changed == 0 && wend >= d.n) { // the world derived is the world walked, to the batch's end
@@ -700,7 +677,6 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 		else if (first != ~0ull) // events before the first changed flag (and the window's end) are settled
 			front = (uint32_t)(first < wend ? first : wend);
 		cur ^= 1;
-		nwalk = tot[3];
 	}
 	if (!*settled)
 		return 0;

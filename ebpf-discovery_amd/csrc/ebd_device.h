@@ -128,7 +128,6 @@ static_assert(sizeof(ClaimRec) == 24, "claim record is 24 bytes");
 // position, opt by event, marker ends, eviction flags), the compacted markers and eviction
 // times, per carried session, the two worlds of eviction flags, per scan block.
 struct LruRound {
-	uint8_t* ops;
 	uint8_t* opt;
 	uint32_t* mend;
 	uint8_t* evt;
@@ -153,8 +152,10 @@ struct LruRound {
 	uint32_t* vic; // victims with no later find
 	uint32_t* vict; // per eviction: its victim marker
 	uint32_t* qfe;  // per eviction: the marker queue's front before it
-	uint8_t* rmark; // sessions (by first sorted position) whose flags changed
-	uint32_t* rlist; // the same as a list: the next round's walk
+	uint32_t* cpos;  // per session (first sorted position): its first changed position, kNone
+	uint32_t* rlist; // the round's walks: start positions
+	uint32_t* wto;   // per session: where its last walk stopped (kNone: at its end)
+	void* snap;      // per sorted position: the session's state before it (SessState)
 };
 
 struct Dev {

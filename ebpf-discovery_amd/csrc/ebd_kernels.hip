@@ -1511,8 +1511,21 @@ __device__ __forceinline__ void session_carry_out(const Dev& d, const SessState&
 // at a session's first position = evicted after its last event (not carried out).  DRY (the
 // rounds' walks): no outputs, only each event's LRU operation in ops[j].  The header-key trie
 // and the byte classes sit in LDS: the walk reads them once per byte.
+// The exact-LRU rounds' walks (DRY): a list entry is the sorted position a session's walk
+// starts at (its first event, or where its flags changed, from the snapshot of its state
+// there); the walk stops before the first event at or past the horizon hz and leaves where
+// it stopped in wto (kNone: the session's end); the state before each event it walks goes to
+// snap, the event's LRU operation to opt (by event).
+struct DryWalk {
+	const uint32_t* head; // sorted position -> its session's first position
+	SessState* snap;
+	uint32_t* wto;
+	uint8_t* opt;
+	uint32_t hz;
+};
+
 template <bool DRY>
-__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, uint8_t* ops, const uint32_t* hlist,
+__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
 		const uint32_t* hcount) {
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
@@ -1520,7 +1533,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 	__syncthreads();
 	const LdsTable T{tabs};
 	const ByteTab A{tabs + kLdsTableBytes};
-	// the sessions to walk: every one (k_walk_heads), or the list an exact-LRU round changed
+	// the sessions to walk: every one (k_walk_heads), or the exact-LRU round's list
 	const uint32_t* heads = hlist ? hlist : d.heads;
 	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	const uint32_t stride = gridDim.x * kWalkThreads;
@@ -1558,14 +1571,19 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 						wave_add(&d.ctr[CTR_INSERTS], 1ull);
 				}
 				if (DRY)
-					ops[e.jj] = (uint8_t)op;
+					dw.opt[e.i] = (uint8_t)op;
 				ended = false;
 			}
 			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
 				if (!have) {
 					jhead = jj = heads[h];
 					grp = (uint32_t)(d.slow_keys[jj] >> 32);
-					session_begin(d, S, jj, d.ev_slot[slow_event(d, jj)]);
+					if (DRY)
+						jhead = dw.head[jj];
+					if (jj == jhead)
+						session_begin(d, S, jj, d.ev_slot[slow_event(d, jj)]);
+					else
+						S = dw.snap[jj]; // the state before event jj, as the last walk left it
 					have = true;
 				}
 				if (jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == grp) {
@@ -1589,6 +1607,15 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 							pf_off = d.off[pf_i];
 						}
 					}
+					if (DRY) {
+						if (i >= dw.hz) { // past the round's horizon: a later round continues here
+							dw.wto[jhead] = jj;
+							have = false;
+							h += stride;
+							continue;
+						}
+						dw.snap[jj] = S;
+					}
 					if (evf && (evf[jj] & 1u))
 						S.live = 0; // evicted since its previous event: find() misses
 					if (ev_begin(d, S, jj, i, fl, L, off, e)) {
@@ -1610,12 +1637,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 					} else {
 						const uint32_t op = ev_end<DRY>(d, S, e, 0);
 						if (DRY)
-							ops[jj] = (uint8_t)op;
+							dw.opt[i] = (uint8_t)op;
 					}
 					jj++;
 				} else {
 					if (!DRY && S.live && !(evf && (evf[jhead] & 2u)))
 						session_carry_out(d, S, jhead, jj - 1);
+					if (DRY)
+						dw.wto[jhead] = kNone; // walked to its end
 					have = false;
 					h += stride;
 				}
@@ -2008,18 +2037,23 @@ __global__ void k_lru_carry_rank(Dev d, const uint32_t* cm_end, uint32_t* mk_ref
 	}
 }
 
-// The walked sessions' operations by event (opt): every session (hlist == nullptr) or the list.
-__global__ void k_lru_opt(Dev d, uint32_t nslow, const uint8_t* ops, const uint32_t* hlist, const uint32_t* hcount, uint8_t* opt) {
-	if (!hlist) {
-		for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
-			opt[(uint32_t)d.slow_keys[j]] = ops[j];
-		return;
-	}
-	const uint32_t nh = *hcount;
+// The round's walks: per session (k_walk_heads' list), from its first changed position if
+// that lies in the part walked before (cpos; cleared here), else from where the last walk
+// stopped (wto) if that event comes before the horizon.  Entries are start positions.
+__global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, uint32_t hz, uint32_t* rlist, uint32_t* tot) {
+	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS];
 	for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
-		const uint32_t j0 = hlist[h], grp = (uint32_t)(d.slow_keys[j0] >> 32);
-		for (uint32_t j = j0; j < nslow && (uint32_t)(d.slow_keys[j] >> 32) == grp; j++)
-			opt[(uint32_t)d.slow_keys[j]] = ops[j];
+		const uint32_t jh = d.heads[h], c = cpos[jh], wt = wto[jh];
+		uint32_t start = kNone;
+		if (c != kNone) {
+			cpos[jh] = kNone;
+			if (wt == kNone || c < wt)
+				start = c;
+		}
+		if (wt != kNone && (uint32_t)d.slow_keys[wt] < hz)
+			start = min(start, wt);
+		if (start != kNone)
+			rlist[atomicAdd(&tot[3], 1u)] = start;
 	}
 }
 
@@ -2204,10 +2238,29 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 	__syncthreads();
 	while (s_more) {
 		const uint32_t mb = s_qf & ~63u, eb = s_j; // stage markers from the front's window, evictions from s_j
-		for (uint32_t k = t; k < kGrM; k += 256)
-			se[k] = mb + k < nmk ? mk_e[mb + k] : 0u;
-		for (uint32_t k = t; k < kGrE; k += 256)
-			sv[k] = eb + k < nev ? ev_t[eb + k] : ~0u;
+		// 8 loads in flight per thread (a load-then-store loop waited a full latency per word)
+		for (uint32_t k0 = 0; k0 < kGrM; k0 += 256 * 8) {
+			uint32_t v[8];
+#pragma unroll
+			for (uint32_t u = 0; u < 8; u++) {
+				const uint32_t k = k0 + u * 256 + t;
+				v[u] = mb + k < nmk ? mk_e[mb + k] : 0u;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < 8; u++)
+				se[k0 + u * 256 + t] = v[u];
+		}
+		{
+			uint32_t v[kGrE / 256];
+#pragma unroll
+			for (uint32_t u = 0; u < kGrE / 256; u++) {
+				const uint32_t k = u * 256 + t;
+				v[u] = eb + k < nev ? ev_t[eb + k] : ~0u;
+			}
+#pragma unroll
+			for (uint32_t u = 0; u < kGrE / 256; u++)
+				sv[u * 256 + t] = v[u];
+		}
 		__syncthreads();
 		if (wave == 0) {
 			uint32_t qf = s_qf, j = eb, bad = 0, restage = 0, stop = 0, rec = s_rec;
@@ -2221,6 +2274,8 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 					break;
 				}
 				uint32_t k = 0;
+				const uint32_t rec0 = rec;
+				uint32_t myv = 0, myq = 0; // lane jl: eviction j + jl's victim and recorded front
 				while (k < nj) {
 					const uint32_t wb = qf & ~63u;
 					if (wb >= nmk) {
@@ -2237,18 +2292,16 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 						// the front after eviction jl - 1, before any window this eviction skips: a
 						// later round resumes there, and its eviction jl may come earlier
 						if (j + jl >= rec) { // once per eviction, also across a restaging
-							if (lane == jl)
-								qfe[j + jl] = wb + p;
+							myq = lane == jl ? wb + p : myq;
 							rec = j + jl + 1;
 						}
-						const uint32_t tt = __shfl(tv, (int)jl);
+						const uint32_t tt = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)jl); // a scalar, not a bpermute
 						const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt)); // alive at tt
 						const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
 						if (avail == 0)
 							break;
 						const uint32_t v = (uint32_t)__builtin_ctzll(avail);
-						if (lane == jl)
-							vict[j + jl] = wb + v;
+						myv = lane == jl ? wb + v : myv;
 						p = v + 1;
 					}
 					// eviction jl finds no live marker in this window: none of its markers lives
@@ -2256,6 +2309,11 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 					qf = jl < nj ? wb + 64 : wb + p;
 					k = jl;
 				}
+				// one vector store each for the block's victims and fronts
+				if (lane < k)
+					vict[j + lane] = myv;
+				if (j + lane >= rec0 && j + lane < rec)
+					qfe[j + lane] = myq;
 				j += k;
 			}
 			if (lane == 0) {
@@ -2317,15 +2375,15 @@ __global__ void k_lru_tails(const uint32_t* vtot, const uint32_t* vic, const uin
 }
 
 // Phase 7: how many flags the round changed (cnt[2]), the first event whose eviction bit
-// changed (cnt[3]: the new frontier), and the sessions the next round walks again (rmark).
+// changed (cnt[3]: the new frontier), and where each session's walk must start again (cpos).
 __global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, const uint8_t* cf, const uint8_t* ncf, uint32_t n2,
-		const unsigned long long* keys, const uint32_t* head, uint8_t* rmark, unsigned long long* cnt) {
+		const unsigned long long* keys, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt) {
 	uint32_t x = 0, first = kNone;
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x) {
 		const bool dk = k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
 		x += dk ? 1u : 0u;
 		if (k < n1 && ((f[k] ^ nf[k]) & 1u)) { // the walk changes only with bit 0
-			rmark[head[k]] = 1;
+			atomicMin(&cpos[head[k]], k); // its session walks again from here
 			const uint32_t tk = (uint32_t)keys[k];
 			first = tk < first ? tk : first;
 		}
@@ -2334,15 +2392,6 @@ __global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, con
 		wave_add(&cnt[2], (unsigned long long)x);
 	if (first != kNone)
 		atomicMin(&cnt[3], (unsigned long long)first);
-}
-
-// The sessions the next round walks again (rmark, by first sorted position; cleared here).
-__global__ void k_lru_rlist(uint32_t nslow, uint8_t* rmark, uint32_t* rlist, uint32_t* tot) {
-	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
-		if (rmark[j]) {
-			rmark[j] = 0;
-			rlist[atomicAdd(&tot[3], 1u)] = j;
-		}
 }
 
 // Aggregator::newRequest for the fast-path requests (coalesced reads of the results, keys
@@ -3308,49 +3357,57 @@ hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d,
-			(const uint8_t*)nullptr, (uint8_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+			(const uint8_t*)nullptr, DryWalk{}, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 
 	return hipGetLastError();
 }
+// Every session's walk starts at its first event.
+__global__ void k_lru_wto_init(Dev d, uint32_t* wto) {
+	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS];
+	for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x)
+		wto[d.heads[h]] = d.heads[h];
+}
+
 // The exact-LRU rounds' once-per-batch part: heads, event -> sorted position, next finds,
-// carried markers, empty operations.
+// carried markers, empty operations, every walk at its session's start.
 hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus) {
 	hipError_t e;
 	if ((e = hipMemsetAsync(w.jpos, 0xff, (size_t)d.n * sizeof(uint32_t), st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cm_end, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cpos, 0xff, (size_t)nslow * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.opt, 0, d.n, st)) != hipSuccess || (e = hipMemsetAsync(w.f[0], 0, nslow, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.jpos, w.head);
 	hipLaunchKernelGGL(k_lru_static, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.mend, w.cm_end, w.cm_head);
+	hipLaunchKernelGGL(k_lru_wto_init, dim3(cus * 4), dim3(256), 0, st, d, w.wto);
 	if (d.n_carry_in)
 		hipLaunchKernelGGL(k_lru_carry_rank, dim3(grid_for(d.n_carry_in, 256, cus * 4)), dim3(256), 0, st, d, (const uint32_t*)w.cm_end,
 				w.mk_ref, w.mk_e);
 	return hipGetLastError();
 }
 
-// One exact-LRU round after a dry walk in the world f / cf (every session when nwalk ==
-// kNone, else the nwalk sessions of the last round's list): the world the evictions of
-// [front, front + window) and all earlier ones imply in nf / ncf; cnt[1] inconsistency,
-// cnt[2] flags changed, cnt[3] the new frontier.
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t nwalk, uint32_t front, uint32_t window,
-		hipStream_t st, int cus) {
+// One exact-LRU round in the world f / cf: the walks up to the horizon front + window (from
+// where flags changed or the last walk stopped), then the world the evictions before the
+// horizon imply in nf / ncf; cnt[1] inconsistency, cnt[2] flags changed, cnt[3] the new
+// frontier.
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t front, uint32_t window, hipStream_t st,
+		int cus) {
 	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
 	const uint8_t* f = w.f[cur];
 	uint8_t* nf = w.f[cur ^ 1];
 	const uint8_t* cf = w.cf[cur];
 	uint8_t* ncf = w.cf[cur ^ 1];
-	const bool all = nwalk == kNone;
-	if (all || nwalk) {
-		const uint32_t g = grid_for(all ? nslow : nwalk, kWalkThreads, cus * EBD_WALK_BLOCKS);
-		hipLaunchKernelGGL(k_walk<true>, dim3(g), dim3(kWalkThreads), 0, st, d, f, w.ops, all ? (const uint32_t*)nullptr : (const uint32_t*)w.rlist,
-				(const uint32_t*)(w.tot + 3));
-		hipLaunchKernelGGL(k_lru_opt, dim3(grid_for(all ? nslow : nwalk, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.ops,
-				all ? (const uint32_t*)nullptr : (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3), w.opt);
-	}
+	const unsigned long long tend64 = (unsigned long long)front + window;
+	const uint32_t tend = (uint32_t)(tend64 < 0xffffffffull ? tend64 : 0xffffffffull);
 	hipError_t e;
+	if ((e = hipMemsetAsync(w.tot + 3, 0, sizeof(uint32_t), st)) != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, tend, w.rlist, w.tot);
+	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
+			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, tend}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
 	if ((e = hipMemsetAsync(ncf, 0, d.carry_cap, st)) != hipSuccess || (e = hipMemsetAsync(w.nf_t, 0, n, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.tot + 4, 0, sizeof(uint32_t), st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cnt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess ||
@@ -3364,26 +3421,22 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(1), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
 	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
 			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, front, w.mk_ref, w.mk_e, w.ev_t, w.tot);
-	const unsigned long long tend = (unsigned long long)front + window;
-	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot,
-			(uint32_t)(tend < 0xffffffffull ? tend : 0xffffffffull), w.vict, w.qfe, w.cnt);
+	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot, tend, w.vict,
+			w.qfe, w.cnt);
 	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
 			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.nf_t, w.vic, w.tot + 4, w.cnt);
 	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.nf_t, nf);
 	hipLaunchKernelGGL(k_lru_tails, dim3(cus), dim3(256), 0, st, (const uint32_t*)(w.tot + 4), (const uint32_t*)w.vic, (const uint32_t*)w.jpos,
 			(const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf);
 	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(nslow + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, f, (const uint8_t*)nf, nslow, cf,
-			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.rmark, w.cnt);
-	if ((e = hipMemsetAsync(w.tot + 3, 0, sizeof(uint32_t), st)) != hipSuccess)
-		return e;
-	hipLaunchKernelGGL(k_lru_rlist, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, nslow, w.rmark, w.rlist, w.tot);
+			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.cpos, w.cnt);
 	return hipGetLastError();
 }
 // The final walk of the exact path in the converged world (with output), then the carried
 // sessions it did not meet.
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f,
-			(uint8_t*)nullptr, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
+			DryWalk{}, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 	if (d.n_carry_in)
 		hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, cf);
 	return hipGetLastError();
