@@ -1608,13 +1608,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 						}
 					}
 					if (DRY) {
+						dw.snap[jj] = S; // the state before event jj: a later walk may start here
 						if (i >= dw.hz) { // past the round's horizon: a later round continues here
 							dw.wto[jhead] = jj;
 							have = false;
 							h += stride;
 							continue;
 						}
-						dw.snap[jj] = S;
 					}
 					if (evf && (evf[jj] & 1u))
 						S.live = 0; // evicted since its previous event: find() misses
@@ -2087,21 +2087,41 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint
 	}
 }
 
-// Phase 2 (one thread): each block's starting size from the context's carried sessions, and
-// its first marker's index (after the carried ones).
-__global__ void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0, long long* lst,
-		uint32_t* moff, uint32_t* tot) {
-	if (blockIdx.x || threadIdx.x)
-		return;
+// Phase 2 (one workgroup of kLsT threads, kLsT scan blocks at a time): each scan block's
+// starting size from the context's carried sessions, and its first marker's index (after the
+// carried ones).
+__global__ __launch_bounds__(kLsT) void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0,
+		long long* lst, uint32_t* moff, uint32_t* tot) {
+	__shared__ LFn F[kLsT];
+	__shared__ uint32_t S[kLsT];
+	const uint32_t t = threadIdx.x;
 	long long x = l0;
 	uint32_t m = m0;
-	for (uint32_t b = 0; b < nb; b++) {
-		lst[b] = x;
-		moff[b] = m;
-		x = lfn_apply(bf[b], x);
-		m += bm[b];
+	for (uint32_t c = 0; c < nb; c += kLsT) {
+		const bool in = c + t < nb;
+		const LFn f = in ? bf[c + t] : lfn_id();
+		const uint32_t mk = in ? bm[c + t] : 0u;
+		F[t] = f;
+		S[t] = mk;
+		__syncthreads();
+		for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) { // inclusive, in order
+			const LFn g = t >= o ? lfn_then(F[t - o], F[t]) : F[t];
+			const uint32_t y = t >= o ? S[t - o] + S[t] : S[t];
+			__syncthreads();
+			F[t] = g;
+			S[t] = y;
+			__syncthreads();
+		}
+		if (in) {
+			lst[c + t] = t ? lfn_apply(F[t - 1], x) : x;
+			moff[c + t] = m + (t ? S[t - 1] : 0u);
+		}
+		x = lfn_apply(F[kLsT - 1], x);
+		m += S[kLsT - 1];
+		__syncthreads();
 	}
-	tot[0] = m; // markers, carried ones included
+	if (t == 0)
+		tot[0] = m; // markers, carried ones included
 }
 
 // Block-wide exclusive scan of the threads' maps (in order), by Hillis-Steele in LDS.
@@ -2165,18 +2185,23 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uin
 		be[blockIdx.x] = tot;
 }
 
-// Phase 4 (one thread): each block's first eviction index; tot[5] = the evictions before the
-// frontier (k_lru_compact sets it when the frontier lies inside the batch).
-__global__ void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot) {
-	if (blockIdx.x || threadIdx.x)
-		return;
+// Phase 4 (one workgroup): each scan block's first eviction index; tot[5] = the evictions
+// before the frontier (k_lru_compact sets it when the frontier lies inside the batch).
+__global__ __launch_bounds__(kLsT) void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot) {
+	__shared__ uint32_t S[kLsT];
+	const uint32_t t = threadIdx.x;
 	uint32_t e = 0;
-	for (uint32_t b = 0; b < nb; b++) {
-		eoff[b] = e;
-		e += be[b];
+	for (uint32_t c = 0; c < nb; c += kLsT) {
+		uint32_t total;
+		const uint32_t ex = u32_block_excl(c + t < nb ? be[c + t] : 0u, S, &total);
+		if (c + t < nb)
+			eoff[c + t] = e + ex;
+		e += total;
 	}
-	tot[1] = e;
-	tot[5] = e;
+	if (t == 0) {
+		tot[1] = e;
+		tot[5] = e;
+	}
 }
 
 // Phase 5: the markers (event position, end) and the eviction times, in event order.
@@ -2276,39 +2301,45 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 				uint32_t k = 0;
 				const uint32_t rec0 = rec;
 				uint32_t myv = 0, myq = 0; // lane jl: eviction j + jl's victim and recorded front
-				while (k < nj) {
-					const uint32_t wb = qf & ~63u;
-					if (wb >= nmk) {
-						bad = 1; // a full cache and no live marker
-						break;
+				// one loop over the block's evictions; a window without a live marker for the
+				// current eviction loads the next one (its markers are dead for every later
+				// eviction too)
+				uint32_t wb = qf & ~63u, p = qf - wb;
+				if (wb >= nmk)
+					bad = 1; // a full cache and no live marker
+				else if (wb + 64 > mb + kGrM)
+					restage = 1; // the staged markers are used up
+				uint32_t e = !bad && !restage && wb + lane < nmk ? se[wb - mb + lane] : 0u;
+				while (k < nj && !bad && !restage) {
+					// the front after eviction k - 1, before any window this eviction skips: a
+					// later round resumes there, and its eviction k may come earlier
+					if (j + k >= rec) {
+						myq = lane == k ? wb + p : myq;
+						rec = j + k + 1;
 					}
-					if (wb + 64 > mb + kGrM) {
-						restage = 1; // the staged markers are used up
-						break;
-					}
-					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
-					uint32_t p = qf - wb, jl = k;
-					for (; jl < nj; jl++) {
-						// the front after eviction jl - 1, before any window this eviction skips: a
-						// later round resumes there, and its eviction jl may come earlier
-						if (j + jl >= rec) { // once per eviction, also across a restaging
-							myq = lane == jl ? wb + p : myq;
-							rec = j + jl + 1;
-						}
-						const uint32_t tt = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)jl); // a scalar, not a bpermute
-						const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt)); // alive at tt
-						const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
-						if (avail == 0)
+					const uint32_t tt = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)k); // a scalar, not a bpermute
+					const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt)); // alive at tt
+					const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
+					if (avail == 0) {
+						wb += 64;
+						p = 0;
+						if (wb >= nmk) {
+							bad = 1;
 							break;
-						const uint32_t v = (uint32_t)__builtin_ctzll(avail);
-						myv = lane == jl ? wb + v : myv;
-						p = v + 1;
+						}
+						if (wb + 64 > mb + kGrM) {
+							restage = 1;
+							break;
+						}
+						e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
+						continue;
 					}
-					// eviction jl finds no live marker in this window: none of its markers lives
-					// on for it or any later eviction, so the front moves to the next window
-					qf = jl < nj ? wb + 64 : wb + p;
-					k = jl;
+					const uint32_t v = (uint32_t)__builtin_ctzll(avail);
+					myv = lane == k ? wb + v : myv;
+					p = v + 1;
+					k++;
 				}
+				qf = wb + p;
 				// one vector store each for the block's victims and fronts
 				if (lane < k)
 					vict[j + lane] = myv;
@@ -3414,11 +3445,11 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 			(e = hipMemsetAsync(w.cnt + 3, 0xff, sizeof(unsigned long long), st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm);
-	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(1), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
+	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(kLsT), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
 			w.moff, w.tot);
 	hipLaunchKernelGGL(k_lru_scan_apply, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (const long long*)w.lst,
 			w.evt, w.be);
-	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(1), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
+	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(kLsT), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
 	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
 			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, front, w.mk_ref, w.mk_e, w.ev_t, w.tot);
 	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot, tend, w.vict,
