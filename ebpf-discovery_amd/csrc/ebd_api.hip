@@ -650,7 +650,13 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	LruRound& w = c->lr;
 	HIP_TRY(launch_lru_init(d, nslow, w, c->stream, c->cus));
 	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
-	const uint32_t window = 1u << 14; // a round settles about one session inter-event gap (config 4: ~4 k events)
+	// a round settles about one session inter-event gap (config 4: ~2.5 k events); a wider window
+	// only makes every round re-derive more of what the next round derives again
+	static const uint32_t window = [] {
+		const char* v = std::getenv("EBD_LRU_WINDOW");
+		const long w = v ? std::atol(v) : 0;
+		return w > 0 ? (uint32_t)w : 8192u; // 1 M config-4 events, LRU 2048: 2048 -> 523 ms, 4096 -> 394, 8192 -> 347, 16384 -> 387
+	}();
 	int cur = 0;
 	uint32_t front = 0;
 	const int max_rounds = 4096;
