@@ -650,8 +650,8 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	LruRound& w = c->lr;
 	HIP_TRY(launch_lru_init(d, nslow, w, c->stream, c->cus));
 	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
-	// a round settles about one session inter-event gap (config 4: ~2.5 k events); a wider window
-	// only makes every round re-derive more of what the next round derives again
+	// the window trades rounds (a round settles at most the window) against each round's merge
+	// work (it re-derives the whole window); EBD_LRU_WINDOW overrides it
 	static const uint32_t window = [] {
 		const char* v = std::getenv("EBD_LRU_WINDOW");
 		const long w = v ? std::atol(v) : 0;
