@@ -13,7 +13,8 @@ namespace ebd {
 struct Slot {
 	unsigned long long tag;    // Hash128.lo of (pid, endpoint); 0 = empty; claimed by CAS
 	unsigned long long hi;     // Hash128.hi, published by the claimer
-	unsigned long long first;  // min over requests of seq << 16 | isHttps << 15 | host length (atomicMin)
+	unsigned long long nfirst; // ~(min over requests of seq << 16 | isHttps << 15 | host length): atomicMax of
+	                           // the complement, so that an empty slot is all zeros (a plain fill clears)
 	unsigned long long pad0[2]; // (the endpoint's arena offset, pid and length live beside the
 	                            //  claimed-slot list, Dev::list_ep / list_pl: written in list order)
 	unsigned int internal_clients; // uint32, wraps like Service.h:53-54

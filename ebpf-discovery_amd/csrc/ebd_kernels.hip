@@ -105,8 +105,8 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 		// atomicMin).  Slot words are only ever written by atomics here, so no dirty line
 		// sits in L2 when the next kernel starts.
 		const ulonglong2 th = *(const ulonglong2*)&s->tag;
-		const ulonglong2 mo = *(const ulonglong2*)&s->first;
-		seen_first = mo.x;
+		const ulonglong2 mo = *(const ulonglong2*)&s->nfirst;
+		seen_first = ~mo.x;
 		unsigned long long t = th.x;
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, h.lo);
@@ -151,7 +151,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 	if (inc_ext)
 		atomicAdd(&s->external_clients, inc_ext);
 	if (first < seen_first)
-		atomicMin(&s->first, first);
+		atomicMax(&s->nfirst, ~first); // the slot keeps ~first: an empty slot is all zeros
 	return idx;
 }
 
@@ -2744,7 +2744,7 @@ __device__ __forceinline__ Slot empty_slot() {
 	Slot s;
 	s.tag = 0;
 	s.hi = 0;
-	s.first = ~0ull;
+	s.nfirst = 0; // first = ~0: no request yet
 	s.pad0[0] = s.pad0[1] = 0;
 	s.internal_clients = 0;
 	s.external_clients = 0;
@@ -2764,10 +2764,15 @@ __global__ void k_clear_used(const unsigned int* used, const unsigned long long*
 	if (4 * n < slot_cap) {
 		for (unsigned long long k = t0; k < n; k += nt)
 			slots[used[k]] = empty_slot();
-	} else {
-		uint4* w = (uint4*)slots; // a slot is 4 pieces; empty: first (piece 1, low half) = ~0, the rest 0
-		for (unsigned long long k = t0; k < 4ull * slot_cap; k += nt)
-			w[k] = (k & 3) == 1 ? make_uint4(~0u, ~0u, 0u, 0u) : make_uint4(0u, 0u, 0u, 0u);
+	} else { // an empty slot is all zeros: a plain fill, 4 stores in flight per lane
+		uint4* w = (uint4*)slots;
+		const unsigned long long nw = 4ull * slot_cap;
+		for (unsigned long long k = t0; k < nw; k += 4 * nt) {
+#pragma unroll
+			for (unsigned long long u = 0; u < 4; u++)
+				if (k + u * nt < nw)
+					w[k + u * nt] = make_uint4(0u, 0u, 0u, 0u);
+		}
 	}
 }
 
@@ -2798,7 +2803,8 @@ __global__ void k_collect(Dev d, ebd_service* out) {
 	for (unsigned long long k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
 		const Slot& s = d.slots[d.new_slots[k]];
 		const unsigned long long ep = d.list_ep[k], pl = d.list_pl[k];
-		const uint32_t hl = (uint32_t)(s.first & 0x7fffu);
+		const unsigned long long first = ~s.nfirst;
+		const uint32_t hl = (uint32_t)(first & 0x7fffu);
 		uint32_t doff = 0, dlen = 0;
 		if (ep != ~0ull)
 			host_domain(d.sarena + ep, hl, &doff, &dlen);
@@ -2806,14 +2812,14 @@ __global__ void k_collect(Dev d, ebd_service* out) {
 		v.pid = (uint32_t)pl;
 		v.internal_clients = s.internal_clients;
 		v.external_clients = s.external_clients;
-		v.https = (uint8_t)((s.first >> 15) & 1u);
+		v.https = (uint8_t)((first >> 15) & 1u);
 		v.pad_[0] = v.pad_[1] = v.pad_[2] = 0;
 		v.endpoint_off = ep;
 		v.endpoint_len = (uint32_t)(pl >> 32);
 		v.domain_off = doff;
 		v.domain_len = dlen;
 		v.host_len = hl;
-		v.first_seq = s.first >> 16;
+		v.first_seq = first >> 16;
 		v.key_lo = s.tag;
 		v.key_hi = s.hi;
 		v.nets_v4_16 = s.nets[0];
@@ -2855,7 +2861,7 @@ __global__ void k_keep_collect(Dev d, KeepRec* keep, unsigned long long* kbytes,
 		KeepRec r;
 		r.tag = s.tag;
 		r.hi = s.hi;
-		r.first = s.first;
+		r.first = ~s.nfirst;
 		const unsigned long long ep = d.list_ep[k], pl = d.list_pl[k];
 		r.pid = (uint32_t)pl;
 		r.ep_len = (uint32_t)(pl >> 32);
