@@ -50,6 +50,41 @@ __device__ __forceinline__ unsigned long long wave_add(unsigned long long* ctr, 
 	return __shfl(base, (int)leader) + pre;
 }
 
+// LDS words written by some lanes of a wave and then read by others: order the accesses.
+__device__ __forceinline__ void wave_sync() {
+	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+	__builtin_amdgcn_wave_barrier();
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A global list grown by a whole 256-thread block at once: x = this thread's entries; returns
+// the index of its first one.  One atomic per call for the block: a list counter takes about
+// 88 returning atomics per microsecond (MI355X_MICROARCH.md, dequeue), so a wave_add per wave
+// and step held k_slow_collect at that rate (1.25 M atomics, 15 ms per 80 M-event poll cycle).
+// Every thread of the block calls it (barriers); part: LDS scratch of 4 words.
+__device__ __forceinline__ unsigned long long block_reserve(unsigned long long* ctr, uint32_t x, uint32_t* part,
+		unsigned long long* base) {
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	uint32_t incl = x;
+	for (int o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(incl, o, 64);
+		if (lane >= (uint32_t)o)
+			incl += y;
+	}
+	if (lane == 63)
+		part[wave] = incl;
+	__syncthreads();
+	uint32_t before = 0, total = 0;
+	for (uint32_t w = 0; w < 4; w++) {
+		before += w < wave ? part[w] : 0u;
+		total += part[w];
+	}
+	if (threadIdx.x == 0)
+		*base = total ? atomicAdd(ctr, (unsigned long long)total) : 0ull;
+	__syncthreads();
+	return *base + before + incl - x; // base and part are rewritten only after the next call's first barrier
+}
+
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
 	return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -277,7 +312,8 @@ __device__ __forceinline__ unsigned long long sset_tag(unsigned long long kv, ui
 
 // ev: the event whose fresh parse was UNFINISHED (kNone for a carried session): the first
 // such event of the batch bounds when the session can have entered the LRU (k_lru_delta).
-__device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry, uint32_t ev) {
+// *claimed: the slot this call claimed (for the dirty list), else kNone.
+__device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid, uint32_t carry, uint32_t ev, uint32_t* claimed) {
 	const unsigned long long kv = ((unsigned long long)fd << 32) | pid;
 	const unsigned long long tag = sset_tag(kv, sid);
 	const uint32_t mask = *d.sset_mask;
@@ -291,8 +327,7 @@ __device__ int sset_insert(const Dev& d, uint32_t pid, uint32_t fd, uint32_t sid
 			if (t == 0) {
 				s->kv = kv;
 				s->sid = sid;
-				const unsigned long long k = wave_add(&d.ctr[CTR_DIRTY], 1ull);
-				d.dirty[k] = idx;
+				*claimed = idx;
 				t = tag;
 			}
 		}
@@ -663,6 +698,7 @@ struct FreshShared {
 	uint32_t rdata[(kStageWords + 1) * kRing];      // staged bytes of each slot's record
 	uint32_t stage[kStageWords * kScanLanes];       // a scan lane's current buffer, as scanned
 	uint32_t fstage[(kStageWords + 1) * kFinLanes]; // a finalize lane's record's bytes
+	uint32_t unf[kFinWaves][128];                   // each finalize wave's UNFINISHED events not yet listed
 	uint32_t next_ev;   // next event of the workgroup's range
 	uint32_t tail;      // positions handed out to scan lanes
 	uint32_t claim;     // positions handed out to finalize waves
@@ -672,13 +708,15 @@ static_assert(sizeof(FreshShared) + kLdsTableBytes <= 160 * 1024, "k_fresh LDS f
 
 // fresh_finalize (ebd_fresh.h) for the record in the lane's registers; the lane's staged
 // bytes are at fs (word j at fs[j * kFinLanes]).
-__device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, const uint32_t (&q)[R_WORDS], const uint32_t* fs) {
+// Returns true for an UNFINISHED parse: its session may be saved (Discovery.cpp:148-150), and
+// the caller lists the event for k_sset_build.
+__device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, const uint32_t (&q)[R_WORDS], const uint32_t* fs) {
 	const uint8_t* p = (const uint8_t*)(uintptr_t)((unsigned long long)q[R_PLO] | ((unsigned long long)(q[R_PHI] & 0xffffu) << 32));
 	const uint32_t L = q[R_PHI] >> 16;
 	const uint32_t i = q[R_IDX];
 	if (i >= d.n || L > EBD_BUFFER_MAX_DATA_SIZE || (unsigned long long)(p - d.payload) >> 40) {
 		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
-		return;
+		return false;
 	}
 	ScanRec sr;
 	sr.url = Trk{q[R_C01] & 0xffffu, q[R_QS + 0]};
@@ -701,13 +739,9 @@ __device__ __forceinline__ void finalize_rec(const Dev& d, const uint8_t* T, con
 			__builtin_memcpy(src, &q[R_SRC], 16);
 			fr.r.info = (uint8_t)(fr.r.info | (classify_source(*d.ifs, (uint8_t)(q[R_SF] >> 8), src) << EBD_INFO_CLASS_SHIFT));
 		}
-	} else if (fr.r.status == EBD_STATUS_UNFINISHED) {
-		// the session may be saved (Discovery.cpp:148-150): sequential path
-		const EventRec& ev = d.ev[i];
-		d.ev_slot[wave_add(&d.ctr[CTR_UNFINISHED], 1ull)] = i; // k_sset_build inserts its session
-		(void)ev;
 	}
 	d.res[i] = fr.r;
+	return fr.r.status == EBD_STATUS_UNFINISHED;
 }
 
 // The table first: LDS address = table index, so a step's read needs no base add.
@@ -744,6 +778,10 @@ void k_fresh(Dev d) {
 		// ---- finalize waves: 64 records at a time, in position order ----
 		const uint32_t fl = (wave - kScanWaves) * 64 + lane; // finalize lane
 		uint32_t* fs = sh.fstage + fl;
+		// UNFINISHED events go to ev_slot 64 at a time, one atomic each (a wave_add per batch of
+		// records held config-4 poll cycles, ~30 % of them UNFINISHED, at the counter's rate)
+		uint32_t* ust = sh.unf[wave - kScanWaves];
+		uint32_t uh = 0, un = 0; // wave-uniform: ring head and entries
 		for (;;) {
 			uint32_t c = 0;
 			if (lane == 0)
@@ -786,12 +824,37 @@ void k_fresh(Dev d) {
 					fs[j * kFinLanes] = sh.rdata[j * kRing + slot];
 				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
 			}
+			bool unf = false;
 			if (st == 1) {
 				if (q[R_POS] != pos + 1)
 					set_error(d, EBD_ERR_INTERNAL); // ring protocol violated: reported, not followed
 				else
-					finalize_rec(d, T, q, fs);
+					unf = finalize_rec(d, T, q, fs);
 			}
+			const unsigned long long b = __ballot(unf);
+			if (unf)
+				ust[(uh + un + __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0))) & 127u] = q[R_IDX];
+			un += (uint32_t)__popcll(b);
+			if (un >= 64) {
+				wave_sync();
+				unsigned long long at = 0;
+				if (lane == 0)
+					at = atomicAdd(&d.ctr[CTR_UNFINISHED], 64ull);
+				at = __shfl(at, 0);
+				d.ev_slot[at + lane] = ust[(uh + lane) & 127u];
+				uh += 64;
+				un -= 64;
+				wave_sync(); // the words just read may be rewritten
+			}
+		}
+		wave_sync();
+		if (un) {
+			unsigned long long at = 0;
+			if (lane == 0)
+				at = atomicAdd(&d.ctr[CTR_UNFINISHED], (unsigned long long)un);
+			at = __shfl(at, 0);
+			if (lane < un)
+				d.ev_slot[at + lane] = ust[(uh + lane) & 127u];
 		}
 		return;
 	}
@@ -1021,40 +1084,76 @@ __global__ void k_sset_size(Dev d, uint32_t cap) {
 		m <<= 1;
 	*d.sset_mask = m - 1u;
 }
-__global__ void k_sset_build(Dev d) {
-	const uint32_t nu = (uint32_t)d.ctr[CTR_UNFINISHED];
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < d.n_carry_in + nu; k += gridDim.x * blockDim.x) {
-		if (k < d.n_carry_in) {
-			const Carry& cr = d.carry_in[k];
-			sset_insert(d, cr.pid, cr.fd, cr.sid, k + 1, kNone);
-		} else {
-			const uint32_t i = d.ev_slot[k - d.n_carry_in];
-			const EventRec& ev = d.ev[i];
-			sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i);
+// Tiles of 256 x kSetPer inserts per block; the claimed slots join the dirty list with one
+// atomic per tile (block_reserve).
+constexpr uint32_t kSetPer = 8;
+__global__ __launch_bounds__(256) void k_sset_build(Dev d) {
+	__shared__ uint32_t part[4];
+	__shared__ unsigned long long base;
+	const uint32_t nu = (uint32_t)d.ctr[CTR_UNFINISHED], total = d.n_carry_in + nu, tile = 256u * kSetPer;
+	for (uint32_t t0 = blockIdx.x * tile; t0 < total; t0 += gridDim.x * tile) { // uniform
+		uint32_t cl[kSetPer], cnt = 0;
+#pragma unroll
+		for (uint32_t u = 0; u < kSetPer; u++) {
+			const uint32_t k = t0 + u * 256u + threadIdx.x;
+			cl[u] = kNone;
+			if (k < d.n_carry_in) {
+				const Carry& cr = d.carry_in[k];
+				sset_insert(d, cr.pid, cr.fd, cr.sid, k + 1, kNone, &cl[u]);
+			} else if (k < total) {
+				const uint32_t i = d.ev_slot[k - d.n_carry_in];
+				const EventRec& ev = d.ev[i];
+				sset_insert(d, ev.pid, ev.fd, ev.sessionID, 0, i, &cl[u]);
+			}
+			cnt += cl[u] != kNone ? 1u : 0u;
 		}
+		unsigned long long at = block_reserve(&d.ctr[CTR_DIRTY], cnt, part, &base);
+#pragma unroll
+		for (uint32_t u = 0; u < kSetPer; u++)
+			if (cl[u] != kNone)
+				d.dirty[at++] = cl[u];
 	}
 }
 
-__global__ void k_slow_collect(Dev d) {
+// Tiles of 256 x kCollectPer events per block, one atomic per tile for the list (block_reserve).
+constexpr uint32_t kCollectPer = 8;
+__global__ __launch_bounds__(256) void k_slow_collect(Dev d) {
+	__shared__ uint32_t part[4];
+	__shared__ unsigned long long base;
 	if (d.ctr[CTR_DIRTY] == 0)
 		return; // no session needs the sequential path in this batch
-	for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) {
-		const EventRec& e = d.ev[i];
-		if (!(e.flags & (FLAG_NEW | FLAG_END)))
-			continue;
-		const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
-		if (slot >= 0) {
-			d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
-			const unsigned long long k = wave_add(&d.ctr[CTR_SLOW], 1ull);
-			// grouped by session, sessions in the order of their first UNFINISHED fresh parse
-			// (carried ones first): the lanes of a walker wave then follow sessions that started
-			// together, whose events lie close together in the batch (L2 / TLB locality), where
-			// the session-set slot order (a hash) sent them all over the batch
-			const SSlot& ss = d.sset[slot];
-			const uint32_t grp = ss.carry ? ss.carry - 1 : d.carry_cap + ~ss.first_c;
-			d.slow_keys[k] = ((unsigned long long)grp << 32) | i;
-			d.ev_slot[i] = (uint32_t)slot;
+	const uint32_t tile = 256u * kCollectPer;
+	for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < d.n; t0 += (uint64_t)gridDim.x * tile) { // uniform
+		unsigned long long key[kCollectPer];
+		uint32_t has = 0;
+#pragma unroll
+		for (uint32_t u = 0; u < kCollectPer; u++) {
+			const uint64_t i = t0 + u * 256u + threadIdx.x;
+			key[u] = 0;
+			if (i >= d.n)
+				continue;
+			const EventRec& e = d.ev[i];
+			if (!(e.flags & (FLAG_NEW | FLAG_END)))
+				continue;
+			const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
+			if (slot >= 0) {
+				d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
+				// grouped by session, sessions in the order of their first UNFINISHED fresh parse
+				// (carried ones first): the lanes of a walker wave then follow sessions that started
+				// together, whose events lie close together in the batch (L2 / TLB locality), where
+				// the session-set slot order (a hash) sent them all over the batch
+				const SSlot& ss = d.sset[slot];
+				const uint32_t grp = ss.carry ? ss.carry - 1 : d.carry_cap + ~ss.first_c;
+				key[u] = ((unsigned long long)grp << 32) | i;
+				has |= 1u << u;
+				d.ev_slot[i] = (uint32_t)slot;
+			}
 		}
+		unsigned long long at = block_reserve(&d.ctr[CTR_SLOW], (uint32_t)__popc(has), part, &base);
+#pragma unroll
+		for (uint32_t u = 0; u < kCollectPer; u++)
+			if (has & (1u << u))
+				d.slow_keys[at++] = key[u];
 	}
 }
 
@@ -1556,6 +1655,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 	uint4 cur = uint4{0u, 0u, 0u, 0u}, n1 = cur, n2 = cur, n3 = cur;
 	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
 	unsigned long long pf_off = 0;
+	uint32_t inserts = 0; // CTR_INSERTS: one atomic per wave when it ends
 	for (;;) {
 		const unsigned long long busy = __ballot(in_ev), wait = __ballot(!in_ev && (ended || h < nh));
 		if (busy == 0 && wait == 0)
@@ -1567,8 +1667,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 				if (op == OP_INSERT) {
 					S.live = 1; // saveSession: a new key goes to the front (LRUCache.h:54-60)
 					S.stamp = d.seq_base + e.i;
-					if (!DRY)
-						wave_add(&d.ctr[CTR_INSERTS], 1ull);
+					inserts++;
 				}
 				if (DRY)
 					dw.opt[e.i] = (uint8_t)op;
@@ -1667,6 +1766,12 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 				ended = true;
 			}
 		}
+	}
+	if (!DRY) { // the loop ends for the whole wave at once
+		for (int o = 32; o > 0; o >>= 1)
+			inserts += __shfl_xor(inserts, o, 64);
+		if ((threadIdx.x & 63) == 0 && inserts)
+			atomicAdd(&d.ctr[CTR_INSERTS], (unsigned long long)inserts);
 	}
 }
 
@@ -2488,13 +2593,6 @@ __device__ __forceinline__ void agg_cip_one(const Dev& d, uint32_t i, uint8_t* r
 EBD_HD uint32_t agg_steps_per_block(uint32_t n, uint32_t grid) {
 	const uint32_t steps = (n + kAggThreads - 1) / kAggThreads;
 	return (steps + grid - 1) / grid;
-}
-
-// LDS words written by some lanes of a wave and then read by others: order the accesses.
-__device__ __forceinline__ void wave_sync() {
-	__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-	__builtin_amdgcn_wave_barrier();
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // 6 waves per SIMD: the compiler fits the kernel in 80 VGPRs without spilling (91 unbounded, 5 waves)
