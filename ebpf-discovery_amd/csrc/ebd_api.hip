@@ -1329,10 +1329,11 @@ int ebd_collect_networks(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_
 	if (!c->net_on)
 		return 0;
 	HIP_TRY(hipSetDevice(c->device));
-	if (!c->d_netdump)
+	if (out && !c->d_netdump)
 		HIP_TRY(hipMalloc(&c->d_netdump, (size_t)c->net_cap * sizeof(ebd_service_net)));
 	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(launch_net_dump(make_dev(c), c->d_netdump, c->net_cap, c->d_cnt, c->stream, c->cus));
+	// a size query (out null) only counts: k_net_dump writes nothing at cap 0
+	HIP_TRY(launch_net_dump(make_dev(c), out ? c->d_netdump : nullptr, out ? c->net_cap : 0u, c->d_cnt, c->stream, c->cus));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	const uint64_t cnt = c->h_ctr[CTR_COUNT];
@@ -1354,10 +1355,9 @@ int ebd_collect_networks_device(ebd_ctx* c, ebd_service_net* out, uint32_t cap, 
 	if (!c->net_on)
 		return 0;
 	HIP_TRY(hipSetDevice(c->device));
-	if (!out && !c->d_netdump)
-		HIP_TRY(hipMalloc(&c->d_netdump, (size_t)c->net_cap * sizeof(ebd_service_net)));
 	HIP_TRY(hipMemsetAsync(c->d_cnt, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(launch_net_dump(make_dev(c), out ? out : c->d_netdump, out ? cap : c->net_cap, c->d_cnt, c->stream, c->cus));
+	// a size query (out null) only counts: k_net_dump writes nothing at cap 0
+	HIP_TRY(launch_net_dump(make_dev(c), out, out ? cap : 0u, c->d_cnt, c->stream, c->cus));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr + CTR_COUNT, c->d_cnt, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	const uint64_t cnt = c->h_ctr[CTR_COUNT];
@@ -1446,6 +1446,18 @@ static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_
 	return e != hipSuccess ? e : excl_scan(c, nb, offs, n);
 }
 
+// A stream-ordered scratch allocation, freed on every return path.
+struct AsyncBuf {
+	hipStream_t st;
+	void* p = nullptr;
+	hipError_t release() {
+		void* q = p;
+		p = nullptr;
+		return q ? hipFreeAsync(q, st) : hipSuccess;
+	}
+	~AsyncBuf() { (void)release(); }
+};
+
 int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
 		uint32_t* counts, uint64_t* str_counts) {
 	if (!c || world == 0 || world > 64 || !counts || !str_counts)
@@ -1454,8 +1466,9 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 	HIP_TRY(hipSetDevice(c->device));
 	if (!c->d_collect)
 		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-	unsigned long long* own = nullptr; // cnt, bytes, cur: world each
-	HIP_TRY(hipMallocAsync((void**)&own, 3 * 64 * sizeof(unsigned long long), c->stream));
+	AsyncBuf own_b{c->stream}; // cnt, bytes, cur: world each
+	HIP_TRY(hipMallocAsync(&own_b.p, 3 * 64 * sizeof(unsigned long long), c->stream));
+	unsigned long long* own = (unsigned long long*)own_b.p;
 	HIP_TRY(hipMemsetAsync(own, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
 	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, own, own + 64, c->stream, c->cus));
@@ -1477,16 +1490,17 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 		} else {
 			// records by owner, then their bytes at the scan of their sizes: owner w's bytes are
 			// the str_counts[w] after the earlier owners', in its records' order
-			unsigned long long* tmp = nullptr; // srcoff, nb, offs: total each
-			HIP_TRY(hipMallocAsync((void**)&tmp, 3 * total * sizeof(unsigned long long), c->stream));
+			AsyncBuf tmp_b{c->stream}; // srcoff, nb, offs: total each
+			HIP_TRY(hipMallocAsync(&tmp_b.p, 3 * total * sizeof(unsigned long long), c->stream));
+			unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
 			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, own + 128, recs, tmp, c->stream, c->cus));
 			HIP_TRY(wire_offsets(c, recs, (uint32_t)total, tmp + total, tmp + 2 * total));
 			HIP_TRY(launch_wire_copy(recs, (uint32_t)total, tmp + 2 * total, tmp, c->d_sarena, strings, c->stream, c->cus));
-			HIP_TRY(hipFreeAsync(tmp, c->stream));
+			HIP_TRY(tmp_b.release());
 		}
 	}
-	HIP_TRY(hipFreeAsync(own, c->stream));
+	HIP_TRY(own_b.release());
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return rc;
 }
