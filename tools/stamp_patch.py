@@ -27,9 +27,9 @@ def main():
     out = sys.argv[1]
     s = open(SRC).read()
     # finalize waves
-    s = sub(s, """		uint32_t* fs = sh.fstage + fl;
+    s = sub(s, """		uint32_t uh = 0, un = 0; // wave-uniform: ring head and entries
 		for (;;) {
-			uint32_t c = 0;""", """		uint32_t* fs = sh.fstage + fl;
+			uint32_t c = 0;""", """		uint32_t uh = 0, un = 0; // wave-uniform: ring head and entries
 		unsigned long long S_b = 0, S_poll = 0, S_load = 0, S_fin = 0;
 		for (;;) {
 			unsigned long long P0 = clock64();
@@ -44,17 +44,18 @@ def main():
 			uint32_t q[R_WORDS];""")
     s = sub(s, """				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
 			}
-			if (st == 1) {""", """				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
+			bool unf = false;""", """				lds_store_rel(&sh.freed[slot], pos + 1); // the slot may be written again
 			}
 			unsigned long long P2 = clock64();
 			S_load += P2 - P1;
-			if (st == 1) {""")
-    s = sub(s, """					finalize_rec(d, T, q, fs);
+			bool unf = false;""")
+    s = sub(s, """					unf = finalize_rec(d, T, q, fs);
+			}""", """					unf = finalize_rec(d, T, q, fs);
 			}
+			S_fin += clock64() - P2;""")
+    s = sub(s, """				d.ev_slot[at + lane] = ust[(uh + lane) & 127u];
 		}
-		return;""", """					finalize_rec(d, T, q, fs);
-			}
-			S_fin += clock64() - P2;
+		return;""", """				d.ev_slot[at + lane] = ust[(uh + lane) & 127u];
 		}
 		if (lane == 0 && blockIdx.x < 8)
 			printf("STAMP fin %u %u %llu %llu %llu %llu\\n", blockIdx.x, wave, S_b, S_poll, S_load, S_fin);
