@@ -210,11 +210,6 @@ struct ebd_ctx {
 		hipEvent_t up = nullptr, used = nullptr;
 	};
 	hipStream_t cstream = nullptr, dstream = nullptr;
-	// Aggregator::clear's table reset (ebd_clear): 1 = requested, 2 = running on xstream beside
-	// the next batch's k_fresh (launched after it, into the CU slots k_fresh leaves free)
-	hipStream_t xstream = nullptr;
-	hipEvent_t ev_xpre = nullptr, ev_clear = nullptr;
-	int clear_state = 0;
 	StageSlot stg[2];
 	int next_slot = 0;
 	uint64_t next_ticket = 1;
@@ -276,46 +271,6 @@ static hipError_t timed(ebd_ctx* c, int kernel, F launch) {
 	c->pending.push_back({kernel, a, b});
 	return e;
 }
-
-// timed() on another of the context's streams
-template <typename F>
-static hipError_t timed_on(ebd_ctx* c, int kernel, hipStream_t st, F launch) {
-	if (!(c->cfg.flags & EBD_CFG_TIMING))
-		return launch();
-	hipEvent_t a = take_event(c), b = take_event(c);
-	(void)hipEventRecord(a, st);
-	hipError_t e = launch();
-	(void)hipEventRecord(b, st);
-	c->pending.push_back({kernel, a, b});
-	return e;
-}
-
-// Settles a table reset ebd_clear requested: the context stream runs it (requested only) or
-// waits for it (running on xstream), then resets the table's counters.  run_batch starts it
-// beside k_fresh and joins just before k_agg_fast (the first kernel of a batch that touches the
-// service table); every other entry point that uses the device joins when it takes the lock.
-static int join_clear(ebd_ctx* c) {
-	if (!c->clear_state)
-		return 0;
-	HIP_TRY(hipSetDevice(c->device));
-	if (c->clear_state == 1)
-		HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
-	else
-		HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_clear, 0));
-	c->clear_state = 0;
-	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
-	return 0;
-}
-
-// The context lock; join: settle a pending table reset first (all but the batch submissions).
-struct CtxLock {
-	std::lock_guard<std::mutex> lk;
-	explicit CtxLock(ebd_ctx* c, bool join = true) : lk(c->mu) {
-		if (join)
-			(void)join_clear(c);
-	}
-};
 
 static void drain_timing(ebd_ctx* c) {
 	for (auto& t : c->pending) {
@@ -421,11 +376,9 @@ static void ctx_free(ebd_ctx* c) {
 		if (c->bounce_ev[k])
 			(void)hipEventDestroy(c->bounce_ev[k]);
 	}
-	for (hipEvent_t e : {c->ev_mid, c->ev_end, c->ev_batch, c->ev_res, c->ev_xpre, c->ev_clear})
+	for (hipEvent_t e : {c->ev_mid, c->ev_end, c->ev_batch, c->ev_res})
 		if (e)
 			(void)hipEventDestroy(e);
-	if (c->xstream)
-		(void)hipStreamDestroy(c->xstream);
 	if (c->cstream)
 		(void)hipStreamDestroy(c->cstream);
 	if (c->dstream)
@@ -508,9 +461,6 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
 	CTX_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
 	CTX_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
-	CTX_TRY(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-	CTX_TRY(hipEventCreateWithFlags(&c->ev_xpre, hipEventDisableTiming));
-	CTX_TRY(hipEventCreateWithFlags(&c->ev_clear, hipEventDisableTiming));
 	for (hipEvent_t* e : {&c->ev_mid, &c->ev_end, &c->ev_batch, &c->ev_res, &c->stg[0].up, &c->stg[0].used, &c->stg[1].up,
 			 &c->stg[1].used, &c->bounce_ev[0], &c->bounce_ev[1]})
 		CTX_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -604,8 +554,6 @@ int ebd_ctx_destroy(ebd_ctx* c) {
 		return -EINVAL;
 	(void)hipSetDevice(c->device);
 	(void)hipStreamSynchronize(c->stream);
-	if (c->xstream)
-		(void)hipStreamSynchronize(c->xstream);
 	ctx_free(c);
 	return 0;
 }
@@ -623,7 +571,7 @@ int ebd_get_hash_key(ebd_ctx* c, uint64_t out[2]) {
 int ebd_set_interfaces(ebd_ctx* c, const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6) {
 	if (!c || n4 > 64 || n6 > 32 || (n4 && !v4) || (n6 && !v6))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	std::memset(&c->ifs_host, 0, sizeof(Interfaces));
 	c->ifs_host.n4 = n4;
 	c->ifs_host.n6 = n6;
@@ -778,25 +726,13 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		c->batch_valid = 1;
 		return 0;
 	}
-	const bool xclear = c->clear_state == 1;
-	if (xclear) // the reset may start once everything before this batch is done
-		HIP_TRY(hipEventRecord(c->ev_xpre, c->stream));
 	HIP_TRY(timed(c, KT_FRESH, [&] { return launch_fresh(d, c->stream, c->cus); }));
-	if (xclear) { // queued after k_fresh: its workgroups take the CU slots k_fresh's leave
-		HIP_TRY(hipStreamWaitEvent(c->xstream, c->ev_xpre, 0));
-		HIP_TRY(timed_on(c, KT_CLEAR, c->xstream,
-				[&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->xstream, c->cus); }));
-		HIP_TRY(hipEventRecord(c->ev_clear, c->xstream));
-		c->clear_state = 2;
-	}
 	HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_sset_build(d, c->sset_cap, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipEventRecord(c->ev_mid, c->stream));
 	// Aggregator::newRequest for the fast-path requests: independent of the session path
 	// (k_slow_collect marked the session events, counters and first arrival are order-free)
-	if (int rc = join_clear(c)) // the table reset ran beside the kernels above
-		return rc;
 	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_PUBLISH, [&] { return launch_publish(d, c->stream, c->cus); }));
 	HIP_TRY(hipEventSynchronize(c->ev_mid));
@@ -884,14 +820,14 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 int ebd_submit_batch_device(ebd_ctx* c, const ebd_device_batch* b) {
 	if (!c || !b || (b->n && (!b->events || !b->len || !b->off || !b->payload)))
 		return -EINVAL;
-	CtxLock lk(c, false); // run_batch joins a pending table reset before k_agg_fast
+	std::lock_guard<std::mutex> lk(c->mu);
 	return run_batch(c, (const EventRec*)b->events, b->len, b->off, b->payload, b->payload_bytes, b->n);
 }
 
 int ebd_set_seq_base(ebd_ctx* c, uint64_t seq) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c, false); // host state only
+	std::lock_guard<std::mutex> lk(c->mu);
 	c->seq_base = seq;
 	return 0;
 }
@@ -899,7 +835,7 @@ int ebd_set_seq_base(ebd_ctx* c, uint64_t seq) {
 int ebd_kernel_times(ebd_ctx* c, ebd_kernel_time* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	(void)hipSetDevice(c->device);
 	drain_timing(c);
 	*n = KT_N;
@@ -919,7 +855,7 @@ int ebd_kernel_times(ebd_ctx* c, ebd_kernel_time* out, uint32_t cap, uint32_t* n
 int ebd_reset_kernel_times(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	(void)hipSetDevice(c->device);
 	drain_timing(c);
 	for (int k = 0; k < 16; k++) {
@@ -932,7 +868,7 @@ int ebd_reset_kernel_times(ebd_ctx* c) {
 int ebd_sync(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	HIP_TRY(hipStreamSynchronize(c->cstream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1085,14 +1021,14 @@ int ebd_stage_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32_
 		return -EINVAL;
 	if (int rc = validate_batch(c, events, len, off, payload, payload_bytes, n))
 		return rc;
-	CtxLock lk(c, false); // run_batch joins a pending table reset before k_agg_fast
+	std::lock_guard<std::mutex> lk(c->mu);
 	return stage_locked(c, events, len, off, payload, payload_bytes, n, ticket);
 }
 
 int ebd_submit_staged(ebd_ctx* c, uint64_t ticket) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c, false); // run_batch joins a pending table reset before k_agg_fast
+	std::lock_guard<std::mutex> lk(c->mu);
 	return submit_staged_locked(c, ticket);
 }
 
@@ -1102,7 +1038,7 @@ int ebd_submit_batch(ebd_ctx* c, const ebd_discovery_event* events, const uint32
 		return -EINVAL;
 	if (int rc = validate_batch(c, events, len, off, payload, payload_bytes, n))
 		return rc;
-	CtxLock lk(c, false); // run_batch joins a pending table reset before k_agg_fast
+	std::lock_guard<std::mutex> lk(c->mu);
 	uint64_t t = 0;
 	if (int rc = stage_locked(c, events, len, off, payload, payload_bytes, n, &t))
 		return rc;
@@ -1134,7 +1070,7 @@ int ebd_host_free(ebd_ctx* c, void* p) {
 int ebd_fetch_results_async(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n || (cap && !out))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	*n = c->last_n;
 	if (!out)
 		return 0; // size query
@@ -1154,7 +1090,7 @@ int ebd_fetch_results_async(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uin
 int ebd_fetch_results(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n || (cap && !out))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	*n = c->last_n;
 	if (!out)
 		return 0; // size query
@@ -1173,7 +1109,7 @@ int ebd_fetch_session_requests(ebd_ctx* c, ebd_session_request* out, uint32_t ca
 		uint64_t strcap, uint64_t* strlen) {
 	if (!c || !n || !strlen)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	if (int rc = finish_pending(c))
 		return rc;
 	*n = (uint32_t)c->last_sreq;
@@ -1195,7 +1131,7 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 		uint64_t* strlen) {
 	if (!c || !n || !strlen)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1272,20 +1208,20 @@ static int clear_keep_nets(ebd_ctx* c) {
 int ebd_clear(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (c->net_on)
 		return clear_keep_nets(c);
-	// requested: the next batch runs it beside its k_fresh, k_sset_build and k_slow_collect
-	// (which do not touch the service table); any other call runs it first (join_clear)
-	c->clear_state = 1;
+	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
+	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SERVICES, 0, sizeof(unsigned long long), c->stream));
 	return 0;
 }
 
 int ebd_set_clock(ebd_ctx* c, uint64_t now_ns) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c, false); // host state only
+	std::lock_guard<std::mutex> lk(c->mu);
 	c->clock_ns = now_ns;
 	return 0;
 }
@@ -1293,7 +1229,7 @@ int ebd_set_clock(ebd_ctx* c, uint64_t now_ns) {
 int ebd_set_event_clock(ebd_ctx* c, const uint64_t* time_ns) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c, false); // host state only
+	std::lock_guard<std::mutex> lk(c->mu);
 	c->ev_times = time_ns;
 	return 0;
 }
@@ -1301,7 +1237,7 @@ int ebd_set_event_clock(ebd_ctx* c, const uint64_t* time_ns) {
 int ebd_network_counters_cleaning(ebd_ctx* c, uint64_t now_ns) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	if (!c->net_on)
 		return 0; // every map is empty
 	HIP_TRY(hipSetDevice(c->device));
@@ -1324,7 +1260,7 @@ int ebd_network_counters_cleaning(ebd_ctx* c, uint64_t now_ns) {
 int ebd_collect_networks(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	*n = 0;
 	if (!c->net_on)
 		return 0;
@@ -1350,7 +1286,7 @@ int ebd_collect_networks(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_
 int ebd_collect_networks_device(ebd_ctx* c, ebd_service_net* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	*n = 0;
 	if (!c->net_on)
 		return 0;
@@ -1368,7 +1304,7 @@ int ebd_collect_networks_device(ebd_ctx* c, ebd_service_net* out, uint32_t cap, 
 int ebd_merge_networks_device(ebd_ctx* c, const ebd_service_net* recs, uint32_t n) {
 	if (!c || (n && !recs))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	if (n == 0)
 		return 0;
 	if (!c->net_on)
@@ -1384,7 +1320,7 @@ int ebd_merge_networks_device(ebd_ctx* c, const ebd_service_net* recs, uint32_t 
 int ebd_reset_services(ebd_ctx* c) {
 	if (!c)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	HIP_TRY(timed(c, KT_CLEAR, [&] { return launch_clear_used(c->d_new_slots, c->d_ctr, c->d_slots, c->slot_cap, c->stream, c->cus); }));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_SARENA, 0, sizeof(unsigned long long), c->stream));
@@ -1462,7 +1398,7 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 		uint32_t* counts, uint64_t* str_counts) {
 	if (!c || world == 0 || world > 64 || !counts || !str_counts)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (!c->d_collect)
 		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
@@ -1508,7 +1444,7 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen) {
 	if (!c || (n && (!recs || (!strings && strlen))))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
@@ -1532,7 +1468,7 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 int ebd_merge_service_keys_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, uint64_t* dst) {
 	if (!c || (n && (!recs || !dst)))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
@@ -1552,7 +1488,7 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 		const uint8_t* need, uint8_t* out, uint64_t outcap, uint64_t* out_len) {
 	if (!c || !out_len || (n && (!recs || !need || (!strings && strlen))))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	*out_len = 0;
 	if (n == 0)
@@ -1585,7 +1521,7 @@ int ebd_merge_service_bytes_device(ebd_ctx* c, const ebd_wire_service* recs, uin
 		uint64_t strlen) {
 	if (!c || (n && (!recs || !dst || (!strings && strlen))))
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
@@ -1612,7 +1548,7 @@ int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, cons
 				need > strings_len - q.str_off)
 			return -EINVAL;
 	}
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (int rc = finish_pending(c))
 		return rc;
@@ -1647,7 +1583,7 @@ int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, cons
 int ebd_get_stats(ebd_ctx* c, ebd_stats* s) {
 	if (!c || !s)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
 	if (int rc = finish_pending(c))
 		return rc;
@@ -1937,7 +1873,7 @@ static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out
 int ebd_trace_size_device(ebd_ctx* c, const ebd_trace_config* t, uint32_t* n_events, uint64_t* payload_bytes) {
 	if (!c || !trace_ok(t) || !payload_bytes || t->n == 0)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	return trace_device(c, t, nullptr, n_events, payload_bytes);
 }
 
@@ -1945,7 +1881,7 @@ int ebd_trace_generate_device(ebd_ctx* c, const ebd_trace_config* t, ebd_discove
 		uint8_t* payload, uint64_t payload_cap, uint64_t* gidx) {
 	if (!c || !trace_ok(t) || t->n == 0 || !events || !len || !off || !payload)
 		return -EINVAL;
-	CtxLock lk(c);
+	std::lock_guard<std::mutex> lk(c->mu);
 	const GenOut o{(EventRec*)events, len, off, payload, payload_cap, gidx};
 	return trace_device(c, t, &o, nullptr, nullptr);
 }

@@ -2403,29 +2403,31 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 					stop = 1; // the window ends at eviction j
 					break;
 				}
-				uint32_t k = 0;
-				const uint32_t rec0 = rec;
-				uint32_t myv = 0, myq = 0; // lane jl: eviction j + jl's victim and recorded front
-				// one loop over the block's evictions; a window without a live marker for the
-				// current eviction loads the next one (its markers are dead for every later
-				// eviction too)
+				uint32_t k = 0; // evictions of the block done
 				uint32_t wb = qf & ~63u, p = qf - wb;
 				if (wb >= nmk)
 					bad = 1; // a full cache and no live marker
 				else if (wb + 64 > mb + kGrM)
 					restage = 1; // the staged markers are used up
-				uint32_t e = !bad && !restage && wb + lane < nmk ? se[wb - mb + lane] : 0u;
+				if (!bad && !restage && j >= rec) { // the front before the block's first eviction
+					if (lane == 0)
+						qfe[j] = qf;
+					rec = j + 1;
+				}
 				while (k < nj && !bad && !restage) {
-					// the front after eviction k - 1, before any window this eviction skips: a
-					// later round resumes there, and its eviction k may come earlier
-					if (j + k >= rec) {
-						myq = lane == k ? wb + p : myq;
-						rec = j + k + 1;
+					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
+					// c: the block's evictions at whose times this marker is alive (e > time), a
+					// prefix of them since the times ascend: a binary search over the lanes' times
+					uint32_t c = 0;
+					for (uint32_t st = 64; st > 0; st >>= 1) {
+						const uint32_t mid = c + st;
+						const uint32_t tm = (uint32_t)__shfl((int)tv, (int)((mid - 1) & 63u), 64);
+						if (mid <= nj && tm < e)
+							c = mid;
 					}
-					const uint32_t tt = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)k); // a scalar, not a bpermute
-					const unsigned long long m = __ballot(wb + lane < nmk && (e == kNone || e > tt)); // alive at tt
-					const unsigned long long avail = p >= 64 ? 0ull : m & (~0ull << p);
-					if (avail == 0) {
+					if (lane < p)
+						c = 0; // taken or passed over already
+					if (__ballot(c > k) == 0) { // no marker of the window alive at eviction k: none later
 						wb += 64;
 						p = 0;
 						if (wb >= nmk) {
@@ -2436,20 +2438,46 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 							restage = 1;
 							break;
 						}
-						e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
 						continue;
 					}
-					const uint32_t v = (uint32_t)__builtin_ctzll(avail);
-					myv = lane == k ? wb + v : myv;
-					p = v + 1;
-					k++;
+					// the greedy over the window's markers in order, in scalar registers: marker L
+					// is taken by eviction A (the evictions done so far) when it is alive then
+					unsigned long long cons = 0;
+					uint32_t A = k;
+#pragma unroll
+					for (uint32_t L = 0; L < 64; L++) {
+						const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)L);
+						const bool take = A < cl;
+						cons |= take ? (1ull << L) : 0ull;
+						A += take ? 1u : 0u;
+					}
+					// marker lane L taken by eviction a: the victim, and the front before eviction
+					// a + 1 (a later round resumes there); one scattered vector store each
+					if ((cons >> lane) & 1ull) {
+						const uint32_t a = k + __builtin_amdgcn_mbcnt_hi((uint32_t)(cons >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cons, 0));
+						vict[j + a] = wb + lane;
+						if (a + 1 < nj)
+							qfe[j + a + 1] = wb + lane + 1;
+					}
+					rec = max(rec, j + min(A + 1, nj));
+					if (A == nj) { // the block is done: the front follows its last victim
+						p = 64u - (uint32_t)__builtin_clzll(cons);
+						k = A;
+						break;
+					}
+					k = A; // every marker of the window is taken or dead: the next window
+					wb += 64;
+					p = 0;
+					if (wb >= nmk) {
+						bad = 1;
+						break;
+					}
+					if (wb + 64 > mb + kGrM) {
+						restage = 1;
+						break;
+					}
 				}
 				qf = wb + p;
-				// one vector store each for the block's victims and fronts
-				if (lane < k)
-					vict[j + lane] = myv;
-				if (j + lane >= rec0 && j + lane < rec)
-					qfe[j + lane] = myq;
 				j += k;
 			}
 			if (lane == 0) {
