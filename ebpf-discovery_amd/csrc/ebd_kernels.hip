@@ -2416,18 +2416,10 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 				}
 				while (k < nj && !bad && !restage) {
 					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
-					// c: the block's evictions at whose times this marker is alive (e > time), a
-					// prefix of them since the times ascend: a binary search over the lanes' times
-					uint32_t c = 0;
-					for (uint32_t st = 64; st > 0; st >>= 1) {
-						const uint32_t mid = c + st;
-						const uint32_t tm = (uint32_t)__shfl((int)tv, (int)((mid - 1) & 63u), 64);
-						if (mid <= nj && tm < e)
-							c = mid;
-					}
-					if (lane < p)
-						c = 0; // taken or passed over already
-					if (__ballot(c > k) == 0) { // no marker of the window alive at eviction k: none later
+					// most windows between the queue's front and the window end hold only dead
+					// markers: one compare at eviction k's time passes over them
+					const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)k);
+					if (__ballot(lane >= p && e > tk) == 0) {
 						wb += 64;
 						p = 0;
 						if (wb >= nmk) {
@@ -2440,6 +2432,17 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 						}
 						continue;
 					}
+					// c: the block's evictions at whose times this marker is alive (e > time), a
+					// prefix of them since the times ascend: a binary search over the lanes' times
+					uint32_t c = 0;
+					for (uint32_t st = 64; st > 0; st >>= 1) {
+						const uint32_t mid = c + st;
+						const uint32_t tm = (uint32_t)__shfl((int)tv, (int)((mid - 1) & 63u), 64);
+						if (mid <= nj && tm < e)
+							c = mid;
+					}
+					if (lane < p)
+						c = 0; // taken or passed over already
 					// the greedy over the window's markers in order, in scalar registers: marker L
 					// is taken by eviction A (the evictions done so far) when it is alive then
 					unsigned long long cons = 0;
