@@ -2450,9 +2450,9 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 #pragma unroll
 					for (uint32_t L = 0; L < 64; L++) {
 						const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)L);
-						const bool take = A < cl;
-						cons |= take ? (1ull << L) : 0ull;
-						A += take ? 1u : 0u;
+						const uint32_t take = (A - cl) >> 31; // A < cl (both at most 64): integer ops, so
+						cons |= (unsigned long long)take << L; // the chain stays in scalar registers
+						A += take;
 					}
 					// marker lane L taken by eviction a: the victim, and the front before eviction
 					// a + 1 (a later round resumes there); one scattered vector store each
