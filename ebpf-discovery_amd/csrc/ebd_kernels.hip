@@ -2163,7 +2163,9 @@ __global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, uint3
 }
 
 // Phase 1: each block's composed size map and its marker count.
-__global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint32_t n, uint32_t cap, LFn* bf, uint32_t* bm) {
+// zero: a per-event byte array cleared on the way (the round's victim flags, nf_t).
+__global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint32_t n, uint32_t cap, LFn* bf, uint32_t* bm,
+		uint8_t* zero) {
 	__shared__ LFn F[kLsT];
 	__shared__ uint32_t M[kLsT];
 	const uint32_t t = threadIdx.x;
@@ -2172,6 +2174,8 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint
 	uint32_t m = 0;
 	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
 		const unsigned long long i = base + k;
+		if (i < n)
+			zero[i] = 0;
 		const uint32_t op = i < n ? opt[i] : OP_NONE;
 		f = lfn_then(f, lfn_op(op, cap));
 		m += op_marks(op) ? 1u : 0u;
@@ -2195,11 +2199,14 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint
 // Phase 2 (one workgroup of kLsT threads, kLsT scan blocks at a time): each scan block's
 // starting size from the context's carried sessions, and its first marker's index (after the
 // carried ones).
+// zc, zn: the round's carried-session flags (ncf), cleared on the way.
 __global__ __launch_bounds__(kLsT) void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0,
-		long long* lst, uint32_t* moff, uint32_t* tot) {
+		long long* lst, uint32_t* moff, uint32_t* tot, uint8_t* zc, uint32_t zn) {
 	__shared__ LFn F[kLsT];
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
+	for (uint32_t k = t; k < zn; k += kLsT)
+		zc[k] = 0;
 	long long x = l0;
 	uint32_t m = m0;
 	for (uint32_t c = 0; c < nb; c += kLsT) {
@@ -3559,6 +3566,16 @@ hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipS
 // where flags changed or the last walk stopped), then the world the evictions before the
 // horizon imply in nf / ncf; cnt[1] inconsistency, cnt[2] flags changed, cnt[3] the new
 // frontier.
+// A round's counters: the walk list (tot[3]), the victims listed (tot[4]), and cnt (evictions,
+// inconsistency, flags changed, first changed event).
+__global__ void k_lru_round_reset(uint32_t* tot, unsigned long long* cnt) {
+	if (threadIdx.x == 0) {
+		tot[3] = tot[4] = 0;
+		cnt[0] = cnt[1] = cnt[2] = 0;
+		cnt[3] = ~0ull;
+	}
+}
+
 hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t front, uint32_t window, hipStream_t st,
 		int cus) {
 	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
@@ -3568,20 +3585,13 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 	uint8_t* ncf = w.cf[cur ^ 1];
 	const unsigned long long tend64 = (unsigned long long)front + window;
 	const uint32_t tend = (uint32_t)(tend64 < 0xffffffffull ? tend64 : 0xffffffffull);
-	hipError_t e;
-	if ((e = hipMemsetAsync(w.tot + 3, 0, sizeof(uint32_t), st)) != hipSuccess)
-		return e;
+	hipLaunchKernelGGL(k_lru_round_reset, dim3(1), dim3(64), 0, st, w.tot, w.cnt);
 	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, tend, w.rlist, w.tot);
 	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
 			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, tend}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
-	if ((e = hipMemsetAsync(ncf, 0, d.carry_cap, st)) != hipSuccess || (e = hipMemsetAsync(w.nf_t, 0, n, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.tot + 4, 0, sizeof(uint32_t), st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cnt, 0, 3 * sizeof(unsigned long long), st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cnt + 3, 0xff, sizeof(unsigned long long), st)) != hipSuccess)
-		return e;
-	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm);
+	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm, w.nf_t);
 	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(kLsT), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
-			w.moff, w.tot);
+			w.moff, w.tot, ncf, d.carry_cap);
 	hipLaunchKernelGGL(k_lru_scan_apply, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (const long long*)w.lst,
 			w.evt, w.be);
 	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(kLsT), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
