@@ -174,6 +174,7 @@ struct ebd_ctx {
 	uint32_t* d_lru_live = nullptr;
 	uint64_t lru_batches_exact = 0;
 	uint64_t lru_rounds = 0, lru_sequential = 0;
+	uint32_t lru_window = 0; // exact-LRU derivation window (0: EBD_LRU_WINDOW or 8192)
 	LruRound lr{};              // the exact-LRU rounds' scratch (allocated on first need)
 	void* lr_mem = nullptr;
 	unsigned long long* h_lr = nullptr; // pinned: a round's counters
@@ -652,14 +653,17 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	static const bool lru_trace = std::getenv("EBD_LRU_TRACE") != nullptr; // per-round progress on stderr
 	// the window trades rounds (a round settles at most the window) against each round's merge
 	// work (it re-derives the whole window); EBD_LRU_WINDOW overrides it
-	static const uint32_t window = [] {
+	static const uint32_t env_window = [] {
 		const char* v = std::getenv("EBD_LRU_WINDOW");
 		const long w = v ? std::atol(v) : 0;
 		return w > 0 ? (uint32_t)w : 8192u; // 1 M config-4 events, LRU 2048: 2048 -> 523 ms, 4096 -> 394, 8192 -> 347, 16384 -> 387
 	}();
+	const uint32_t window = c->lru_window ? c->lru_window : env_window;
 	int cur = 0;
 	uint32_t front = 0;
-	const int max_rounds = 4096;
+	// a round settles at least one event and usually most of a window (1 M config-4 events: ~3.3
+	// rounds per window), so the cap grows with the windows the batch holds
+	const int max_rounds = (int)std::min<unsigned long long>(1ull << 30, 4096ull + 8ull * ((d.n + window - 1) / window));
 	for (int r = 0; r < max_rounds; r++) {
 		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, front, window, c->stream, c->cus); }));
 		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
@@ -1453,14 +1457,14 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 		return rc;
 	Dev d = make_dev(c);
 	d.n = 0;
-	unsigned long long* tmp = nullptr; // nb, offs
-	HIP_TRY(hipMallocAsync((void**)&tmp, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c->stream}; // nb, offs
+	HIP_TRY(hipMallocAsync(&tmp_b.p, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
-	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_EVICTIONS, 0, sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_merge(d, recs, n, strings, strlen, tmp + n, c->stream, c->cus));
 	HIP_TRY(launch_verify(d, c->stream, c->cus));
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(tmp_b.release());
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
@@ -1493,8 +1497,9 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 	*out_len = 0;
 	if (n == 0)
 		return 0;
-	unsigned long long* tmp = nullptr; // nb, soff, nbn, doff
-	HIP_TRY(hipMallocAsync((void**)&tmp, 4 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c->stream}; // nb, soff, nbn, doff
+	HIP_TRY(hipMallocAsync(&tmp_b.p, 4 * (size_t)n * sizeof(unsigned long long), c->stream));
+	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(launch_wire_bytes_needed(recs, n, need, nullptr, tmp + 2 * (size_t)n, c->stream, c->cus));
 	HIP_TRY(excl_scan(c, tmp + 2 * (size_t)n, tmp + 3 * (size_t)n, n));
@@ -1511,7 +1516,7 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 			HIP_TRY(launch_wire_compact(recs, n, need, tmp + n, tmp + 3 * (size_t)n, strings, strlen, out, outcap, c->d_ctr, c->stream,
 					c->cus));
 	}
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(tmp_b.release());
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	*out_len = total;
 	return rc;
@@ -1527,12 +1532,13 @@ int ebd_merge_service_bytes_device(ebd_ctx* c, const ebd_wire_service* recs, uin
 		return 0;
 	Dev d = make_dev(c);
 	d.n = 0;
-	unsigned long long* tmp = nullptr; // nb, offs
-	HIP_TRY(hipMallocAsync((void**)&tmp, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c->stream}; // nb, offs
+	HIP_TRY(hipMallocAsync(&tmp_b.p, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(launch_wire_bytes_needed(recs, n, nullptr, (const unsigned long long*)dst, tmp, c->stream, c->cus));
 	HIP_TRY(excl_scan(c, tmp, tmp + n, n));
 	HIP_TRY(launch_merge_bytes(d, recs, n, (const unsigned long long*)dst, tmp + n, strings, strlen, c->stream, c->cus));
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
+	HIP_TRY(tmp_b.release());
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
@@ -2083,6 +2089,14 @@ int ebd_host_endpoint_key(const uint64_t hash_key[2], uint32_t pid, const uint8_
 	const Hash128 h = kh.finish();
 	key[0] = h.lo;
 	key[1] = h.hi;
+	return 0;
+}
+
+int ebd_testing_set_lru_window(ebd_ctx* c, uint32_t window) {
+	if (!c)
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	c->lru_window = window;
 	return 0;
 }
 

@@ -2872,8 +2872,11 @@ __global__ void k_verify(Dev d) {
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
 		if (d.slots[d.verify[k].slot].hi != d.verify[k].hi)
 			set_error(d, EBD_ERR_COLLISION);
-	if (blockIdx.x == 0 && threadIdx.x == 0) // the last kernel of a batch: batch totals into run totals
+	if (blockIdx.x == 0 && threadIdx.x == 0) { // the last kernel of a batch: batch totals into run totals,
+		// consumed, so a later k_verify (key merges, ebd_aggregate_requests) adds nothing twice
 		d.ctr[CTR_EVICTIONS_TOTAL] += d.ctr[CTR_EVICTIONS];
+		d.ctr[CTR_EVICTIONS] = 0;
+	}
 }
 
 __device__ __forceinline__ Slot empty_slot() {

@@ -167,6 +167,7 @@ _SIGS = {
     "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
                                     C.c_uint32]),
     "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "ebd_testing_set_lru_window": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_host_endpoint_key": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
 }
 
@@ -321,10 +322,11 @@ class Context:
         _check(lib().ebd_fetch_results_async(self.h, _p(out), out.size, C.byref(n)), "ebd_fetch_results_async")
         return n.value
 
-    def _fence(self, *tensors):
+    def _fence(self, *tensors, hold=True):
         """The context stream waits for the work torch queued for these tensors on its current
         stream (the context stream is a non-blocking stream: it does not order itself after
-        torch's).  Raw pointers are the caller's to order."""
+        torch's).  Raw pointers are the caller's to order.  hold=False: the C call blocks until
+        the context stream is done with them, so nothing needs to keep them alive."""
         import torch
         ts = [t for t in tensors if isinstance(t, torch.Tensor) and t.is_cuda]
         if not ts:
@@ -335,7 +337,8 @@ class Context:
         # and the tensors stay referenced until the context's queued work is known done (sync,
         # close): torch's caching allocator may not hand their memory out again before then.
         # (record_stream on the context's stream would outlive it: ebd_ctx_destroy destroys it.)
-        self._held.extend(ts)
+        if hold:
+            self._held.extend(ts)
 
     def submit_device(self, events, lens, offs, payload, n, payload_bytes=None):
         """Device-resident batch (torch tensors on the context's device or raw pointers).
@@ -494,7 +497,7 @@ class Context:
         n, sb = int(counts.sum()), int(scounts.sum())
         recs = torch.empty(max(n, 1) * WIRE_DTYPE.itemsize, dtype=torch.uint8, device=device)
         strs = torch.empty(max(sb, 8), dtype=torch.uint8, device=device)
-        self._fence(recs, strs)  # torch may hand back memory its stream still uses
+        self._fence(recs, strs, hold=False)  # torch may hand back memory its stream still uses
         _check(lib().ebd_export_services_device(self.h, world, C.c_void_p(recs.data_ptr()), max(n, 1),
                                                 C.c_void_p(strs.data_ptr()), strs.numel(), _p(counts), _p(scounts)),
                "ebd_export_services_device")
@@ -504,7 +507,7 @@ class Context:
         """Inserts wire records (device uint8 tensors; strings readable 8 bytes past their
         bytes) into this table."""
         n = recs.numel() // WIRE_DTYPE.itemsize
-        self._fence(recs, strings)
+        self._fence(recs, strings, hold=False)
         _check(lib().ebd_merge_services_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
                                                C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                strings.numel()), "ebd_merge_services_device")
@@ -517,7 +520,7 @@ class Context:
         assert dst.dtype == __import__("torch").int64 and dst.numel() == n
         if n == 0:
             return
-        self._fence(recs, dst)
+        self._fence(recs, dst, hold=False)
         _check(lib().ebd_merge_service_keys_device(self.h, C.c_void_p(recs.data_ptr()), n, C.c_void_p(dst.data_ptr())),
                "ebd_merge_service_keys_device")
 
@@ -529,13 +532,13 @@ class Context:
         assert need.dtype == torch.uint8 and need.numel() == n
         if n == 0:
             return torch.empty(0, dtype=torch.uint8, device=recs.device)
-        self._fence(recs, strings, need)
+        self._fence(recs, strings, need, hold=False)
         ln = C.c_uint64(0)
         sp = C.c_void_p(strings.data_ptr()) if strings.numel() else None
         _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
                                              C.c_void_p(need.data_ptr()), None, 0, C.byref(ln)), "ebd_wire_compact_device")
         out = torch.empty(max(int(ln.value), 8), dtype=torch.uint8, device=recs.device)
-        self._fence(out)
+        self._fence(out, hold=False)
         _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
                                              C.c_void_p(need.data_ptr()), C.c_void_p(out.data_ptr()), out.numel(),
                                              C.byref(ln)), "ebd_wire_compact_device")
@@ -547,7 +550,7 @@ class Context:
         n = recs.numel() // WIRE_DTYPE.itemsize
         if n == 0:
             return
-        self._fence(recs, dst, strings)
+        self._fence(recs, dst, strings, hold=False)
         _check(lib().ebd_merge_service_bytes_device(self.h, C.c_void_p(recs.data_ptr()), n, C.c_void_p(dst.data_ptr()),
                                                     C.c_void_p(strings.data_ptr()) if strings.numel() else None,
                                                     strings.numel()), "ebd_merge_service_bytes_device")
@@ -567,6 +570,10 @@ class Context:
             strings += host + url + (cip or b"")
         sb = np.frombuffer(bytes(strings) or b"\0", np.uint8)
         _check(lib().ebd_aggregate_requests(self.h, _p(recs), len(recs), _p(sb), len(strings)), "ebd_aggregate_requests")
+
+    def set_lru_window(self, window):
+        """The exact LRU's derivation window (testing hook; 0 = default)."""
+        _check(lib().ebd_testing_set_lru_window(self.h, window), "ebd_testing_set_lru_window")
 
     def stats(self):
         s = Stats()

@@ -46,6 +46,10 @@ int ebd_host_classify(const uint8_t* token, uint32_t len, int is_source, uint8_t
  * key[0] = lo, key[1] = hi.  The fast path computes the same key word by word from spans. */
 int ebd_host_endpoint_key(const uint64_t hash_key[2], uint32_t pid, const uint8_t* endpoint, uint32_t len, uint64_t key[2]);
 
+/* The exact LRU's derivation window in events (0: EBD_LRU_WINDOW or the default 8192), so a
+ * test can make one batch span several windows and resumed walks. */
+int ebd_testing_set_lru_window(ebd_ctx* ctx, uint32_t window);
+
 /* inet_pton restatement used on the device: 1 = parsed. */
 int ebd_host_pton(int af6, const uint8_t* text, uint32_t len, uint8_t* out);
 

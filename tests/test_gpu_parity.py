@@ -19,9 +19,11 @@ def b(s):
     return s.encode("latin-1")
 
 
-def run_gpu(ev, lens, offs, payload, batches=1, lru=0, v4=(), v6=(), max_events=None):
+def run_gpu(ev, lens, offs, payload, batches=1, lru=0, v4=(), v6=(), max_events=None, lru_window=0):
     n = len(ev)
     ctx = ebd.Context(max_events=max_events or max(n, 1), max_payload=payload.size, lru_capacity=lru)
+    if lru_window:
+        ctx.set_lru_window(lru_window)
     if v4 or v6:
         ctx.set_interfaces(v4, v6)
     views = []
@@ -384,25 +386,54 @@ def test_device_sharded_generator_matches_host():
             assert pd[a:a + int(hl[i])].tobytes() == hp[a:a + int(hl[i])].tobytes()
 
 
-@pytest.mark.parametrize("cap,n_conn,window,batches", [(64, 600, 256, 1), (64, 600, 256, 4), (8192, 11000, 11000, 1),
-                                                       (8192, 11000, 11000, 3)])
-def test_lru_eviction_exact(cap, n_conn, window, batches):
+@pytest.mark.parametrize("cap,n_conn,window,batches,lru_window", [(64, 600, 256, 1, 0), (64, 600, 256, 4, 0),
+                                                                  (8192, 11000, 11000, 1, 0), (8192, 11000, 11000, 3, 0),
+                                                                  (64, 600, 256, 1, 97), (64, 600, 256, 2, 301)])
+def test_lru_eviction_exact(cap, n_conn, window, batches, lru_window):
     """More live sessions than the LRU holds (LRUCache.h:50-89; Discovery.cpp:39): the full
     cache evicts its least recently used session on insert, whose later buffers then parse
-    as new sessions.  The exact walker (k_walk_lru) must reproduce the oracle's LRU event for
-    event, within a batch and across batches (recency carried with the sessions)."""
+    as new sessions.  The exact LRU (walk-and-derive rounds, k_lru_*) must reproduce the
+    oracle's LRU event for event, within a batch and across batches (recency carried with the
+    sessions), and must settle by itself: no batch may fall back to the one-lane replay.  A
+    small derivation window makes one batch span many windows, so resumed walks (states
+    restored from the per-event snapshot) run on the device."""
     ev, lens, offs, payload = T.fragmented_trace(n_conn, seed=31, window=window)
-    gv, gs, gst, _ = run_gpu(ev, lens, offs, payload, batches=batches, lru=cap)
+    gv, gs, gst, _ = run_gpu(ev, lens, offs, payload, batches=batches, lru=cap, lru_window=lru_window)
     ov, os_, ost = run_oracle(ev, lens, offs, payload, lru=cap)
     assert ost["lru_evictions"] > 0
     assert gst["errors"] == 0, gst
     assert gst["lru_exact_batches"] >= 1
+    assert gst["lru_sequential"] == 0 and gst["lru_rounds"] > 0, gst
+    if lru_window:
+        assert gst["lru_rounds"] > len(ev) // batches // lru_window, gst  # several windows per batch
     bad = [i for i in range(len(ov)) if gv[i] != ov[i]]
     assert not bad, [(i, gv[i], ov[i]) for i in bad[:5]]
     assert gs == os_
     assert gst["kernel_deletes"] == ost["kernel_deletes"]
     assert gst["live_sessions"] == ost["lru_size"]
     assert gst["lru_evictions"] == ost["lru_evictions"]
+
+
+def test_lru_evictions_counted_once_across_merges():
+    """ebd_get_stats().lru_evictions after an evicting batch stays put through the calls that
+    run k_verify again (ebd_merge_service_keys_device, ebd_aggregate_requests): the batch's
+    evictions enter the run total once."""
+    import torch
+    ev, lens, offs, payload = T.fragmented_trace(600, seed=31, window=256)
+    _, _, gst, ctx = run_gpu(ev, lens, offs, payload, lru=64)
+    ost = run_oracle(ev, lens, offs, payload, lru=64)[2]
+    assert gst["lru_evictions"] == ost["lru_evictions"] > 0
+    recs, strs, counts, scounts = ctx.export_services_device(1, "cuda")
+    dst = torch.empty(int(counts[0]), dtype=torch.int64, device="cuda")
+    other = ebd.Context(max_events=16, hash_key=ctx.hash_key)
+    other.merge_service_keys_device(recs, dst)
+    assert other.stats()["lru_evictions"] == 0
+    ctx.merge_service_keys_device(recs, dst)
+    assert ctx.stats()["lru_evictions"] == gst["lru_evictions"]
+    ctx.aggregate_requests([(7, b"h", b"/x", None, 2, False, b"\x0a\0\0\x01")])
+    assert ctx.stats()["lru_evictions"] == gst["lru_evictions"]
+    ctx.aggregate_requests([(7, b"h", b"/y", None, 2, False, b"\x0a\0\0\x01")])
+    assert ctx.stats()["lru_evictions"] == gst["lru_evictions"]
 
 
 def test_lru_bound_keeps_parallel_walker_when_no_eviction():
