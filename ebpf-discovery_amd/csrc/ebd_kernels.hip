@@ -531,74 +531,65 @@ enum : uint32_t { EK_PARSE = 0, EK_SKIP = 1, EK_BAD = 2, EK_NONE = 3 };
 // the first j0 precede the buffer.  Other buffers use buffer-relative windows (j0 = 0).
 struct LaneEv {
 	uint32_t idx;
-	uint32_t L;       // buffer length (0 unless EK_PARSE)
-	uint32_t kind;
-	uint32_t pf;      // pid (the DiscoveryEvent's, Discovery.cpp:136, 157)
-	uint32_t flags;
-	uint32_t j0;      // pieces of window 0 before the buffer
-	uint32_t lastp;   // the buffer's last piece, counted from base
-	const uint8_t* p; // buffer (a harmless valid address unless EK_PARSE)
-	unsigned long long base; // window 0's first byte
-	v4u src;          // the session's source address (DiscoverySockSourceIP), classified by finalize
+	uint32_t L;  // buffer length (0 unless EK_PARSE)
+	uint32_t pf; // pid (the DiscoveryEvent's, Discovery.cpp:136, 157)
+	uint32_t m;  // kind | j0 << 2 | flags << 8; j0 = pieces of window 0 before the buffer
+	unsigned long long base; // window 0's first byte (a harmless valid address unless EK_PARSE)
+	__device__ __forceinline__ uint32_t kind() const { return m & 3u; }
+	__device__ __forceinline__ uint32_t j0() const { return (m >> 2) & 3u; }
+	__device__ __forceinline__ uint32_t flags() const { return m >> 8; }
+	// the buffer's last piece, counted from base
+	__device__ __forceinline__ uint32_t lastp() const { return L ? (16u * j0() + L - 1u) >> 4 : 0u; }
+	__device__ __forceinline__ const uint8_t* p() const { return (const uint8_t*)(uintptr_t)(base + 16u * j0()); }
 };
 
 // An event's words as loaded (lane_ev decodes them).  Decoding the next event only where it
 // is first needed (a window later) was measured slower: 3.02 against 2.90 ms per 20 M config-3
-// events, same box.
+// events, same box.  The source address is not carried: finalize reads it from the event.
 struct LaneRaw {
-	uint32_t idx, pf, flags, len; // flags bit 8: past the workgroup's range
+	uint32_t idx, pf, flags, len, past; // past: beyond the workgroup's range (no event)
 	unsigned long long off;
-	v4u src;
 };
 
+// Branch-free: an index past the range loads event 0's words (and is marked so), so every call
+// issues the same four loads and the scan loop's memory counter waits stay exact.
 __device__ __forceinline__ LaneRaw lane_load(const Dev& d, uint32_t i, uint32_t end) {
 	LaneRaw r;
 	r.idx = i;
-	if (i >= end) {
-		r.pf = r.len = 0;
-		r.flags = 0x100u;
-		r.off = 0;
-		r.src = v4u{0u, 0u, 0u, 0u};
-		return r;
-	}
-	const uint8_t* evb = (const uint8_t*)(d.ev + i);
+	const uint32_t j = i < end ? i : 0u;
+	const uint8_t* evb = (const uint8_t*)(d.ev + j);
+	r.past = i < end ? 0u : 1u; // kept apart from the loaded words: nothing here waits for them
 	r.flags = evb[32];
 	r.pf = *(const uint32_t*)evb;
-	r.src = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // 4-byte aligned, beside pid and flags
-	r.len = d.len[i];
-	r.off = d.off[i];
+	r.len = d.len[j];
+	r.off = d.off[j];
 	return r;
 }
 
 __device__ __forceinline__ LaneEv lane_ev(const Dev& d, const LaneRaw& r) {
 	LaneEv e;
 	e.idx = r.idx;
-	if (r.flags & 0x100u) {
-		e.kind = EK_NONE;
+	if (r.past) {
+		e.m = EK_NONE;
 		e.L = 0;
-		e.pf = e.flags = 0;
-		e.j0 = e.lastp = 0;
-		e.p = d.payload;
+		e.pf = 0;
 		e.base = (unsigned long long)(uintptr_t)d.payload;
-		e.src = v4u{0u, 0u, 0u, 0u};
 		return e;
 	}
 	const uint32_t flags = r.flags;
 	e.pf = r.pf;
-	e.src = r.src;
-	e.flags = flags;
 	const uint32_t L = r.len;
 	const uint64_t off = r.off;
-	e.kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : !buf_in(d, L, off) ? EK_BAD : EK_PARSE;
-	e.L = e.kind == EK_PARSE ? L : 0;
-	e.p = e.kind == EK_PARSE ? d.payload + off : d.payload;
+	const uint32_t kind = !(flags & FLAG_NEW) || L == EBD_NO_BUFFER ? EK_SKIP : !buf_in(d, L, off) ? EK_BAD : EK_PARSE;
+	e.L = kind == EK_PARSE ? L : 0;
+	const uint8_t* p = kind == EK_PARSE ? d.payload + off : d.payload;
 	// the 64-byte grid when the buffer is 16-byte aligned and its line half stays inside the
 	// readable allocation (from the 16-byte boundary at or below payload, ebpf_discovery_amd.h)
-	const unsigned long long a = (unsigned long long)(uintptr_t)e.p, a64 = a & ~63ull;
+	const unsigned long long a = (unsigned long long)(uintptr_t)p, a64 = a & ~63ull;
 	const bool grid = (a & 15u) == 0 && a64 >= ((unsigned long long)(uintptr_t)d.payload & ~15ull);
-	e.j0 = grid ? (uint32_t)((a & 63u) >> 4) : 0u;
+	const uint32_t j0 = grid ? (uint32_t)((a & 63u) >> 4) : 0u;
 	e.base = grid ? a64 : a;
-	e.lastp = e.L ? (16u * e.j0 + e.L - 1u) >> 4 : 0u;
+	e.m = kind | (j0 << 2) | (flags << 8);
 	return e;
 }
 
@@ -642,12 +633,11 @@ enum : uint32_t {
 	R_C4,   // term.c
 	R_QS,   // qs[0..4] (url, host, hend, cip, term)
 	R_LIM = R_QS + 5, // staged leading bytes that are valid
-	R_SRC,  // the source address (4 words): finalize classifies it (Aggregator.cpp:60-66, 85-88)
-	R_POS = R_SRC + 4, // ring position + 1 (checked by finalize)
+	R_POS,  // ring position + 1 (checked by finalize)
 	R_TW,   // the 4 bytes the terminal tracker's rescan needs, from the scan lane's registers
 	R_WORDS
 };
-static_assert(R_WORDS == 21, "finalize record is 21 words");
+static_assert(R_WORDS == 17, "finalize record is 17 words");
 
 // Leading buffer bytes a scan lane stages (window 0), carried to finalize in LDS so that it
 // reads the request line and usually the Host header from LDS instead of reloading lines
@@ -718,6 +708,9 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
 		return false;
 	}
+	// the session's source address (Aggregator.cpp:60-66, 85-88), loaded first so that its latency
+	// overlaps the rescans: it classifies the client when the request has no client-IP header
+	const v4u sv = *(const __attribute__((address_space(1))) v4u*)((const uint8_t*)(d.ev + i) + 16);
 	ScanRec sr;
 	sr.url = Trk{q[R_C01] & 0xffffu, q[R_QS + 0]};
 	sr.host = Trk{q[R_C01] >> 16, q[R_QS + 1]};
@@ -736,7 +729,7 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 		d.keys[i] = fr.key;
 		if (!fr.cip) { // the client is the session's source address; a client-IP token is k_agg_fast's
 			uint8_t src[16];
-			__builtin_memcpy(src, &q[R_SRC], 16);
+			__builtin_memcpy(src, &sv, 16);
 			fr.r.info = (uint8_t)(fr.r.info | (classify_source(*d.ifs, (uint8_t)(q[R_SF] >> 8), src) << EBD_INFO_CLASS_SHIFT));
 		}
 	}
@@ -863,7 +856,11 @@ void k_fresh(Dev d) {
 	const uint32_t sl = wave * 64 + lane; // scan lane
 	uint32_t* stg = sh.stage + sl;        // this lane's staging row (word j at stg[j * kScanLanes])
 	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
-	// the lane's current event (e0) and the next one (e1, whose record arrives early)
+	// The lane's current event (e0), the next one (e1, decoded: its first window is loaded while
+	// e0's last one is scanned) and the one after (n2, its words as loaded).  n2 is decoded only
+	// at the next hand-off, an event later, so a hand-off never waits for the loads it issues:
+	// waiting for them (and, the counter being in order, for the window issued before them)
+	// had cost the scan waves 23 % of their time (clock stamps).
 	LaneEv e0 = lane_ev(d, lane_load(d, rb + sl, re));
 	LaneEv e1 = lane_ev(d, lane_load(d, rb + kScanLanes + sl, re));
 	uint32_t w0 = 0; // e0's window to scan next
@@ -887,15 +884,15 @@ void k_fresh(Dev d) {
 				while (lds_load_acq(&sh.freed[slot]) != pos - kRing + 1)
 					__builtin_amdgcn_s_sleep(1);
 			// staged bytes equal the buffer's up to the loaded windows and the last chunk's end
-			const uint32_t scanned = min(64u * w0 - 16u * e0.j0, kStage), chunks_end = (e0.L + 15u) & ~15u;
+			const uint32_t scanned = min(64u * w0 - 16u * e0.j0(), kStage), chunks_end = (e0.L + 15u) & ~15u;
 			const uint32_t post = (stg[0] & 0xffu) == 'P' ? 1u : 0u; // the method's first byte
-			const unsigned long long a = (unsigned long long)(uintptr_t)e0.p;
+			const unsigned long long a = (unsigned long long)(uintptr_t)e0.p();
 			uint32_t t[R_WORDS];
 			t[R_PLO] = (uint32_t)a;
 			t[R_PHI] = ((uint32_t)(a >> 32) & 0xffffu) | (e0.L << 16);
 			t[R_IDX] = e0.idx;
 			t[R_PID] = e0.pf;
-			t[R_SF] = s | (e0.flags << 8) | (sr.cseen << 16) | (post << 17);
+			t[R_SF] = s | (e0.flags() << 8) | (sr.cseen << 16) | (post << 17);
 			t[R_CQM] = sr.cqm;
 			t[R_C01] = sr.url.c | (sr.host.c << 16);
 			t[R_C23] = sr.hend.c | (sr.cip.c << 16);
@@ -906,10 +903,6 @@ void k_fresh(Dev d) {
 			t[R_QS + 3] = sr.cip.qs;
 			t[R_QS + 4] = sr.term.qs;
 			t[R_LIM] = min(scanned, chunks_end);
-			t[R_SRC + 0] = e0.src.x;
-			t[R_SRC + 1] = e0.src.y;
-			t[R_SRC + 2] = e0.src.z;
-			t[R_SRC + 3] = e0.src.w;
 			t[R_POS] = pos + 1;
 			t[R_TW] = tw;
 #pragma unroll
@@ -924,12 +917,12 @@ void k_fresh(Dev d) {
 	// Moves on while e0 needs no scan: such events are resolved here.
 	auto resolve = [&]() {
 		for (;;) {
-			if (e0.kind == EK_SKIP) {
+			if (e0.kind() == EK_SKIP) {
 				write_none(d, e0.idx);
-			} else if (e0.kind == EK_BAD) {
+			} else if (e0.kind() == EK_BAD) {
 				set_error(d, EBD_ERR_BAD_INPUT);
 				write_none(d, e0.idx);
-			} else if (e0.kind == EK_PARSE && e0.L == 0) {
+			} else if (e0.kind() == EK_PARSE && e0.L == 0) {
 				write_empty(d, e0.idx);
 			} else {
 				break;
@@ -940,12 +933,12 @@ void k_fresh(Dev d) {
 		w0 = 0;
 		s = di.init;
 		rec_init(di, sr);
-		live = e0.kind == EK_PARSE ? 1u : 0u;
+		live = e0.kind() == EK_PARSE ? 1u : 0u;
 	};
 	resolve();
 
 	// The window in flight: (tidx, tw) names what W holds for this lane.
-	auto nwin = [](const LaneEv& e) { return e.L ? (e.lastp >> 2) + 1u : 0u; };
+	auto nwin = [](const LaneEv& e) { return e.L ? (e.lastp() >> 2) + 1u : 0u; };
 	Chunk W[4];
 	uint32_t tidx, tw;
 	auto issue = [&](unsigned long long a, uint32_t last, uint32_t w) {
@@ -965,22 +958,22 @@ void k_fresh(Dev d) {
 	};
 	tidx = e0.idx;
 	tw = 0;
-	issue(e0.base, e0.lastp, 0);
+	issue(e0.base, e0.lastp(), 0);
 
-	while (__any(e0.kind != EK_NONE)) {
+	while (__any(e0.kind() != EK_NONE)) {
 		// is the window in flight the one e0 needs?
-		const bool valid = e0.kind == EK_PARSE && tidx == e0.idx && tw == w0;
+		const bool valid = e0.kind() == EK_PARSE && tidx == e0.idx && tw == w0;
 		Chunk X[4] = {W[0], W[1], W[2], W[3]};
 		// predict and load the next window
 		{
 			unsigned long long na;
 			uint32_t nl, ni, nw;
 			if (!valid) {
-				na = e0.base, nl = e0.lastp, ni = e0.idx, nw = w0;
+				na = e0.base, nl = e0.lastp(), ni = e0.idx, nw = w0;
 			} else if (w0 + 1 < nwin(e0)) {
-				na = e0.base, nl = e0.lastp, ni = e0.idx, nw = w0 + 1;
+				na = e0.base, nl = e0.lastp(), ni = e0.idx, nw = w0 + 1;
 			} else {
-				na = e1.base, nl = e1.lastp, ni = e1.idx, nw = 0;
+				na = e1.base, nl = e1.lastp(), ni = e1.idx, nw = 0;
 			}
 			issue(na, nl, nw);
 			tidx = ni;
@@ -992,7 +985,7 @@ void k_fresh(Dev d) {
 			// slot k holds the buffer's chunk c = 4 w0 + k - j0 (slots before the buffer: c < 0)
 #pragma unroll
 			for (int k = 0; k < 4; k++) { // the buffer's first kStage bytes into the lane's staging row
-				const int c = (int)(4 * w0 + k) - (int)e0.j0;
+				const int c = (int)(4 * w0 + k) - (int)e0.j0();
 				if (c >= 0 && c < (int)(kStage / 16))
 #pragma unroll
 					for (int j = 0; j < 4; j++)
@@ -1002,7 +995,7 @@ void k_fresh(Dev d) {
 			for (int k = 0; k < 4; k++) {
 				uint32_t sx = s, m, qs, qm;
 				scan_chunk(T, X[k], sx, m, qs, qm);
-				const int ci = (int)(4 * w0 + k) - (int)e0.j0;
+				const int ci = (int)(4 * w0 + k) - (int)e0.j0();
 				if (live && ci >= 0) {
 					const uint32_t c = (uint32_t)ci;
 					chunk_update(di, sr, c, s, qs, qm, m);
@@ -1015,7 +1008,7 @@ void k_fresh(Dev d) {
 		}
 		uint32_t tw = 0;
 		if (done) { // the last chunk scanned is the terminal tracker's, in this window's registers
-			const uint32_t k = (sr.term.c + e0.j0) & 3u, qt = flip_quarter<RS_TERM>(di, sr.term, 0);
+			const uint32_t k = (sr.term.c + e0.j0()) & 3u, qt = flip_quarter<RS_TERM>(di, sr.term, 0);
 			uint32_t w4[4];
 #pragma unroll
 			for (int j = 0; j < 4; j++)
