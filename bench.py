@@ -67,6 +67,9 @@ def parse_args():
                     help="events per poll cycle (default: the whole batch; config 4: 81 M); a step submits them all")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget per thread count (rank 0, N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-config4", action="store_true",
+                    help="N = 1 default run: skip the config-4 measurement reported beside the headline")
+    ap.add_argument("--config4-steps", type=int, default=3, help="timed config-4 steps (N = 1 default run)")
     ap.add_argument("--mode", choices=("cold", "warm"), default="cold",
                     help="cold: every step is one report interval, the service table cleared before the batch "
                          "(every service of the batch is created inside the timed step); warm: the table keeps "
@@ -117,10 +120,10 @@ def copy_peak(dev):
     return gbps
 
 
-def cpu_baseline(config, seed, budget_s):
+def cpu_baseline(config, seed, budget_s, threads=True):
     """The oracle (C restatement of the reference path) on a bounded sample of the same
     workload regenerated on the host, 1 thread (the reference's single consumer thread,
-    ServiceDetectionTask.cpp:43) and all host threads (connection-sharded)."""
+    ServiceDetectionTask.cpp:43) and, with threads, all host threads (connection-sharded)."""
     import oracle_py as O
     import ebd
     o = O.Oracle()
@@ -149,7 +152,7 @@ def cpu_baseline(config, seed, budget_s):
                sample=f"first {done} events of the same config-{config} trace (seed {seed}) regenerated on the host, "
                       f"oracle/ C restatement (Discovery+HttpRequestParser+Aggregator semantics), 1 thread, "
                       f"{spent:.1f} s")
-    mt = O.parallel_throughput(gen, seed, budget_s)
+    mt = O.parallel_throughput(gen, seed, budget_s) if threads else None
     if mt:
         out["all_threads"] = mt
     return out
@@ -220,36 +223,21 @@ def generate_shard(ctx, cfg, seed, E, world, rank, dev):
     return ev_t, len_t, off_t, pay_t, gidx_t, n_tot, b_tot
 
 
-def main():
-    args = parse_args()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
-    if args.dry_run_cpu:
-        return dry_run_cpu(args)
+def run_config(args, cfg, E, steps, warmup, world, rank, dev, key, mode):
+    """One workload on this rank: generate its batch in HBM, `warmup` untimed steps, `steps`
+    timed steps (barrier + synchronize on both sides, max over ranks), the other step mode
+    beside, and one untimed step that tallies the algorithmic bytes.  Returns the measurement
+    (rank 0; other ranks return None at N > 1)."""
     import torch
     import ebd
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
-    cfg = args.config or (5 if world > 1 else 3)
+    local = dev.index
     seed = args.seed or cfg
-    E = args.events or DEFAULT_EVENTS[cfg]
-
-    # every rank keys services with the same secret (the merge matches keys across GPUs)
-    key = np.frombuffer(os.urandom(16), np.uint64).copy()
-    if world > 1:
-        kt_ = torch.tensor(key.view(np.int64), device=dev)
-        torch.distributed.broadcast(kt_, 0)
-        key = kt_.cpu().numpy().view(np.uint64)
     cap = int(E * 1.15) if cfg == 5 else E
     sub = args.sub_batch or SUB_BATCH.get(cfg, 0) or cap
     reqs = cap / 3.2 if cfg == 4 else cap  # requests, not events, create services
-    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(reqs, 1) * 0.8)))))
+    # the service table at half a slot per request: config 3's 30 M services of 100 M requests fill
+    # 2^26 slots to 45 %, and the cold clear streams 4.3 GB instead of the 8.6 GB of 2^27 slots
+    svc_cap = args.service_capacity or (1 << max(20, int(np.ceil(np.log2(max(reqs, 1) * 0.5)))))
     ctx = ebd.Context(max_events=min(cap, sub), device=local, service_capacity=svc_cap,
                       string_arena=max(256 << 20, int(reqs) * 48), timing=True, hash_key=(int(key[0]), int(key[1])))
     t0 = time.perf_counter()
@@ -288,7 +276,7 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        for k in range(k0, k0 + args.steps):
+        for k in range(k0, k0 + steps):
             step(k, cold, merge=world > 1 and cold)
         ctx.sync()
         torch.cuda.synchronize()
@@ -301,20 +289,20 @@ def main():
             el = float(tt.item())
         return el
 
-    cold = args.mode == "cold"
-    for k in range(args.warmup):
+    cold = mode == "cold"
+    for k in range(warmup):
         step(k, cold, merge=world > 1 and cold)
     ctx.sync()
     ctx.reset_kernel_times()
     merges.clear()
-    elapsed = timed_steps(args.warmup, cold)
+    elapsed = timed_steps(warmup, cold)
     kt = ctx.kernel_times()
     st = ctx.stats()
     step_merges = list(merges)
     # the other mode, reported beside (same batch, same number of steps)
     other_mode = "warm" if cold else "cold"
     ctx.reset_kernel_times()
-    k_other = args.warmup + args.steps
+    k_other = warmup + steps
     other_elapsed = timed_steps(k_other, not cold)
     other_kt = ctx.kernel_times()
 
@@ -331,12 +319,12 @@ def main():
         acc["data"] += int(((f & ebd.FLAG_NEW_DATA) != 0).sum())
         acc["close"] += int(((f & ebd.FLAG_NEW_DATA) == 0).sum())
 
-    step(k_other + args.steps, cold, each=tally)
+    step(k_other + steps, cold, each=tally)
     ctx.sync()
     alg_bytes = acc["consumed"] + 40 * acc["data"] + 36 * acc["close"]
     # the roofline's kernel: k_fresh (configs 1-3, 5), or for config 4 the kernel with the most
     # time per step (the session walk), timed over all its launches in one step
-    per_step = {k: v[1] / args.steps for k, v in kt.items() if v[0]}
+    per_step = {k: v[1] / steps for k, v in kt.items() if v[0]}
     top = max(per_step, key=per_step.get) if cfg == 4 else "k_fresh"
     fresh_launches, fresh_ms = kt[top]
     fresh_avg_ms = per_step[top] if cfg == 4 else fresh_ms / max(fresh_launches, 1)
@@ -385,12 +373,79 @@ def main():
                  "string_bytes_if_one_round": int(tot[6]), "record_size": shard.REC.itemsize,
                  "protocol": "two rounds: records, need flags back, endpoint bytes only for keys new to the owner"}
         if rank != 0:
-            torch.distributed.destroy_process_group()
-            return
+            return None
 
+    total_events = n_all * steps
+    res = {
+        "value": total_events / elapsed, "ms_per_step": elapsed / steps * 1e3, "n": n, "n_all": n_all, "size": size,
+        "poll_cycles": len(cuts) - 1, "seed": seed, "alg_bytes": alg_bytes, "elapsed": elapsed, "top": top,
+        "achieved": achieved, "kernel_avg_ms": fresh_avg_ms, "traffic": traffic, "merge": merge,
+        "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items() if v[0]},
+        "kernel_ms_per_step": per_step, "services": st["services"], "errors": st["error_names"],
+        "other_mode": other_mode,
+        "other": {"value": total_events / other_elapsed, "ms_per_step": other_elapsed / steps * 1e3,
+                  "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in other_kt.items() if v[0]}},
+    }
+    ctx.close()
+    del ev_t, len_t, off_t, pay_t, gidx_t
+    torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.dry_run_cpu:
+        return dry_run_cpu(args)
+    import torch
+    import ebd
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = args.config or (5 if world > 1 else 3)
+    E = args.events or DEFAULT_EVENTS[cfg]
+    # every rank keys services with the same secret (the merge matches keys across GPUs)
+    key = np.frombuffer(os.urandom(16), np.uint64).copy()
+    if world > 1:
+        kt_ = torch.tensor(key.view(np.int64), device=dev)
+        torch.distributed.broadcast(kt_, 0)
+        key = kt_.cpu().numpy().view(np.uint64)
+    m = run_config(args, cfg, E, args.steps, args.warmup, world, rank, dev, key, args.mode)
+    if m is None:  # a rank other than 0 at N > 1
+        torch.distributed.destroy_process_group()
+        return
+    n, n_all, size, elapsed, alg_bytes, top = m["n"], m["n_all"], m["size"], m["elapsed"], m["alg_bytes"], m["top"]
+    seed = m["seed"]
+    # config 4 (multi-buffer reassembly) beside the headline at one GPU: its own
+    # step time, the session walk's roofline and the 1-thread CPU baseline, driver-timed with the rest
+    c4 = None
+    if world == 1 and not args.config and not args.events and not args.no_config4:
+        t4 = time.perf_counter()
+        m4 = run_config(args, 4, DEFAULT_EVENTS[4], args.config4_steps, 1, 1, 0, dev, key, "cold")
+        c4 = {"workload": WORKLOADS[4], "config": 4, "events_per_step": m4["n"], "seed": m4["seed"],
+              "poll_cycles_per_step": m4["poll_cycles"], "steps": args.config4_steps, "warmup": 1, "mode": "cold",
+              "value": m4["value"], "unit": "events/s", "ms_per_step": m4["ms_per_step"],
+              "roofline": {"bound": "hbm", "kernel": m4["top"], "kernel_ms_per_step": m4["kernel_avg_ms"],
+                           "achieved": m4["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": m4["achieved"] / HBM_PEAK_GBS, "alg_bytes_per_step": m4["alg_bytes"],
+                           "step_frac": m4["alg_bytes"] / (m4["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS},
+              "kernel_ms_per_step": m4["kernel_ms_per_step"], "errors": m4["errors"],
+              "warm": m4["other"]}
+        if not args.no_cpu_baseline:
+            cb = cpu_baseline(4, 4, args.cpu_seconds / 2, threads=False)
+            c4["cpu_baseline"] = cb
+        c4["wall_s"] = time.perf_counter() - t4
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, seed, args.cpu_seconds)
+    traffic, merge = m["traffic"], m["merge"]
+    local = dev.index
     peak_copy = copy_peak(dev)
     # the measured read-stream peak: the faster of two read-only shapes
     rb = ebd.read_bandwidth(local, 4 << 30, 10)
@@ -398,7 +453,7 @@ def main():
     total_events = n_all * args.steps
     out = {
         "metric": "HTTP events parsed/s (device-resident)",
-        "value": total_events / elapsed,
+        "value": m["value"],
         "unit": "events/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -410,28 +465,28 @@ def main():
         "dtype": "u8",
         "data": "synthetic: Philox-seeded trace generated in HBM (bit-identical to the host generator)",
         "config": {"workload": WORKLOADS[cfg], "config": cfg, "events_per_gpu": n, "seed": seed,
-                   "payload_bytes_per_gpu": size, "step_mode": args.mode, "poll_cycles_per_step": len(cuts) - 1,
+                   "payload_bytes_per_gpu": size, "step_mode": args.mode, "poll_cycles_per_step": m["poll_cycles"],
                    "parallelism": (f"{world} shards by hash(pid, fd, sessionID), RCCL owner merge" if world > 1
                                    else "1 GPU")},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "measured_read_peak": read_peak, "frac_of_measured_read_peak": achieved / read_peak,
+        "roofline": {"bound": "hbm", "achieved": m["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": m["achieved"] / HBM_PEAK_GBS, "traffic": traffic,
+                     "measured_read_peak": read_peak, "frac_of_measured_read_peak": m["achieved"] / read_peak,
                      "measured_read_shapes_gbps": rb,
-                     "kernel": top, "kernel_avg_ms": fresh_avg_ms, "alg_bytes_per_launch": alg_bytes,
+                     "kernel": top, "kernel_avg_ms": m["kernel_avg_ms"], "alg_bytes_per_launch": alg_bytes,
                      "alg_bytes_def": "sum(consumed) + 40 B per data event (36-B DiscoveryEvent + 4-B length) + 36 B per "
                                       "close-only event" + (" (kernel time: all its launches in one step of %d poll "
-                                                             "cycles)" % (len(cuts) - 1) if cfg == 4 else "")},
+                                                             "cycles)" % m["poll_cycles"] if cfg == 4 else "")},
         "step_roofline_frac": alg_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
         "cpu_baseline": cpu,
         "step_gbps_alg": alg_bytes * world * args.steps / elapsed / 1e9,
-        "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in kt.items() if v[0]},
+        "kernel_ms": m["kernel_ms"],
         "measured_copy_gbps": peak_copy,
-        "services": st["services"],
-        "errors": st["error_names"],
+        "services": m["services"],
+        "errors": m["errors"],
         "merge": merge,
         "mode": args.mode,
-        other_mode: {"value": total_events / other_elapsed, "ms_per_step": other_elapsed / args.steps * 1e3,
-                     "kernel_ms": {k: (v[1] / v[0] if v[0] else 0.0) for k, v in other_kt.items() if v[0]}},
+        m["other_mode"]: m["other"],
+        "config4": c4,
         "build_id": ebd.build_id(),
     }
     print(json.dumps(out), flush=True)
