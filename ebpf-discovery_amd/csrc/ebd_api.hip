@@ -39,6 +39,7 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st);
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint32_t n, const uint8_t* data, hipStream_t st);
 hipError_t launch_publish(const Dev& d, hipStream_t st, int cus);
 uint32_t agg_stage_per_block(uint32_t n, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
@@ -2089,6 +2090,60 @@ int ebd_host_endpoint_key(const uint64_t hash_key[2], uint32_t pid, const uint8_
 	const Hash128 h = kh.finish();
 	key[0] = h.lo;
 	key[1] = h.hi;
+	return 0;
+}
+
+int ebd_parser_init(ebd_parser_state* st) {
+	if (!st)
+		return -EINVAL;
+	std::memset(st, 0, sizeof(*st));
+	GenParser g;
+	gp_init(g);
+	std::memcpy(st, &g, sizeof(g)); // no client-IP value, no tokens
+	return 0;
+}
+
+int ebd_parser_reset(ebd_parser_state* st) {
+	if (!st)
+		return -EINVAL;
+	GenParser g;
+	std::memcpy(&g, st, sizeof(g));
+	gp_reset(g); // keeps result.clientIPKey (P:374-379)
+	std::memset(st, 0, sizeof(*st));
+	std::memcpy(st, &g, sizeof(g));
+	return 0;
+}
+
+const char* ebd_client_ip_key_name(uint32_t id) {
+	static const char* names[6] = {"", "rproxy_remote_address", "true-client-ip", "x-client-ip", "x-forwarded-for", "x-http-client-ip"};
+	return id < 6 ? names[id] : "";
+}
+
+int ebd_parse_streams(ebd_ctx* c, ebd_parse_call* calls, uint32_t n, const uint8_t* data, uint64_t data_len) {
+	if (!c || (n && (!calls || (!data && data_len))))
+		return -EINVAL;
+	for (uint32_t k = 0; k < n; k++) { // every stream inside data, every state from this ABI
+		const ebd_parse_call& q = calls[k];
+		GenParser g;
+		std::memcpy(&g, &q.state, sizeof(g));
+		if (q.data_off > data_len || q.data_len > data_len - q.data_off || g.length > q.data_len || g.state > ST_INVALID)
+			return -EINVAL;
+	}
+	if (n == 0)
+		return 0;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	AsyncBuf calls_b{c->stream}, data_b{c->stream};
+	HIP_TRY(hipMallocAsync(&calls_b.p, (size_t)n * sizeof(ebd_parse_call), c->stream));
+	HIP_TRY(hipMallocAsync(&data_b.p, (size_t)data_len + 16, c->stream));
+	HIP_TRY(hipMemcpyAsync(calls_b.p, calls, (size_t)n * sizeof(ebd_parse_call), hipMemcpyHostToDevice, c->stream));
+	if (data_len)
+		HIP_TRY(hipMemcpyAsync(data_b.p, data, (size_t)data_len, hipMemcpyHostToDevice, c->stream));
+	HIP_TRY(launch_parse_streams(c->d_trie, (ebd_parse_call*)calls_b.p, n, (const uint8_t*)data_b.p, c->stream));
+	HIP_TRY(hipMemcpyAsync(calls, calls_b.p, (size_t)n * sizeof(ebd_parse_call), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(calls_b.release());
+	HIP_TRY(data_b.release());
+	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
 

@@ -3364,6 +3364,113 @@ __global__ void k_agg_requests(Dev d, const ebd_request* rq, uint32_t n, const u
 }
 
 // ---------------------------------------------------------------------------------
+// httpparser::HttpRequestParser one stream at a time (ebd_parse_streams): the generic state
+// machine gp_step (HttpRequestParser.cpp:124-364) over the bytes of one chunk per call, plus
+// what HttpRequest holds beyond the aggregator's needs: every value of a header whose key is
+// result.clientIPKey, split into result.clientIp's tokens at its newline (P:248-262, 381-409).
+// ---------------------------------------------------------------------------------
+struct StreamParser {
+	GenParser g;
+	uint32_t vstart, vend; // the current client-IP header value (stream positions)
+	uint32_t ntok, dropped;
+	uint32_t tok[EBD_PARSE_MAX_TOKENS][2];
+};
+static_assert(sizeof(StreamParser) <= sizeof(ebd_parser_state), "stream parser fits ebd_parser_state");
+
+// parseClientIPValue (P:392-409): boost::split(token_compress_on) on ',' then each token's trim
+// and IPv4 port / IPv6 bracket handling (front_token); tokens appended in order.
+__device__ void stream_split_value(StreamParser& sp, const uint8_t* s, uint32_t a, uint32_t e) {
+	uint32_t b = a;
+	for (;;) {
+		uint32_t t = b;
+		while (t < e && s[t] != ',')
+			t++;
+		uint32_t tb, te;
+		front_token(s + b, t - b, &tb, &te);
+		if (sp.ntok < EBD_PARSE_MAX_TOKENS) {
+			sp.tok[sp.ntok][0] = b + tb;
+			sp.tok[sp.ntok][1] = b + te;
+			sp.ntok++;
+		} else {
+			sp.dropped = 1;
+		}
+		if (t >= e)
+			break;
+		b = t;
+		while (b < e && s[b] == ',') // adjacent separators are one (token_compress_on)
+			b++;
+		if (b >= e) { // a trailing separator leaves an empty last token
+			if (sp.ntok < EBD_PARSE_MAX_TOKENS) {
+				sp.tok[sp.ntok][0] = sp.tok[sp.ntok][1] = e;
+				sp.ntok++;
+			} else {
+				sp.dropped = 1;
+			}
+			break;
+		}
+	}
+}
+
+__global__ void k_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint32_t n, const uint8_t* data) {
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		ebd_parse_call& c = calls[k];
+		StreamParser sp;
+		__builtin_memcpy(&sp, &c.state, sizeof(sp));
+		GenParser& g = sp.g;
+		const uint8_t* s = data + c.data_off; // stream position p is s[p]
+		const uint32_t end = c.data_len;
+		uint32_t i = g.length; // the chunk: the stream from the parser's position
+		const uint32_t i0 = i;
+		while (i < end) { // P:85-106
+			if (g.length > kMaxRequestLength) {
+				g.state = ST_INVALID;
+				break;
+			}
+			const uint32_t ch = s[i], st0 = g.state, kt = gp_key_type(trie, g.key);
+			gp_step(g, trie, ch, g.length);
+			if (st0 == ST_SP_VAL && g.state == ST_HDR_VAL && kt >= KT_CLIENT0) // the value's first byte (P:311-316)
+				sp.vstart = sp.vend = g.length;
+			if (st0 == ST_HDR_VAL && g.state == ST_HDR_NL && kt >= KT_CLIENT0) // its CR ends it
+				sp.vend = g.length;
+			if (st0 == ST_HDR_NL && g.state == ST_HDR_KEY && kt >= KT_CLIENT0 && key_client_id((uint8_t)kt) == g.cipkey)
+				stream_split_value(sp, s, sp.vstart, sp.vend); // P:254-257
+			i++;
+			g.length++;
+			if (gp_done(g)) {
+				if (c.flags & 16) // DISCOVERY_FLAG_SESSION_SSL_HTTP (P:97-99)
+					g.f |= GPF_HTTPS;
+				else
+					g.f &= (uint8_t)~GPF_HTTPS;
+				break;
+			}
+		}
+		c.consumed = i - i0;
+		c.status = g.state == ST_FINISHED ? EBD_PARSER_FINISHED : g.state == ST_INVALID ? EBD_PARSER_INVALID : EBD_PARSER_UNFINISHED;
+		c.is_https = (g.f & GPF_HTTPS) ? 1 : 0;
+		c.client_ip_key = g.cipkey;
+		c.tokens_dropped = (uint8_t)sp.dropped;
+		c.method_len = g.mlen;
+		c.url_off = g.url_start;
+		c.url_len = g.url_len;
+		c.protocol_off = g.url_start + g.url_len + 1; // 'H' follows the URL's space (P:215-224)
+		c.protocol_len = g.plen;
+		c.host_off = g.host_start;
+		c.host_len = g.host_len;
+		c.ntokens = sp.ntok;
+		for (uint32_t t = 0; t < sp.ntok; t++) {
+			c.tokens[t][0] = sp.tok[t][0];
+			c.tokens[t][1] = sp.tok[t][1];
+		}
+		__builtin_memcpy(&c.state, &sp, sizeof(sp));
+	}
+}
+
+hipError_t launch_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint32_t n, const uint8_t* data, hipStream_t st) {
+	hipLaunchKernelGGL(k_parse_streams, dim3((n + 63) / 64), dim3(64), 0, st, trie, calls, n, data);
+	return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // Synthetic trace generation in HBM (ebd_gen.h).
 // ---------------------------------------------------------------------------------
 // Pass 1: aligned length of every candidate event (0: another shard's), and whether it is kept.

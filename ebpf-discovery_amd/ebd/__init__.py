@@ -168,6 +168,10 @@ _SIGS = {
                                     C.c_uint32]),
     "ebd_host_pton": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p]),
     "ebd_testing_set_lru_window": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "ebd_parser_init": (C.c_int, [C.c_void_p]),
+    "ebd_parser_reset": (C.c_int, [C.c_void_p]),
+    "ebd_parse_streams": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "ebd_client_ip_key_name": (C.c_char_p, [C.c_uint32]),
     "ebd_host_endpoint_key": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
 }
 
@@ -581,6 +585,69 @@ class Context:
         d = {k: getattr(s, k) for k, _ in Stats._fields_}
         d["error_names"] = [v for b, v in ERR_BITS.items() if d["errors"] & b]
         return d
+
+
+PARSE_MAX_TOKENS = 32
+PARSE_CALL_DTYPE = np.dtype([("state", np.uint8, 320), ("data_off", np.uint64), ("data_len", np.uint32), ("flags", np.uint8),
+                             ("pad_", np.uint8, 3), ("consumed", np.uint32), ("status", np.uint8), ("is_https", np.uint8),
+                             ("client_ip_key", np.uint8), ("tokens_dropped", np.uint8), ("method_len", np.uint32),
+                             ("url_off", np.uint32), ("url_len", np.uint32), ("protocol_off", np.uint32),
+                             ("protocol_len", np.uint32), ("host_off", np.uint32), ("host_len", np.uint32),
+                             ("ntokens", np.uint32), ("tokens", np.uint32, (PARSE_MAX_TOKENS, 2))])
+assert PARSE_CALL_DTYPE.itemsize == 632
+PARSER_UNFINISHED, PARSER_FINISHED, PARSER_INVALID = 0, 1, 2
+
+
+class StreamParser:
+    """httpparser::HttpRequestParser (HttpRequestParser.h:41-101) over ebd_parse_streams: one GPU
+    call per parse(); the request's bytes since reset() are kept here and `result` is
+    materialised from the stream positions the GPU returns (the C++ facade's
+    ebdamd::HttpRequestParser does the same)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self.call = np.zeros(1, PARSE_CALL_DTYPE)
+        _check(lib().ebd_parser_init(_p(self.call["state"][0])), "ebd_parser_init")
+        self.stream = b""
+        self.status = PARSER_UNFINISHED
+        self.result = self._result()
+
+    def parse(self, data: bytes, flags: int) -> int:
+        base = len(self.stream)
+        buf = np.frombuffer(self.stream + data or b"\0", np.uint8)
+        self.call["data_off"], self.call["data_len"], self.call["flags"] = 0, len(self.stream) + len(data), flags
+        _check(lib().ebd_parse_streams(self.ctx.h, _p(self.call), 1, _p(buf), len(self.stream) + len(data)), "ebd_parse_streams")
+        c = self.call[0]
+        self.stream = (self.stream + data)[:base + int(c["consumed"])]
+        self.status = int(c["status"])
+        self.result = self._result()
+        return int(c["consumed"])
+
+    def reset(self):
+        _check(lib().ebd_parser_reset(_p(self.call["state"][0])), "ebd_parser_reset")
+        self.stream = b""
+        self.status = PARSER_UNFINISHED
+        self.result = self._result(cleared=True)
+
+    def is_finished(self):
+        return self.status != PARSER_UNFINISHED
+
+    def is_invalid(self):
+        return self.status == PARSER_INVALID
+
+    def _result(self, cleared=False):
+        c = self.call[0]
+        s = self.stream
+        key = lib().ebd_client_ip_key_name(int(c["client_ip_key"])).decode()
+        if cleared or not s and int(c["consumed"]) == 0:
+            return {"method": b"", "url": b"", "protocol": b"", "host": b"", "client_ip": [], "client_ip_key": key,
+                    "is_https": False}
+        sp = lambda o, n: s[int(o):int(o) + int(n)]  # noqa: E731
+        return {"method": sp(0, c["method_len"]), "url": sp(c["url_off"], c["url_len"]),
+                "protocol": sp(c["protocol_off"], c["protocol_len"]) if c["protocol_len"] else b"",
+                "host": sp(c["host_off"], c["host_len"]),
+                "client_ip": [s[int(a):int(b)] for a, b in c["tokens"][:int(c["ntokens"])]],
+                "client_ip_key": key, "is_https": bool(c["is_https"]), "tokens_dropped": bool(c["tokens_dropped"])}
 
 
 def format_services_json(records, strings: bytes):

@@ -422,6 +422,52 @@ typedef struct ebd_request {
  * until done.  Lengths over EBD_MAX_HTTP_REQUEST_LENGTH, or strings past strings_len: -EINVAL. */
 int ebd_aggregate_requests(ebd_ctx* ctx, const ebd_request* reqs, uint32_t n, const char* strings, uint64_t strings_len);
 
+/* --- one request stream at a time (httpparser::HttpRequestParser, HttpRequestParser.h:41-101) ---
+ * For callers that drive a parser object per connection, as the reference's tests and
+ * handleExistingSession do: parse(std::string_view, flags), isFinished, isInvalidState, reset,
+ * result.  The parser state is caller-owned plain data (ebd_parser_state: the generic state
+ * machine plus the result's client-IP tokens); ebd_parse_streams runs n such parsers, one chunk
+ * each, on the GPU (HttpRequestParser.cpp:85-106 and the handlers :162-409, exactly; the 8192-B
+ * cap included).  A call sees the request stream since the parser's last reset, data[data_off,
+ * data_off + data_len), and parses the bytes from the parser's position onwards: the chunk the
+ * caller appended.  Every span it returns is a position in that stream. */
+#define EBD_PARSE_MAX_TOKENS 32
+typedef struct ebd_parser_state {
+	uint64_t opaque_[40]; /* 320 bytes */
+} ebd_parser_state;
+enum {
+	EBD_PARSER_UNFINISHED = 0, /* waiting for more bytes */
+	EBD_PARSER_FINISHED = 1,   /* isFinished() && !isInvalidState() */
+	EBD_PARSER_INVALID = 2,    /* isInvalidState() (isFinished() too) */
+};
+typedef struct ebd_parse_call {
+	ebd_parser_state state; /* in: the parser (ebd_parser_init / ebd_parser_reset / a previous call); out: after */
+	uint64_t data_off;      /* the stream since reset: data[data_off, data_off + data_len) */
+	uint32_t data_len;
+	uint8_t flags;          /* DiscoveryFlags of the chunk: EBD_FLAG_SESSION_SSL_HTTP sets isHttps when it ends */
+	uint8_t pad_[3];
+	/* out: HttpRequestParser::parse's return value and HttpRequest (HttpRequestParser.h:28-39) */
+	uint32_t consumed;
+	uint8_t status;         /* EBD_PARSER_* */
+	uint8_t is_https;       /* result.isHttps (set when the parse ended) */
+	uint8_t client_ip_key;  /* result.clientIPKey: 0 none, 1..5 = ebd_client_ip_key_name(id) (sticky across reset) */
+	uint8_t tokens_dropped; /* result.clientIp had more than EBD_PARSE_MAX_TOKENS entries (the rest are not listed) */
+	uint32_t method_len;    /* result.method = stream[0, method_len) */
+	uint32_t url_off, url_len;
+	uint32_t protocol_off, protocol_len;
+	uint32_t host_off, host_len;
+	uint32_t ntokens;       /* result.clientIp[k] = stream[tokens[k][0], tokens[k][1]) */
+	uint32_t tokens[EBD_PARSE_MAX_TOKENS][2];
+} ebd_parse_call;
+/* HttpRequestParser() and reset() (HttpRequestParser.cpp:82-83, 374-379: reset keeps
+ * result.clientIPKey).  Host-only: they write the state, nothing runs on the GPU. */
+int ebd_parser_init(ebd_parser_state* st);
+int ebd_parser_reset(ebd_parser_state* st);
+/* n parsers, one chunk each (host arrays; data is the calls' streams).  Blocks until done. */
+int ebd_parse_streams(ebd_ctx* ctx, ebd_parse_call* calls, uint32_t n, const uint8_t* data, uint64_t data_len);
+/* HEADER_CLIENT_IP_KEYS[id - 1] (HttpRequestParser.cpp:43) for a client_ip_key id, "" for 0. */
+const char* ebd_client_ip_key_name(uint32_t id);
+
 int ebd_get_stats(ebd_ctx* ctx, ebd_stats* out);
 const char* ebd_strerror(int err);
 /* The measured HBM read-stream peak of `device` over a `bytes` buffer (>= 16 MiB), `reps` timed

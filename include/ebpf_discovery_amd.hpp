@@ -10,6 +10,9 @@
  *                         DiscoverySessionMeta) takes requests parsed elsewhere, queued and handed
  *                         to the GPU in batches (ebd_aggregate_requests)
  *   ebdamd::HttpRequest ~ httpparser::HttpRequest  (HttpRequestParser.h:28-39)
+ *   ebdamd::HttpRequestParser ~ httpparser::HttpRequestParser (HttpRequestParser.h:41-101): parse,
+ *                         isFinished, isInvalidState, reset, result; each parse() is one GPU call
+ *                         (ebd_parse_streams) on the parser's own state
  *   ebdamd::DiscoverySessionMeta ~ DiscoverySessionMeta (Aggregator.h:40-44)
  *   ebdamd::Service     ~ service::Service         (Service.h:43-66; the network maps as their sizes,
  *                         which is all the report prints, Service.h:84-98)
@@ -34,6 +37,7 @@
 #include <iostream>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
@@ -100,6 +104,93 @@ struct HttpRequest {
 		clientIp.clear();
 		isHttps = false;
 	}
+};
+
+/* httpparser::HttpRequestParser (HttpRequestParser.h:41-101) over ebd_parse_streams: the state
+ * machine runs on the GPU one chunk per parse() call (speed is not the point here: the batch
+ * entry points are); the facade keeps the request's bytes since reset() and materialises
+ * `result` from the positions the GPU returns, as the reference returns std::string copies.
+ * A parser without a context uses one process-wide context on device 0, created on first use
+ * and kept until exit (destroying it from a static destructor could outlive the HIP runtime). */
+class HttpRequestParser {
+public:
+	explicit HttpRequestParser(ebd_ctx* ctx = nullptr) : ctx_(ctx ? ctx : sharedContext()) {
+		check(ebd_parser_init(&state_), "ebd_parser_init");
+	}
+
+	/* HttpRequestParser::parse (HttpRequestParser.cpp:85-106): the bytes of `data` this call
+	 * consumed; the rest of a chunk after the request's end is not parsed (no pipelining). */
+	size_t parse(std::string_view data, uint8_t discoveryFlags) {
+		const size_t base = stream_.size();
+		stream_.append(data.data(), data.size());
+		ebd_parse_call call{};
+		call.state = state_;
+		call.data_off = 0;
+		call.data_len = (uint32_t)stream_.size();
+		call.flags = discoveryFlags;
+		const int rc = ebd_parse_streams(ctx_, &call, 1, reinterpret_cast<const uint8_t*>(stream_.data()), stream_.size());
+		if (rc != 0) {
+			stream_.resize(base);
+			throw Error("ebd_parse_streams", rc);
+		}
+		state_ = call.state;
+		status_ = call.status;
+		stream_.resize(base + call.consumed);
+		fill(call);
+		return call.consumed;
+	}
+
+	/* HttpRequestParser.cpp:108-114 */
+	bool isInvalidState() const { return status_ == EBD_PARSER_INVALID; }
+	bool isFinished() const { return status_ != EBD_PARSER_UNFINISHED; }
+
+	/* HttpRequestParser.cpp:374-379: result.clientIPKey survives */
+	void reset() {
+		check(ebd_parser_reset(&state_), "ebd_parser_reset");
+		status_ = EBD_PARSER_UNFINISHED;
+		stream_.clear();
+		result.clear();
+	}
+
+	HttpRequest result;
+
+private:
+	static ebd_ctx* sharedContext() {
+		static ebd_ctx* ctx = [] {
+			ebd_config cfg{};
+			cfg.max_events = 1;
+			cfg.service_capacity = 1024;
+			cfg.string_arena = 1 << 20;
+			cfg.lru_capacity = 1;
+			ebd_ctx* c = nullptr;
+			check(ebd_ctx_create(&cfg, &c), "ebd_ctx_create");
+			return c;
+		}();
+		return ctx;
+	}
+
+	std::string span(uint32_t off, uint32_t len) const {
+		if (off > stream_.size())
+			return std::string();
+		return stream_.substr(off, std::min<size_t>(len, stream_.size() - off));
+	}
+
+	void fill(const ebd_parse_call& c) {
+		result.method = span(0, c.method_len);
+		result.url = span(c.url_off, c.url_len);
+		result.protocol = c.protocol_len ? span(c.protocol_off, c.protocol_len) : std::string();
+		result.host = span(c.host_off, c.host_len);
+		result.clientIPKey = ebd_client_ip_key_name(c.client_ip_key);
+		result.clientIp.clear();
+		for (uint32_t k = 0; k < c.ntokens && k < EBD_PARSE_MAX_TOKENS; k++)
+			result.clientIp.push_back(span(c.tokens[k][0], c.tokens[k][1] - c.tokens[k][0]));
+		result.isHttps = c.is_https != 0;
+	}
+
+	ebd_ctx* ctx_;
+	ebd_parser_state state_{};
+	uint8_t status_ = EBD_PARSER_UNFINISHED;
+	std::string stream_; // the request's bytes since reset (what the parser consumed)
 };
 
 /* DiscoverySessionMeta (Aggregator.h:40-44): the session a request came in on. */

@@ -9,7 +9,10 @@
 //                     report and clear of outputServicesToStdout (Discovery.cpp:60-71) and the
 //                     network counters with an overridden getCurrentTime (AggregatorTest.cpp:41-46);
 //                     AggregatorTest's two scenarios (AggregatorTest.cpp:69-172, 174-285) rebuilt on
-//                     Aggregator::newRequest(HttpRequest, DiscoverySessionMeta), the batching adapter
+//                     Aggregator::newRequest(HttpRequest, DiscoverySessionMeta), the batching adapter;
+//                     HttpRequestParserTest.cpp's TestValidRequest / testInvalidRequest cases
+//                     (:152-191 over :193-300) on ebdamd::HttpRequestParser, and reset()'s sticky
+//                     clientIPKey (HttpRequestParser.cpp:374-379)
 // Prints "ok" and exits 0 when every check passes.
 #include "ebpf_discovery_amd.hpp"
 
@@ -242,7 +245,96 @@ void aggregator_test_scenarios() {
 	}
 }
 
+// HttpRequestParserTest.cpp:152-191: chunks in order, the bytes parse() consumed in all, then
+// isFinished / isInvalidState and the HttpRequest fields.
+std::vector<std::string> chunk_string(const std::string& s, size_t n) { // the test's chunkString
+	std::vector<std::string> out;
+	for (size_t k = 0; k < s.size(); k += n)
+		out.push_back(s.substr(k, n));
+	return out;
+}
+
+struct ValidCase {
+	std::vector<std::string> chunks;
+	std::string method, url, protocol, host;
+	std::vector<std::string> clientIp;
+	bool isHttps = false, finished = true;
+	size_t total = 0; // 0: every byte
+};
+
+void parser_test_cases() {
+	const std::string post3 = "POST /example/ HTTP/1.1\r\nHost: example.com\r\nUser-Agent: curl/7.81.0\r\nAccept: */*\r\n"
+	                          "X-Forwarded-For: 192.168.0.1:8080, 10.0.0.1, [2001:0db8:85a3::8a2e:0370:7334]\r\n\r\n"
+	                          "{\"name\":\"example\"}\r\n";
+	const std::vector<ValidCase> valid = {
+			{{"GET /example HTTP/1.1\r\nHost: example.com\r\n\r\n"}, "GET", "/example", "HTTP/1.1", "example.com", {}},
+			{{"POST /example HTTP/1.0\r\nHOST: example.com\r\n\r\n"}, "POST", "/example", "HTTP/1.0", "example.com", {}},
+			{{"GET /example HTTP/1.1\r\nHost: example.com\r\n\r"}, "GET", "/example", "HTTP/1.1", "example.com", {}, false, false},
+			{{"GET /Hello%20World/index.html HTTP/1.1\r\nHost:  example.com\r\nx-forwarded-for:  127.0.0.1\r\n\r\n"}, "GET",
+					"/Hello%20World/index.html", "HTTP/1.1", "example.com", {"127.0.0.1"}},
+			{{"GET / HTTP/1.1\r\n\r\n"}, "GET", "/", "HTTP/1.1", "", {}},
+			{chunk_string("GET /example HTTP/1.1\r\nHost: example.com\r\nX-Forwarded-For: 0.0.0.0\r\n\r\n", 1), "GET", "/example",
+					"HTTP/1.1", "example.com", {"0.0.0.0"}},
+			{{post3}, "POST", "/example/", "HTTP/1.1", "example.com", {"192.168.0.1", "10.0.0.1", "2001:0db8:85a3::8a2e:0370:7334"},
+					true, true, 163},
+			{chunk_string("GET /example/ HTTP/1.1\r\nHost: example.com\r\nX-Forwarded-For: 10.0.0.1\r\nUser-Agent: curl/7.81.0\r\n"
+			              "Accept: */*\r\nx-forwarded-for: 127.0.0.1,[2001:0db8:85a3::8a2e:0370:7335]:1234\r\n\r\n",
+					 2),
+					"GET", "/example/", "HTTP/1.1", "example.com", {"10.0.0.1", "127.0.0.1", "2001:0db8:85a3::8a2e:0370:7335"}},
+			{chunk_string("GET / HTTP/1.1\r\n", 1), "GET", "/", "HTTP/1.1", "", {}, false, false},
+			{{"GET /"}, "GET", "/", "", "", {}, false, false},
+			{{"", ""}, "", "", "", "", {}, false, false},
+	};
+	for (const ValidCase& c : valid) {
+		ebdamd::HttpRequestParser parser;
+		size_t total = 0, all = 0;
+		for (const std::string& ch : c.chunks) {
+			total += parser.parse(ch, c.isHttps ? EBD_FLAG_SESSION_SSL_HTTP : EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
+			all += ch.size();
+		}
+		CHECK(parser.isFinished() == c.finished);
+		CHECK(!parser.isInvalidState());
+		CHECK(total == (c.total ? c.total : all));
+		CHECK(parser.result.method == c.method);
+		CHECK(parser.result.url == c.url);
+		CHECK(parser.result.protocol == c.protocol);
+		CHECK(parser.result.host == c.host);
+		CHECK(parser.result.clientIp == c.clientIp);
+		CHECK(parser.result.isHttps == c.isHttps);
+	}
+	const std::vector<std::pair<std::vector<std::string>, size_t>> invalid = {
+			{{"get /example HTTP/1.1\r\nHost: example.com\r\n\r\n"}, 1},
+			{{"POST  HTTP/1.1\r\nHost: example.com\r\n\r\n"}, 6},
+			{{"GET / HTTP/1.1\r\nHost: \r\n\r\n"}, 23},
+			{{"GET / HTTP/1.1 \r\nHost: example.com\r\n\r\n"}, 15},
+			{{"GET / HTTP/1.1\nHost: example.con\n\n"}, 15},
+			{{"GET /example", "HTTP/1.1\r\nHost: example.com\r\n\r\n"}, 21},
+			{{"GET / HTTP/0.0\r\nHost: example.com\r\n\r\n"}, 12},
+			{{"GET http://example.com HTTP/1.1\r\nHost: example.com\r\n\r\n"}, 5},
+	};
+	for (const auto& c : invalid) {
+		ebdamd::HttpRequestParser parser;
+		size_t total = 0;
+		for (const std::string& ch : c.first)
+			total += parser.parse(ch, EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
+		CHECK(parser.isFinished());
+		CHECK(parser.isInvalidState());
+		CHECK(total == c.second);
+	}
+	// reset() keeps result.clientIPKey (HttpRequestParser.cpp:374-379)
+	ebdamd::HttpRequestParser parser;
+	parser.parse("GET / HTTP/1.1\r\nX-Forwarded-For: 1.2.3.4\r\n\r\n", EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
+	CHECK(parser.result.clientIPKey == "x-forwarded-for");
+	parser.reset();
+	CHECK(parser.result.url.empty() && parser.result.clientIp.empty() && !parser.isFinished());
+	parser.parse("GET /b HTTP/1.1\r\nX-Client-IP: 5.6.7.8\r\nX-Forwarded-For: 9.9.9.9\r\n\r\n", EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
+	CHECK(parser.isFinished() && !parser.isInvalidState());
+	CHECK(parser.result.clientIp == std::vector<std::string>{"9.9.9.9"});
+	CHECK(parser.result.clientIPKey == "x-forwarded-for");
+}
+
 int run_gpu() {
+	parser_test_cases();
 	// config 1: 1000 x the 35-byte GET, one connection per event
 	{
 		MemorySource src;

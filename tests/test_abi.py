@@ -51,3 +51,20 @@ def test_ctx_create_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(ebd.EbdError):
         ebd.Context(max_events=16)
+
+
+def test_parser_state_init_and_reset_keep_the_client_ip_key():
+    """ebd_parser_init / ebd_parser_reset are host-only (HttpRequestParser.cpp:82-83, 374-379):
+    reset returns the state machine to METHOD with nothing parsed, and keeps clientIPKey."""
+    import numpy as np
+    import ebd
+    st = np.zeros(320, np.uint8)
+    assert ebd.lib().ebd_parser_init(ebd._p(st)) == 0
+    assert st[6] == 0 and st[12:16].view(np.uint32)[0] == 0  # cipkey, length
+    init_state = int(st[0])
+    st[0], st[6] = 10, 4                                       # some later state, clientIPKey x-forwarded-for
+    st[12:16] = np.frombuffer(np.uint32(77).tobytes(), np.uint8)
+    assert ebd.lib().ebd_parser_reset(ebd._p(st)) == 0
+    assert st[0] == init_state and st[6] == 4 and st[12:16].view(np.uint32)[0] == 0
+    assert ebd.lib().ebd_client_ip_key_name(4) == b"x-forwarded-for"
+    assert ebd.lib().ebd_client_ip_key_name(0) == b""
