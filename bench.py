@@ -371,7 +371,9 @@ def run_config(args, cfg, E, steps, warmup, world, rank, dev, key, mode):
                  "records_exchanged": int(tot[2]), "record_bytes_per_interval": int(tot[3]),
                  "string_bytes_per_interval": int(tot[4]), "need_flag_bytes_per_interval": int(tot[5]),
                  "string_bytes_if_one_round": int(tot[6]), "record_size": shard.REC.itemsize,
-                 "protocol": "two rounds: records, need flags back, endpoint bytes only for keys new to the owner"}
+                 "protocol": "two rounds: records, need flags back, endpoint bytes only for keys new to the owner",
+                 "split_ms_rank0": {"export": x["export_ms"], "exchange": x["exchange_ms"], "device_merge": x["merge_ms"]},
+                 "host_reads_per_interval": x["host_reads"]}
         if rank != 0:
             return None
 

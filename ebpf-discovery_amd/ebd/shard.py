@@ -274,7 +274,7 @@ def exchange_merge(table, device="cpu", group=None, two_round=True, stats=None):
     out_r, rc = exchange_counts(r, counts, REC.itemsize, group)
     got = out_r.cpu().numpy().view(REC).copy()
     need = claimers(got, rc, rank)
-    back, _ = exchange_counts(torch.from_numpy(need.astype(np.uint8)).to(device), rc, 1, group)
+    back = return_to_sources(torch.from_numpy(need.astype(np.uint8)).to(device), rc, counts, group)
     mask = back.cpu().numpy().astype(bool)
     nb = wire_bytes(rec["endpoint_len"])
     soff = np.zeros(nb.size, np.int64)
@@ -288,6 +288,18 @@ def exchange_merge(table, device="cpu", group=None, two_round=True, stats=None):
         stats.update(record_bytes=rec.nbytes, string_bytes=int(sent.size), need_bytes=int(need.size),
                      string_bytes_one_round=int(strings.size))
     return merged_with_bytes(got, need, out_s.cpu().numpy())
+
+
+def return_to_sources(flags, rc, counts, group=None):
+    """One uint8 per received record (rc[s] from source s, in source order) back to the record's
+    source, which gets counts[w] flags from owner w in the order it sent them.  Both sides know
+    the sizes already (the record exchange's), so nothing is read back to the host."""
+    import torch
+    import torch.distributed as dist
+    out = torch.empty(int(np.sum(counts)), dtype=torch.uint8, device=flags.device)
+    dist.all_to_all_single(out, flags, output_split_sizes=[int(c) for c in counts],
+                           input_split_sizes=[int(c) for c in rc], group=group)
+    return out
 
 
 def claimers(w, rc, rank):
@@ -367,23 +379,33 @@ def device_exchange_merge(ctx, device, group=None, map_first=None, two_round=Tru
     trace positions, applied before the exchange.  Returns {sent, received, record_bytes,
     string_bytes, need_bytes, string_bytes_one_round, net_sent, net_received}: this rank's
     records out and in, and the bytes it sent."""
+    import time
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    check_same_hash_key(ctx, device, group)
-    recs, strs, counts, scounts = ctx.export_services_device(world, device)
+    t0 = time.perf_counter()
+    check_same_hash_key(ctx, device, group)  # once per context and group
+    recs, strs, counts, scounts = ctx.export_services_device(world, device)  # counts: the export's one sync
     if map_first is not None:
         map_wire_first(recs, map_first)
     nets = ncounts = None
     if getattr(ctx, "network_counters", False):
         nets, ncounts = group_by_owner(ctx.networks_device(device), NET_REC_BYTES, world)
+    t_export = time.perf_counter()
+    t_merge = 0.0  # the device merges' share (each C call returns when its work is done)
+    d2h = 1        # host reads of exchange sizes (the export's counts included)
     if not two_round:
         out_r, out_s = exchange(recs, strs, counts, scounts, group)
+        d2h += 2
+        tm = time.perf_counter()
         ctx.reset_services()
         ctx.merge_services_device(out_r, out_s)
+        t_merge += time.perf_counter() - tm
         sent_bytes, need_bytes = strs.numel(), 0
     else:
         out_r, rc = exchange_counts(recs, counts, REC.itemsize, group)
+        d2h += 1
+        tm = time.perf_counter()
         ctx.reset_services()
         n_in = out_r.numel() // REC.itemsize
         dst = torch.empty(n_in, dtype=torch.int64, device=device)
@@ -394,22 +416,54 @@ def device_exchange_merge(ctx, device, group=None, map_first=None, two_round=Tru
         ctx.merge_service_keys_device(out_r[a * rb:b * rb], dst[a:b])
         ctx.merge_service_keys_device(out_r[:a * rb], dst[:a])
         ctx.merge_service_keys_device(out_r[b * rb:], dst[b:])
+        t_merge += time.perf_counter() - tm
         need_in = (dst >= 0).to(torch.uint8)
-        need, _ = exchange_counts(need_in, rc, 1, group)  # one flag per record this rank sent
+        # one flag per record back to its source: both sides already know the sizes (the records'
+        # counts), so no size exchange and no host read
+        need = return_to_sources(need_in, rc, counts, group)
         sbytes = ctx.wire_compact_device(recs, strs, need)
-        bc = owner_byte_counts(recs, need, counts, world)
-        out_s, _ = exchange_counts(sbytes, bc, 1, group, slack=STR_SLACK)
+        # the byte counts per owner and per source from the device in one read
+        bc = owner_byte_counts_device(recs, need, counts, world)
+        rbc = torch.empty_like(bc)
+        dist.all_to_all_single(rbc, bc, group=group)
+        both = torch.cat([bc, rbc]).cpu().numpy()
+        d2h += 1
+        out_s = torch.zeros(int(both[world:].sum()) + STR_SLACK, dtype=torch.uint8, device=device)
+        dist.all_to_all_single(out_s[:int(both[world:].sum())], sbytes,
+                               output_split_sizes=[int(c) for c in both[world:]],
+                               input_split_sizes=[int(c) for c in both[:world]], group=group)
+        tm = time.perf_counter()
         ctx.merge_service_bytes_device(out_r, dst, out_s)
+        t_merge += time.perf_counter() - tm
         sent_bytes, need_bytes = sbytes.numel(), need_in.numel()
     out_n = None
     if nets is not None:
         out_n = exchange_fixed(nets, ncounts, NET_REC_BYTES, group)
+        d2h += 1
+        tm = time.perf_counter()
         ctx.merge_networks_device(out_n)
+        t_merge += time.perf_counter() - tm
+    t_end = time.perf_counter()
     return {"sent": int(counts.sum()), "received": out_r.numel() // REC.itemsize,
             "record_bytes": recs.numel(), "string_bytes": sent_bytes, "need_bytes": need_bytes,
             "string_bytes_one_round": strs.numel(),
             "net_sent": int(ncounts.sum()) if ncounts is not None else 0,
-            "net_received": out_n.numel() // NET_REC_BYTES if out_n is not None else 0}
+            "net_received": out_n.numel() // NET_REC_BYTES if out_n is not None else 0,
+            "export_ms": (t_export - t0) * 1e3, "merge_ms": t_merge * 1e3,
+            "exchange_ms": (t_end - t_export - t_merge) * 1e3, "host_reads": d2h}
+
+
+def owner_byte_counts_device(recs, need, counts, world):
+    """owner_byte_counts left on the device (int64 tensor of world entries)."""
+    import torch
+    n = recs.numel() // REC.itemsize
+    if n == 0:
+        return torch.zeros(world, dtype=torch.int64, device=recs.device)
+    ln = recs.view(torch.int32).view(n, REC.itemsize // 4)[:, 9].to(torch.int64) & 0xFFFFFFFF  # endpoint_len
+    nb = torch.where((ln & WIRE_NO_BYTES) != 0, torch.zeros_like(ln), (ln + 7) & ~7) * need.to(torch.int64)
+    own = torch.repeat_interleave(torch.arange(world, device=recs.device),
+                                  torch.tensor(np.asarray(counts, np.int64), device=recs.device))
+    return torch.zeros(world, dtype=torch.int64, device=recs.device).index_add_(0, own, nb)
 
 
 def owner_byte_counts(recs, need, counts, world):
@@ -522,11 +576,15 @@ def check_same_hash_key(ctx, device, group=None):
     every rank's context uses the same service-key secret."""
     import torch
     import torch.distributed as dist
+    tag = (id(group), dist.get_world_size(group))
+    if getattr(ctx, "_hash_key_checked", None) == tag:  # the key is fixed per context: once per group
+        return
     mine = torch.tensor(np.array(ctx.hash_key, np.uint64).view(np.int64), device=device)
     parts = [torch.empty_like(mine) for _ in range(dist.get_world_size(group))]
     dist.all_gather(parts, mine, group=group)
     if any(not torch.equal(p, mine) for p in parts):
         raise ValueError("device_exchange_merge: ranks key services with different secrets (pass one hash_key)")
+    ctx._hash_key_checked = tag
 
 
 def torch_int64():
