@@ -12,7 +12,7 @@ B=$(python3 -c "import sys; sys.path.insert(0, 'ebpf-discovery_amd'); import ebd
 T=${1:-$B}
 O=gpurun_out/prof_$T
 mkdir -p "$O"
-CMD="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+CMD="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config4"
 tools/gpu_steps.sh \
 	"pmc_fetch:240:rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o p --output-format csv -- $CMD" \
 	"pmc_write:240:rocprofv3 --pmc WRITE_SIZE -d $O/write -o p --output-format csv -- $CMD" \
