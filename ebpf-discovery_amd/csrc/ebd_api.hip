@@ -30,8 +30,8 @@ hipError_t launch_lru_bound(const Dev& d, uint32_t nslow, int* delta, uint8_t* m
 hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_t* head, SessState* S, uint32_t* live,
 		uint32_t cap, hipStream_t st, int cus);
 size_t sess_state_bytes();
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t front, uint32_t window, hipStream_t st,
-		int cus);
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t window, hipStream_t st, int cus);
+hipError_t launch_lru_ctl_init(const LruRound& w, uint32_t window, hipStream_t st);
 hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus);
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus);
 size_t lru_scan_blocks(uint32_t n);
@@ -622,7 +622,7 @@ static int lru_alloc(ebd_ctx* c) {
 			{(void**)&w.mk_e, 4 * (n + cc)}, {(void**)&w.ev_t, 4 * n}, {(void**)&w.cm_end, 4 * cc}, {(void**)&w.cm_head, 4 * cc},
 			{(void**)&w.f[0], n}, {(void**)&w.f[1], n}, {(void**)&w.cf[0], cc}, {(void**)&w.cf[1], cc}, {(void**)&w.bf, 16 * nb},
 			{(void**)&w.bm, 4 * nb}, {(void**)&w.lst, 8 * nb}, {(void**)&w.moff, 4 * nb}, {(void**)&w.be, 4 * nb}, {(void**)&w.eoff, 4 * nb},
-			{(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32}, {(void**)&w.nf_t, n},
+			{(void**)&w.ctl, sizeof(LruCtrl)}, {(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32}, {(void**)&w.nf_t, n},
 			{(void**)&w.vic, 4 * (n + cc)}, {(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
 			{(void**)&w.qfe, 4 * (n + 1)}, {(void**)&w.wto, 4 * n}, {(void**)&w.snap, sess_state_bytes() * n}};
 	size_t total = 0;
@@ -660,37 +660,33 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 		return w > 0 ? (uint32_t)w : 8192u; // 1 M config-4 events, LRU 2048: 2048 -> 523 ms, 4096 -> 394, 8192 -> 347, 16384 -> 387
 	}();
 	const uint32_t window = c->lru_window ? c->lru_window : env_window;
-	int cur = 0;
-	uint32_t front = 0;
 	// a round settles at least one event and usually most of a window (1 M config-4 events: ~3.3
 	// rounds per window), so the cap grows with the windows the batch holds
 	const int max_rounds = (int)std::min<unsigned long long>(1ull << 30, 4096ull + 8ull * ((d.n + window - 1) / window));
-	for (int r = 0; r < max_rounds; r++) {
-		HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, cur, front, window, c->stream, c->cus); }));
-		HIP_TRY(hipMemcpyAsync(c->h_lr, w.cnt, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-		HIP_TRY(hipMemcpyAsync(c->h_lr + 4, w.tot, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+	// The rounds advance their frontier on the device (k_lru_advance) and stop themselves once
+	// settled, so the host enqueues them kRoundChunk at a time and reads the control word once per
+	// chunk: no host round trip per round (a settled chunk's remaining rounds exit at once).
+	constexpr int kRoundChunk = 8;
+	HIP_TRY(launch_lru_ctl_init(w, window, c->stream));
+	LruCtrl* h = (LruCtrl*)c->h_lr;
+	static_assert(sizeof(LruCtrl) <= 8 * sizeof(unsigned long long), "the control word fits the host read buffer");
+	int r = 0;
+	for (;;) {
+		for (int k = 0; k < kRoundChunk; k++, r++)
+			HIP_TRY(timed(c, KT_WALK, [&] { return launch_lru_round(d, nslow, w, r & 1, window, c->stream, c->cus); }));
+		HIP_TRY(hipMemcpyAsync(h, w.ctl, sizeof(LruCtrl), hipMemcpyDeviceToHost, c->stream));
 		HIP_TRY(hipStreamSynchronize(c->stream));
-		c->lru_rounds++;
-		const uint32_t* tot = (const uint32_t*)(c->h_lr + 4);
-		const unsigned long long changed = c->h_lr[2], first = c->h_lr[3];
-		const unsigned long long wend = (unsigned long long)front + window;
 		if (lru_trace)
-			std::fprintf(stderr, "ebd lru round %d: front %u, evictions %u (window to %u), flags changed %llu, first at %lld, walked %u\n", r,
-					front, tot[1], tot[2], changed, first == ~0ull ? -1ll : (long long)first, tot[3]);
-		if (c->h_lr[1]) // operations with a full cache and no victim: not a world to walk on
-			return 0;
-		if (changed == 0 && wend >= d.n) { // the world derived is the world walked, to the batch's end
-			*settled = 1;
+			std::fprintf(stderr, "ebd lru rounds %d..%d: front %u, done %u, settled %u, rounds run %u\n", r - kRoundChunk, r - 1, h->front,
+					h->done, h->settled, h->rounds);
+		if (h->done || r >= max_rounds)
 			break;
-		}
-		if (changed == 0)
-			front = (uint32_t)wend;
-		else if (first != ~0ull) // events before the first changed flag (and the window's end) are settled
-			front = (uint32_t)(first < wend ? first : wend);
-		cur ^= 1;
 	}
-	if (!*settled)
+	c->lru_rounds += h->rounds;
+	if (!h->done || !h->settled)
 		return 0;
+	*settled = 1;
+	const int cur = (int)h->cur_final;
 	HIP_TRY(timed(c, KT_WALK, [&] { return launch_walk_flags(d, nslow, w.f[cur], w.cf[cur], c->stream, c->cus); }));
 	HIP_TRY(hipMemcpyAsync(c->d_ctr + CTR_EVICTIONS, w.cnt, sizeof(unsigned long long), hipMemcpyDeviceToDevice, c->stream));
 	return 0;

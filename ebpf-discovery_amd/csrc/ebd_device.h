@@ -128,7 +128,16 @@ static_assert(sizeof(ClaimRec) == 24, "claim record is 24 bytes");
 // Scratch of the exact-LRU rounds (k_lru_*, ebd_api.hip run_batch): per event (ops by sorted
 // position, opt by event, marker ends, eviction flags), the compacted markers and eviction
 // times, per carried session, the two worlds of eviction flags, per scan block.
+// The exact-LRU rounds' control word, advanced on the device at the end of every round
+// (k_lru_advance), so the host enqueues rounds without reading each one's counters: the
+// window's first event, the horizon, done (settled, or an inconsistent world), the world the
+// walk settled in, and the rounds that ran.  Every round kernel returns at once when done.
+struct LruCtrl {
+	uint32_t front, tend, done, settled, cur_final, rounds, pad_[2];
+};
+
 struct LruRound {
+	LruCtrl* ctl;
 	uint8_t* opt;
 	uint32_t* mend;
 	uint8_t* evt;

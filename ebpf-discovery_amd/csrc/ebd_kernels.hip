@@ -1613,12 +1613,15 @@ struct DryWalk {
 	SessState* snap;
 	uint32_t* wto;
 	uint8_t* opt;
-	uint32_t hz;
+	const LruCtrl* ctl;   // the round's horizon (ctl->tend); nothing to do once ctl->done
 };
 
 template <bool DRY>
 __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
 		const uint32_t* hcount) {
+	if (DRY && dw.ctl->done) // the rounds have settled: later rounds' kernels do nothing
+		return;
+	const uint32_t hz = DRY ? dw.ctl->tend : 0u;
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
 		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
@@ -1701,7 +1704,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 					}
 					if (DRY) {
 						dw.snap[jj] = S; // the state before event jj: a later walk may start here
-						if (i >= dw.hz) { // past the round's horizon: a later round continues here
+						if (i >= hz) { // past the round's horizon: a later round continues here
 							dw.wto[jhead] = jj;
 							have = false;
 							h += stride;
@@ -2138,7 +2141,10 @@ __global__ void k_lru_carry_rank(Dev d, const uint32_t* cm_end, uint32_t* mk_ref
 // The round's walks: per session (k_walk_heads' list), from its first changed position if
 // that lies in the part walked before (cpos; cleared here), else from where the last walk
 // stopped (wto) if that event comes before the horizon.  Entries are start positions.
-__global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, uint32_t hz, uint32_t* rlist, uint32_t* tot) {
+__global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, const LruCtrl* ctl, uint32_t* rlist, uint32_t* tot) {
+	if (ctl->done)
+		return;
+	const uint32_t hz = ctl->tend;
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS];
 	for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
 		const uint32_t jh = d.heads[h], c = cpos[jh], wt = wto[jh];
@@ -2158,7 +2164,9 @@ __global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, uint3
 // Phase 1: each block's composed size map and its marker count.
 // zero: a per-event byte array cleared on the way (the round's victim flags, nf_t).
 __global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint32_t n, uint32_t cap, LFn* bf, uint32_t* bm,
-		uint8_t* zero) {
+		uint8_t* zero, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	__shared__ LFn F[kLsT];
 	__shared__ uint32_t M[kLsT];
 	const uint32_t t = threadIdx.x;
@@ -2194,7 +2202,9 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint
 // carried ones).
 // zc, zn: the round's carried-session flags (ncf), cleared on the way.
 __global__ __launch_bounds__(kLsT) void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0,
-		long long* lst, uint32_t* moff, uint32_t* tot, uint8_t* zc, uint32_t zn) {
+		long long* lst, uint32_t* moff, uint32_t* tot, uint8_t* zc, uint32_t zn, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	__shared__ LFn F[kLsT];
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
@@ -2262,7 +2272,9 @@ __device__ __forceinline__ uint32_t u32_block_excl(uint32_t x, uint32_t* S, uint
 
 // Phase 3: each event's size before it; evt[i] = 1 where an insert finds the cache full.
 __global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uint32_t n, uint32_t cap, const long long* lst,
-		uint8_t* evt, uint32_t* be) {
+		uint8_t* evt, uint32_t* be, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	__shared__ LFn F[kLsT];
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
@@ -2292,7 +2304,9 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uin
 
 // Phase 4 (one workgroup): each scan block's first eviction index; tot[5] = the evictions
 // before the frontier (k_lru_compact sets it when the frontier lies inside the batch).
-__global__ __launch_bounds__(kLsT) void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot) {
+__global__ __launch_bounds__(kLsT) void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
 	uint32_t e = 0;
@@ -2311,7 +2325,10 @@ __global__ __launch_bounds__(kLsT) void k_lru_scan_top2(const uint32_t* be, uint
 
 // Phase 5: the markers (event position, end) and the eviction times, in event order.
 __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const uint32_t* mend, const uint8_t* evt, uint32_t n,
-		const uint32_t* moff, const uint32_t* eoff, uint32_t front, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* tot) {
+		const uint32_t* moff, const uint32_t* eoff, const LruCtrl* ctl, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* tot) {
+	if (ctl->done)
+		return;
+	const uint32_t front = ctl->front;
 	__shared__ uint32_t S[kLsT];
 	const uint32_t t = threadIdx.x;
 	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
@@ -2352,8 +2369,11 @@ __global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const 
 // window's end (first eviction not processed).  cnt[1] = 1: the operations are inconsistent
 // (a full cache with no victim).
 constexpr uint32_t kGrM = 8192, kGrE = 2048; // markers / evictions staged in LDS at a time
-__global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const uint32_t* ev_t, uint32_t* tot, uint32_t tend,
+__global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const uint32_t* ev_t, uint32_t* tot, const LruCtrl* ctl,
 		uint32_t* vict, uint32_t* qfe, unsigned long long* cnt) {
+	if (ctl->done)
+		return;
+	const uint32_t tend = ctl->tend;
 	__shared__ uint32_t se[kGrM], sv[kGrE];
 	__shared__ uint32_t s_qf, s_j, s_more, s_bad, s_rec;
 	const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -2505,7 +2525,9 @@ __global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const 
 // Phase 6b: the world the evictions before the window's end imply, by event (nf_t zeroed
 // before): the victim's next find, or the victims with none (tot[4] of them) in vic.
 __global__ void k_lru_victims(const uint32_t* tot, const uint32_t* vict, const uint32_t* mk_ref, const uint32_t* mk_e,
-		const uint32_t* ev_t, uint8_t* nf_t, uint32_t* vic, uint32_t* vtot, unsigned long long* cnt) {
+		const uint32_t* ev_t, uint8_t* nf_t, uint32_t* vic, uint32_t* vtot, unsigned long long* cnt, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	const uint32_t ne = tot[2];
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ne; j += gridDim.x * blockDim.x) {
 		const uint32_t q = vict[j], vr = mk_ref[q], ve = mk_e[q];
@@ -2520,12 +2542,16 @@ __global__ void k_lru_victims(const uint32_t* tot, const uint32_t* vict, const u
 
 // Phase 6c: the round's flags by sorted position: bit 0 from nf_t, then bit 1 (after the
 // session's last event) or the carry flag for the listed victims (ncf zeroed before).
-__global__ void k_lru_flags(Dev d, uint32_t nslow, const uint8_t* nf_t, uint8_t* nf) {
+__global__ void k_lru_flags(Dev d, uint32_t nslow, const uint8_t* nf_t, uint8_t* nf, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
 		nf[j] = nf_t[(uint32_t)d.slow_keys[j]];
 }
 __global__ void k_lru_tails(const uint32_t* vtot, const uint32_t* vic, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head,
-		uint8_t* nf, uint8_t* ncf) {
+		uint8_t* nf, uint8_t* ncf, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	const uint32_t nv = *vtot;
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nv; k += gridDim.x * blockDim.x) {
 		const uint32_t vr = vic[k];
@@ -2544,7 +2570,9 @@ __global__ void k_lru_tails(const uint32_t* vtot, const uint32_t* vic, const uin
 // Phase 7: how many flags the round changed (cnt[2]), the first event whose eviction bit
 // changed (cnt[3]: the new frontier), and where each session's walk must start again (cpos).
 __global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, const uint8_t* cf, const uint8_t* ncf, uint32_t n2,
-		const unsigned long long* keys, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt) {
+		const unsigned long long* keys, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt, const LruCtrl* ctl) {
+	if (ctl->done)
+		return;
 	uint32_t x = 0, first = kNone;
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x) {
 		const bool dk = k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
@@ -3671,44 +3699,86 @@ hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipS
 // frontier.
 // A round's counters: the walk list (tot[3]), the victims listed (tot[4]), and cnt (evictions,
 // inconsistency, flags changed, first changed event).
-__global__ void k_lru_round_reset(uint32_t* tot, unsigned long long* cnt) {
-	if (threadIdx.x == 0) {
+__global__ void k_lru_round_reset(uint32_t* tot, unsigned long long* cnt, const LruCtrl* ctl) {
+	if (threadIdx.x == 0 && !ctl->done) {
 		tot[3] = tot[4] = 0;
 		cnt[0] = cnt[1] = cnt[2] = 0;
 		cnt[3] = ~0ull;
 	}
 }
 
-hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t front, uint32_t window, hipStream_t st,
-		int cus) {
+// The end of a round (one thread): the world derived is the world walked up to the batch's
+// end -> settled in world cur; an inconsistent world -> done, not settled (the one-lane replay
+// takes the batch); else the frontier moves past every event the round settled.
+__global__ void k_lru_advance(LruCtrl* ctl, const unsigned long long* cnt, uint32_t window, uint32_t n, uint32_t cur) {
+	if (threadIdx.x != 0 || ctl->done)
+		return;
+	ctl->rounds++;
+	const unsigned long long changed = cnt[2], first = cnt[3];
+	const unsigned long long wend = (unsigned long long)ctl->front + window;
+	if (cnt[1]) { // operations with a full cache and no victim: not a world to walk on
+		ctl->done = 1;
+		ctl->settled = 0;
+		return;
+	}
+	if (changed == 0 && wend >= n) {
+		ctl->done = 1;
+		ctl->settled = 1;
+		ctl->cur_final = cur;
+		return;
+	}
+	unsigned long long front = ctl->front;
+	if (changed == 0)
+		front = wend;
+	else if (first != ~0ull) // events before the first changed flag (and the window's end) are settled
+		front = first < wend ? first : wend;
+	const unsigned long long tend = front + window;
+	ctl->front = (uint32_t)front;
+	ctl->tend = (uint32_t)(tend < 0xffffffffull ? tend : 0xffffffffull);
+}
+
+__global__ void k_lru_ctl_init(LruCtrl* ctl, uint32_t window) {
+	if (threadIdx.x == 0) {
+		ctl->front = 0;
+		ctl->tend = window;
+		ctl->done = ctl->settled = ctl->cur_final = ctl->rounds = 0;
+	}
+}
+
+hipError_t launch_lru_ctl_init(const LruRound& w, uint32_t window, hipStream_t st) {
+	hipLaunchKernelGGL(k_lru_ctl_init, dim3(1), dim3(64), 0, st, w.ctl, window);
+	return hipGetLastError();
+}
+
+hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t window, hipStream_t st, int cus) {
 	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
 	const uint8_t* f = w.f[cur];
 	uint8_t* nf = w.f[cur ^ 1];
 	const uint8_t* cf = w.cf[cur];
 	uint8_t* ncf = w.cf[cur ^ 1];
-	const unsigned long long tend64 = (unsigned long long)front + window;
-	const uint32_t tend = (uint32_t)(tend64 < 0xffffffffull ? tend64 : 0xffffffffull);
-	hipLaunchKernelGGL(k_lru_round_reset, dim3(1), dim3(64), 0, st, w.tot, w.cnt);
-	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, tend, w.rlist, w.tot);
+	const LruCtrl* ctl = w.ctl;
+	hipLaunchKernelGGL(k_lru_round_reset, dim3(1), dim3(64), 0, st, w.tot, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, ctl, w.rlist, w.tot);
 	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
-			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, tend}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
-	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm, w.nf_t);
+			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, ctl}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
+	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm, w.nf_t, ctl);
 	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(kLsT), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
-			w.moff, w.tot, ncf, d.carry_cap);
+			w.moff, w.tot, ncf, d.carry_cap, ctl);
 	hipLaunchKernelGGL(k_lru_scan_apply, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (const long long*)w.lst,
-			w.evt, w.be);
-	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(kLsT), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot);
+			w.evt, w.be, ctl);
+	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(kLsT), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot, ctl);
 	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
-			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, front, w.mk_ref, w.mk_e, w.ev_t, w.tot);
-	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot, tend, w.vict,
+			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, ctl, w.mk_ref, w.mk_e, w.ev_t, w.tot);
+	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot, ctl, w.vict,
 			w.qfe, w.cnt);
 	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
-			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.nf_t, w.vic, w.tot + 4, w.cnt);
-	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.nf_t, nf);
+			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.nf_t, w.vic, w.tot + 4, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.nf_t, nf, ctl);
 	hipLaunchKernelGGL(k_lru_tails, dim3(cus), dim3(256), 0, st, (const uint32_t*)(w.tot + 4), (const uint32_t*)w.vic, (const uint32_t*)w.jpos,
-			(const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf);
+			(const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf, ctl);
 	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(nslow + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, f, (const uint8_t*)nf, nslow, cf,
-			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.cpos, w.cnt);
+			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.cpos, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_advance, dim3(1), dim3(64), 0, st, w.ctl, (const unsigned long long*)w.cnt, window, n, (uint32_t)cur);
 	return hipGetLastError();
 }
 // The final walk of the exact path in the converged world (with output), then the carried
