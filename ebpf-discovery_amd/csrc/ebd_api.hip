@@ -31,7 +31,8 @@ hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_
 		uint32_t cap, hipStream_t st, int cus);
 size_t sess_state_bytes();
 hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t window, hipStream_t st, int cus);
-hipError_t launch_lru_ctl_init(const LruRound& w, uint32_t window, hipStream_t st);
+hipError_t launch_lru_ctl_init(const Dev& d, const LruRound& w, uint32_t window, hipStream_t st);
+int lru_size_limit();
 hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipStream_t st, int cus);
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus);
 size_t lru_scan_blocks(uint32_t n);
@@ -618,13 +619,12 @@ static int lru_alloc(ebd_ctx* c) {
 	struct Part {
 		void** p;
 		size_t bytes;
-	} parts[] = {{(void**)&w.opt, n}, {(void**)&w.mend, 4 * n}, {(void**)&w.evt, n}, {(void**)&w.mk_ref, 4 * (n + cc)},
-			{(void**)&w.mk_e, 4 * (n + cc)}, {(void**)&w.ev_t, 4 * n}, {(void**)&w.cm_end, 4 * cc}, {(void**)&w.cm_head, 4 * cc},
-			{(void**)&w.f[0], n}, {(void**)&w.f[1], n}, {(void**)&w.cf[0], cc}, {(void**)&w.cf[1], cc}, {(void**)&w.bf, 16 * nb},
-			{(void**)&w.bm, 4 * nb}, {(void**)&w.lst, 8 * nb}, {(void**)&w.moff, 4 * nb}, {(void**)&w.be, 4 * nb}, {(void**)&w.eoff, 4 * nb},
-			{(void**)&w.ctl, sizeof(LruCtrl)}, {(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32}, {(void**)&w.nf_t, n},
-			{(void**)&w.vic, 4 * (n + cc)}, {(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
-			{(void**)&w.qfe, 4 * (n + 1)}, {(void**)&w.wto, 4 * n}, {(void**)&w.snap, sess_state_bytes() * n}};
+	} parts[] = {{(void**)&w.opt, n}, {(void**)&w.mend, 4 * n}, {(void**)&w.mk_ref, 4 * (n + cc)}, {(void**)&w.mk_e, 4 * (n + cc)},
+			{(void**)&w.ev_t, 4 * n}, {(void**)&w.evc, 4 * n}, {(void**)&w.cm_end, 4 * cc}, {(void**)&w.cm_head, 4 * cc},
+			{(void**)&w.f[0], n}, {(void**)&w.f[1], n}, {(void**)&w.cf[0], cc}, {(void**)&w.cf[1], cc}, {(void**)&w.bs, sizeof(LsState) * (nb + 1)},
+			{(void**)&w.ctl, sizeof(LruCtrl)}, {(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32},
+			{(void**)&w.nf_t, n}, {(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
+			{(void**)&w.mx, 4 * (n + cc + 64)}, {(void**)&w.wto, 4 * n}, {(void**)&w.snap, sess_state_bytes() * n}};
 	size_t total = 0;
 	for (const Part& q : parts)
 		total += (q.bytes + 255) & ~(size_t)255;
@@ -647,6 +647,8 @@ static int lru_alloc(ebd_ctx* c) {
 // rounds did not settle (the caller replays the batch sequentially instead).
 static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled) {
 	*settled = 0;
+	if (c->carry_cap >= (uint32_t)lru_size_limit())
+		return 0; // the rounds' 32-bit size maps do not reach: the one-lane replay takes the batch
 	if (int rc = lru_alloc(c))
 		return rc;
 	LruRound& w = c->lr;
@@ -667,7 +669,7 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	// settled, so the host enqueues them kRoundChunk at a time and reads the control word once per
 	// chunk: no host round trip per round (a settled chunk's remaining rounds exit at once).
 	constexpr int kRoundChunk = 8;
-	HIP_TRY(launch_lru_ctl_init(w, window, c->stream));
+	HIP_TRY(launch_lru_ctl_init(d, w, window, c->stream));
 	LruCtrl* h = (LruCtrl*)c->h_lr;
 	static_assert(sizeof(LruCtrl) <= 8 * sizeof(unsigned long long), "the control word fits the host read buffer");
 	int r = 0;

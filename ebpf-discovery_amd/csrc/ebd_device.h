@@ -136,32 +136,32 @@ struct LruCtrl {
 	uint32_t front, tend, done, settled, cur_final, rounds, pad_[2];
 };
 
+// A scan block's start state in the exact-LRU rounds: the LRU's size, the markers and the
+// evictions before the block.
+struct LsState {
+	int x;
+	uint32_t m, e, pad_;
+};
 struct LruRound {
 	LruCtrl* ctl;
-	uint8_t* opt;
-	uint32_t* mend;
-	uint8_t* evt;
+	uint8_t* opt;    // per event: its LRU operation in the walked world
+	uint32_t* mend;  // per event: the session's next find
 	uint32_t* mk_ref;
 	uint32_t* mk_e;
 	uint32_t* ev_t;
+	uint32_t* evc;   // per event: the evictions before it
 	uint32_t* cm_end;
 	uint32_t* cm_head;
 	uint8_t* f[2];
 	uint8_t* cf[2];
-	void* bf; // LFn per scan block
-	uint32_t* bm;
-	long long* lst;
-	uint32_t* moff;
-	uint32_t* be;
-	uint32_t* eoff;
-	uint32_t* tot; // 0 markers, 1 evictions, 2 window end, 3 next walk list, 4 listed victims, 5 evictions before the frontier
+	LsState* bs;     // per scan block: its start state
+	uint32_t* tot; // 1 evictions (to the span's end), 2 window end, 3 next walk list, 5 evictions before the frontier, 6 markers born before the horizon, 7 evictions before it
 	uint32_t* jpos;
 	uint32_t* head;
 	unsigned long long* cnt;
 	uint8_t* nf_t; // the round's eviction flags by event
-	uint32_t* vic; // victims with no later find
 	uint32_t* vict; // per eviction: its victim marker
-	uint32_t* qfe;  // per eviction: the marker queue's front before it
+	uint32_t* mx;   // per marker from the round's queue front: its threshold (k_lru_thresh)
 	uint32_t* cpos;  // per session (first sorted position): its first changed position, kNone
 	uint32_t* rlist; // the round's walks: start positions
 	uint32_t* wto;   // per session: where its last walk stopped (kNone: at its end)

@@ -1621,6 +1621,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 		const uint32_t* hcount) {
 	if (DRY && dw.ctl->done) // the rounds have settled: later rounds' kernels do nothing
 		return;
+	if (DRY && blockIdx.x * kWalkThreads >= *hcount)
+		return; // a round walks few sessions: the workgroups past them skip the table load
 	const uint32_t hz = DRY ? dw.ctl->tend : 0u;
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
 	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
@@ -2085,18 +2087,20 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // A round therefore only derives the evictions in a window [F, F + H) (the greedy resumes at
 // F from its saved state) and only walks again the sessions whose flags changed.
 // ---------------------------------------------------------------------------------
-constexpr int kLsT = 256, kLsPer = 16;
-constexpr uint32_t kLsBlk = kLsT * kLsPer; // events per scan block
-constexpr long long kLInf = 1ll << 60;
+constexpr int kScT = 1024, kScPer = 4;
+constexpr uint32_t kLsBlk = kScT * kScPer; // events per scan block
+// x -> min(a, x + b) in 32 bits: sizes stay below 2^30 (the LRU capacity and the carried
+// sessions, checked on the host), a block's b within +-kLsBlk
+constexpr int kLInf = 1 << 30;
 struct LFn {
-	long long a, b; // x -> min(a, x + b)
+	int a, b;
 };
 __device__ __forceinline__ LFn lfn_id() { return LFn{kLInf, 0}; }
 __device__ __forceinline__ LFn lfn_op(uint32_t op, uint32_t cap) {
-	return op == OP_INSERT ? LFn{(long long)cap, 1} : op == OP_ERASE ? LFn{kLInf, -1} : lfn_id();
+	return op == OP_INSERT ? LFn{(int)cap, 1} : op == OP_ERASE ? LFn{kLInf, -1} : lfn_id();
 }
 __device__ __forceinline__ LFn lfn_then(LFn f, LFn g) { return LFn{min(g.a, f.a + g.b), f.b + g.b}; } // g after f
-__device__ __forceinline__ long long lfn_apply(LFn f, long long x) { return min(f.a, x + f.b); }
+__device__ __forceinline__ int lfn_apply(LFn f, int x) { return min(f.a, x + f.b); }
 __device__ __forceinline__ bool op_marks(uint32_t op) { return op == OP_INSERT || op == OP_ACCESS; }
 
 // Once per batch: each session event's next find (Discovery.cpp:114 for a buffer, :195 for a
@@ -2141,9 +2145,13 @@ __global__ void k_lru_carry_rank(Dev d, const uint32_t* cm_end, uint32_t* mk_ref
 // The round's walks: per session (k_walk_heads' list), from its first changed position if
 // that lies in the part walked before (cpos; cleared here), else from where the last walk
 // stopped (wto) if that event comes before the horizon.  Entries are start positions.
-__global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, const LruCtrl* ctl, uint32_t* rlist, uint32_t* tot) {
+// zc, zn: the round's carried-session flags (ncf), cleared on the way.
+__global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, const LruCtrl* ctl, uint32_t* rlist, uint32_t* tot,
+		uint8_t* zc, uint32_t zn) {
 	if (ctl->done)
 		return;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < zn; k += gridDim.x * blockDim.x)
+		zc[k] = 0;
 	const uint32_t hz = ctl->tend;
 	const uint32_t nh = (uint32_t)d.ctr[CTR_HEADS];
 	for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
@@ -2161,371 +2169,277 @@ __global__ void k_lru_walklist(Dev d, uint32_t* cpos, const uint32_t* wto, const
 	}
 }
 
-// Phase 1: each block's composed size map and its marker count.
-// zero: a per-event byte array cleared on the way (the round's victim flags, nf_t).
-__global__ __launch_bounds__(kLsT) void k_lru_scan_part(const uint8_t* opt, uint32_t n, uint32_t cap, LFn* bf, uint32_t* bm,
-		uint8_t* zero, const LruCtrl* ctl) {
+// The scan blocks a round derives: from the frontier's to the horizon's (the operations before
+// the frontier are settled, so are the earlier blocks' markers, evictions and start states
+// from the round that last derived them; nothing past the horizon is used).
+struct LsSpan {
+	uint32_t first, last; // scan blocks, inclusive
+};
+__device__ __forceinline__ LsSpan lru_span(const LruCtrl* ctl, uint32_t n) {
+	const uint32_t nb = (n + kLsBlk - 1) / kLsBlk, tend = ctl->tend;
+	const uint32_t first = min(ctl->front, n ? n - 1 : 0u) / kLsBlk;
+	const uint32_t last = tend < n ? tend / kLsBlk : (nb ? nb - 1 : 0u);
+	return LsSpan{first, last};
+}
+
+// Phases 1-5 in one workgroup, block by block over the span (about window / kLsBlk + 1 of
+// them): the LRU's size before each event (maps x -> min(a, x + b) scanned in event order, from
+// the block's start state), the evictions (an insert that finds the cache full), and the
+// markers (event, end) and eviction times in order, numbered on from the block's start
+// state; evc[i] = the evictions before event i.  bs[b + 1] = the state after block b.
+// tot[5] = the evictions before the frontier, tot[6] / tot[7] = the markers / evictions
+// before the horizon, tot[1] = the evictions up to the span's end.
+__device__ __forceinline__ LFn lfn_shfl_up(LFn f, uint32_t o) { return LFn{__shfl_up(f.a, o, 64), __shfl_up(f.b, o, 64)}; }
+__global__ __launch_bounds__(kScT) void k_lru_scan(const uint8_t* opt, const uint32_t* mend, uint32_t n, uint32_t cap, LsState* bs,
+		uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* evc, uint32_t* tot, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
-	__shared__ LFn F[kLsT];
-	__shared__ uint32_t M[kLsT];
-	const uint32_t t = threadIdx.x;
-	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
-	LFn f = lfn_id();
-	uint32_t m = 0;
-	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
-		const unsigned long long i = base + k;
-		if (i < n)
-			zero[i] = 0;
-		const uint32_t op = i < n ? opt[i] : OP_NONE;
-		f = lfn_then(f, lfn_op(op, cap));
-		m += op_marks(op) ? 1u : 0u;
-	}
-	F[t] = f;
-	M[t] = m;
-	__syncthreads();
-	for (uint32_t s = 1; s < (uint32_t)kLsT; s <<= 1) { // in-order tree: F[t] = F[t] then F[t + s]
-		if ((t & (2 * s - 1)) == 0) {
-			F[t] = lfn_then(F[t], F[t + s]);
-			M[t] += M[t + s];
+	constexpr uint32_t kW = kScT / 64;
+	const LsSpan sp = lru_span(ctl, n);
+	const uint32_t front = ctl->front, tend = ctl->tend;
+	__shared__ LFn wf[kW];
+	__shared__ uint32_t wm[kW], we[kW];
+	const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+	LsState st = bs[sp.first];
+	for (uint32_t blk = sp.first; blk <= sp.last; blk++) {
+		const uint32_t i0 = blk * kLsBlk + t * kScPer;
+		uint32_t ops4 = 0; // OP_NONE past the batch
+		if (i0 + kScPer <= n) {
+			ops4 = *(const uint32_t*)(opt + i0);
+		} else {
+			for (uint32_t k = 0; k < kScPer; k++)
+				if (i0 + k < n)
+					ops4 |= (uint32_t)opt[i0 + k] << (8 * k);
+		}
+		LFn f = lfn_id();
+		uint32_t mk = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < kScPer; k++) {
+			const uint32_t op = (ops4 >> (8 * k)) & 0xffu;
+			f = lfn_then(f, lfn_op(op, cap));
+			mk += op_marks(op) ? 1u : 0u;
+		}
+		LFn fi = f; // inclusive over the wave
+		uint32_t mi = mk;
+#pragma unroll
+		for (uint32_t o = 1; o < 64; o <<= 1) {
+			const LFn g = lfn_shfl_up(fi, o);
+			const uint32_t mg = __shfl_up(mi, o, 64);
+			if (lane >= o) {
+				fi = lfn_then(g, fi);
+				mi += mg;
+			}
+		}
+		if (lane == 63) {
+			wf[wv] = fi;
+			wm[wv] = mi;
 		}
 		__syncthreads();
+		LFn pre = lfn_id();
+		uint32_t m = st.m;
+		for (uint32_t w = 0; w < wv; w++) {
+			pre = lfn_then(pre, wf[w]);
+			m += wm[w];
+		}
+		const LFn fx = lfn_shfl_up(fi, 1);
+		const uint32_t mx_ = __shfl_up(mi, 1, 64);
+		if (lane) {
+			pre = lfn_then(pre, fx);
+			m += mx_;
+		}
+		int x = lfn_apply(pre, st.x);
+		uint32_t evs = 0, ne = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < kScPer; k++) {
+			const uint32_t op = (ops4 >> (8 * k)) & 0xffu;
+			const bool ev = op == OP_INSERT && x >= (int)cap;
+			evs |= (ev ? 1u : 0u) << k;
+			ne += ev ? 1u : 0u;
+			x = lfn_apply(lfn_op(op, cap), x);
+		}
+		uint32_t ni = ne;
+#pragma unroll
+		for (uint32_t o = 1; o < 64; o <<= 1) {
+			const uint32_t g = __shfl_up(ni, o, 64);
+			if (lane >= o)
+				ni += g;
+		}
+		if (lane == 63)
+			we[wv] = ni;
+		__syncthreads();
+		uint32_t e = st.e + ni - ne;
+		for (uint32_t w = 0; w < wv; w++)
+			e += we[w];
+		for (uint32_t k = 0; k < kScPer; k++) {
+			const uint32_t i = i0 + k;
+			if (i >= n)
+				break;
+			if (i == front)
+				tot[5] = e;
+			if (i == tend) {
+				tot[6] = m;
+				tot[7] = e;
+			}
+			evc[i] = e;
+			if (op_marks((ops4 >> (8 * k)) & 0xffu)) {
+				mk_ref[m] = i;
+				mk_e[m] = mend[i];
+				m++;
+			}
+			if ((evs >> k) & 1u)
+				ev_t[e++] = i;
+		}
+		LFn tf = lfn_id();
+		for (uint32_t w = 0; w < kW; w++) {
+			tf = lfn_then(tf, wf[w]);
+			st.m += wm[w];
+			st.e += we[w];
+		}
+		st.x = lfn_apply(tf, st.x);
+		if (t == 0)
+			bs[blk + 1] = st;
+		__syncthreads(); // wf / wm / we are reused
 	}
 	if (t == 0) {
-		bf[blockIdx.x] = F[0];
-		bm[blockIdx.x] = M[0];
+		if (tend >= n) {
+			tot[6] = st.m;
+			tot[7] = st.e;
+		}
+		tot[1] = st.e;
 	}
 }
 
-// Phase 2 (one workgroup of kLsT threads, kLsT scan blocks at a time): each scan block's
-// starting size from the context's carried sessions, and its first marker's index (after the
-// carried ones).
-// zc, zn: the round's carried-session flags (ncf), cleared on the way.
-__global__ __launch_bounds__(kLsT) void k_lru_scan_top(const LFn* bf, const uint32_t* bm, uint32_t nb, long long l0, uint32_t m0,
-		long long* lst, uint32_t* moff, uint32_t* tot, uint8_t* zc, uint32_t zn, const LruCtrl* ctl) {
+// Phase 6: the window's evictions [j0, jend) (those from the frontier to the horizon) take the
+// oldest marker alive at their time, in order (LRUCache.h:54-60's evict-the-back in the
+// sequential walk).  The merge resumes at qf, after the victim of eviction j0 - 1 (that
+// victim and every earlier marker is taken or dead by then), and only markers born before the
+// horizon can be victims (a later one would be an inconsistency k_lru_victims reports).  Taken
+// from the markers' side: marker m (in order) goes to eviction A, the evictions done so far,
+// when it is alive then, i.e. A < c_m = the window's evictions before its end e_m, and A += 1.
+// The map A -> A + [A < c] composes over a block of 64 markers into A -> A + #{k : A < X_k}
+// with one threshold per marker (marker k of the block is taken iff the block starts at
+// A < X_k), so k_lru_thresh derives every block's thresholds in parallel and k_lru_take
+// chains the blocks, one compare and popcount each, listing the victims (vict[j] = eviction
+// j's marker).  tot[2] = the window's end (first eviction not processed); cnt[1] = 1: the
+// operations are inconsistent (a full cache with no victim).
+constexpr uint32_t kThT = 256;
+__device__ __forceinline__ uint32_t lru_queue_front(const uint32_t* tot, const uint32_t* vict) {
+	const uint32_t j0 = tot[5];
+	return j0 ? vict[j0 - 1] + 1u : 0u;
+}
+// c_m from evc (the evictions before the marker's end).  The thresholds: with S the block's
+// positive thresholds so far (distinct; ms of them), the map A -> A + #{S > A} rises by one
+// at every A not in S, so X_k = the (c_k - ms)-th positive integer not in S (0 when
+// c_k <= ms: the markers before take c_k evictions from any start).  S is kept sorted in the
+// lanes: that integer is r + #{s_j : s_j - j < r} (one ballot), and it goes in at that rank
+// (a wave shift by one lane).
+__global__ __launch_bounds__(kThT) void k_lru_thresh(const uint32_t* mk_e, const uint32_t* evc, const uint32_t* tot, const LruCtrl* ctl,
+		const uint32_t* vict, uint32_t* mx) {
 	if (ctl->done)
 		return;
-	__shared__ LFn F[kLsT];
-	__shared__ uint32_t S[kLsT];
-	const uint32_t t = threadIdx.x;
-	for (uint32_t k = t; k < zn; k += kLsT)
-		zc[k] = 0;
-	long long x = l0;
-	uint32_t m = m0;
-	for (uint32_t c = 0; c < nb; c += kLsT) {
-		const bool in = c + t < nb;
-		const LFn f = in ? bf[c + t] : lfn_id();
-		const uint32_t mk = in ? bm[c + t] : 0u;
-		F[t] = f;
-		S[t] = mk;
-		__syncthreads();
-		for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) { // inclusive, in order
-			const LFn g = t >= o ? lfn_then(F[t - o], F[t]) : F[t];
-			const uint32_t y = t >= o ? S[t - o] + S[t] : S[t];
-			__syncthreads();
-			F[t] = g;
-			S[t] = y;
-			__syncthreads();
+	const uint32_t j0 = tot[5], jend = tot[7], mend = tot[6], qf = lru_queue_front(tot, vict), tend = ctl->tend;
+	if (jend <= j0 || qf >= mend)
+		return;
+	const uint32_t nj = jend - j0, nbk = (mend - qf + 63u) / 64u, wpb = kThT / 64u;
+	const uint32_t lane = threadIdx.x & 63u;
+	for (uint32_t bk = blockIdx.x * wpb + (threadIdx.x >> 6); bk < nbk; bk += gridDim.x * wpb) {
+		const uint32_t m = qf + 64u * bk + lane;
+		uint32_t c = 0; // the window's evictions before the marker's end
+		if (m < mend) {
+			const uint32_t e = mk_e[m];
+			if (e >= tend) {
+				c = nj; // kNone (never found again) included
+			} else {
+				const uint32_t eb = evc[e];
+				c = eb > j0 ? min(eb, jend) - j0 : 0u;
+			}
 		}
-		if (in) {
-			lst[c + t] = t ? lfn_apply(F[t - 1], x) : x;
-			moff[c + t] = m + (t ? S[t - 1] : 0u);
+		uint32_t S = 0, X = 0, ms = 0;
+		for (unsigned long long live = __ballot(c > 0); live; live &= live - 1) {
+			const uint32_t k = (uint32_t)__builtin_ctzll(live);
+			const uint32_t ck = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)k);
+			if (ck <= ms)
+				continue;
+			const uint32_t r = ck - ms;
+			const uint32_t i = (uint32_t)__popcll(__ballot(lane < ms && S < r + lane + 1u));
+			const uint32_t xk = r + i;
+			const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp((int)S, (int)S, 0x138, 0xf, 0xf, false); // wave_shr:1
+			S = lane > i ? sh : lane == i ? xk : S;
+			ms++;
+			if (lane == k)
+				X = xk;
 		}
-		x = lfn_apply(F[kLsT - 1], x);
-		m += S[kLsT - 1];
-		__syncthreads();
+		if (m < mend)
+			mx[m - qf] = X;
 	}
+}
+
+constexpr uint32_t kTkM = 16384; // thresholds staged in LDS at a time
+__global__ __launch_bounds__(kThT) void k_lru_take(const uint32_t* mx, uint32_t* tot, const LruCtrl* ctl, uint32_t* vict,
+		unsigned long long* cnt) {
+	if (ctl->done)
+		return;
+	const uint32_t j0 = tot[5], jend = tot[7], mend = tot[6], nev = tot[1], qf = lru_queue_front(tot, vict);
+	const uint32_t nj = jend - j0, nm = mend > qf ? mend - qf : 0u;
+	__shared__ uint32_t sx[kTkM];
+	__shared__ uint32_t s_x;
+	const uint32_t t = threadIdx.x, lane = t & 63u;
 	if (t == 0)
-		tot[0] = m; // markers, carried ones included
-}
-
-// Block-wide exclusive scan of the threads' maps (in order), by Hillis-Steele in LDS.
-__device__ __forceinline__ LFn lfn_block_excl(LFn f, LFn* F) {
-	const uint32_t t = threadIdx.x;
-	F[t] = f;
+		s_x = 0;
 	__syncthreads();
-	for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) {
-		const LFn g = t >= o ? lfn_then(F[t - o], F[t]) : F[t];
-		__syncthreads();
-		F[t] = g;
-		__syncthreads();
-	}
-	const LFn r = t ? F[t - 1] : lfn_id();
-	__syncthreads();
-	return r;
-}
-__device__ __forceinline__ uint32_t u32_block_excl(uint32_t x, uint32_t* S, uint32_t* total) {
-	const uint32_t t = threadIdx.x;
-	S[t] = x;
-	__syncthreads();
-	for (uint32_t o = 1; o < (uint32_t)kLsT; o <<= 1) {
-		const uint32_t g = t >= o ? S[t - o] + S[t] : S[t];
-		__syncthreads();
-		S[t] = g;
-		__syncthreads();
-	}
-	const uint32_t r = t ? S[t - 1] : 0u;
-	*total = S[kLsT - 1];
-	__syncthreads();
-	return r;
-}
-
-// Phase 3: each event's size before it; evt[i] = 1 where an insert finds the cache full.
-__global__ __launch_bounds__(kLsT) void k_lru_scan_apply(const uint8_t* opt, uint32_t n, uint32_t cap, const long long* lst,
-		uint8_t* evt, uint32_t* be, const LruCtrl* ctl) {
-	if (ctl->done)
-		return;
-	__shared__ LFn F[kLsT];
-	__shared__ uint32_t S[kLsT];
-	const uint32_t t = threadIdx.x;
-	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
-	LFn f = lfn_id();
-	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
-		const unsigned long long i = base + k;
-		f = lfn_then(f, lfn_op(i < n ? opt[i] : OP_NONE, cap));
-	}
-	long long x = lfn_apply(lfn_block_excl(f, F), lst[blockIdx.x]);
-	uint32_t ne = 0;
-	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
-		const unsigned long long i = base + k;
-		if (i >= n)
-			break;
-		const uint32_t op = opt[i];
-		const bool ev = op == OP_INSERT && x >= (long long)cap;
-		evt[i] = ev ? 1 : 0;
-		ne += ev ? 1u : 0u;
-		x = lfn_apply(lfn_op(op, cap), x);
-	}
-	uint32_t tot;
-	(void)u32_block_excl(ne, S, &tot);
-	if (t == 0)
-		be[blockIdx.x] = tot;
-}
-
-// Phase 4 (one workgroup): each scan block's first eviction index; tot[5] = the evictions
-// before the frontier (k_lru_compact sets it when the frontier lies inside the batch).
-__global__ __launch_bounds__(kLsT) void k_lru_scan_top2(const uint32_t* be, uint32_t nb, uint32_t* eoff, uint32_t* tot, const LruCtrl* ctl) {
-	if (ctl->done)
-		return;
-	__shared__ uint32_t S[kLsT];
-	const uint32_t t = threadIdx.x;
-	uint32_t e = 0;
-	for (uint32_t c = 0; c < nb; c += kLsT) {
-		uint32_t total;
-		const uint32_t ex = u32_block_excl(c + t < nb ? be[c + t] : 0u, S, &total);
-		if (c + t < nb)
-			eoff[c + t] = e + ex;
-		e += total;
-	}
-	if (t == 0) {
-		tot[1] = e;
-		tot[5] = e;
-	}
-}
-
-// Phase 5: the markers (event position, end) and the eviction times, in event order.
-__global__ __launch_bounds__(kLsT) void k_lru_compact(const uint8_t* opt, const uint32_t* mend, const uint8_t* evt, uint32_t n,
-		const uint32_t* moff, const uint32_t* eoff, const LruCtrl* ctl, uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* tot) {
-	if (ctl->done)
-		return;
-	const uint32_t front = ctl->front;
-	__shared__ uint32_t S[kLsT];
-	const uint32_t t = threadIdx.x;
-	const unsigned long long base = (unsigned long long)blockIdx.x * kLsBlk + (unsigned long long)t * kLsPer;
-	uint32_t nm = 0, ne = 0;
-	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
-		const unsigned long long i = base + k;
-		if (i >= n)
-			break;
-		nm += op_marks(opt[i]) ? 1u : 0u;
-		ne += evt[i];
-	}
-	uint32_t tot_;
-	uint32_t m = moff[blockIdx.x] + u32_block_excl(nm, S, &tot_);
-	uint32_t e = eoff[blockIdx.x] + u32_block_excl(ne, S, &tot_);
-	for (uint32_t k = 0; k < (uint32_t)kLsPer; k++) {
-		const unsigned long long i = base + k;
-		if (i >= n)
-			break;
-		if (i == front)
-			tot[5] = e; // evictions before the frontier
-		if (op_marks(opt[i])) {
-			mk_ref[m] = (uint32_t)i;
-			mk_e[m] = mend[i];
-			m++;
-		}
-		if (evt[i])
-			ev_t[e++] = (uint32_t)i;
-	}
-}
-
-// Phase 6 (one workgroup): the evictions of the window [front, tend), from eviction tot[5] on,
-// each take the oldest marker alive at their time.  The queue front after the evictions
-// before j is qfe[j] (kept from the round that processed them: the evictions and markers
-// before the frontier do not change), so the merge resumes there.  All threads stage the
-// markers' ends and the eviction times in LDS; wave 0 merges: one ballot per eviction gives
-// the 64-marker window's markers alive at its time, and the victim is the first of them after
-// the previous victim (a window with none moves the front on by 64).  vict[j] = eviction j's marker; tot[2] = the
-// window's end (first eviction not processed).  cnt[1] = 1: the operations are inconsistent
-// (a full cache with no victim).
-constexpr uint32_t kGrM = 8192, kGrE = 2048; // markers / evictions staged in LDS at a time
-__global__ __launch_bounds__(256) void k_lru_greedy(const uint32_t* mk_e, const uint32_t* ev_t, uint32_t* tot, const LruCtrl* ctl,
-		uint32_t* vict, uint32_t* qfe, unsigned long long* cnt) {
-	if (ctl->done)
-		return;
-	const uint32_t tend = ctl->tend;
-	__shared__ uint32_t se[kGrM], sv[kGrE];
-	__shared__ uint32_t s_qf, s_j, s_more, s_bad, s_rec;
-	const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-	const uint32_t nmk = tot[0], nev = tot[1], j0 = tot[5];
-	if (t == 0) {
-		s_qf = j0 ? qfe[j0] : 0u;
-		s_j = j0;
-		s_rec = j0; // evictions before s_rec have their front recorded
-		s_bad = 0;
-		s_more = j0 < nev;
-	}
-	__syncthreads();
-	while (s_more) {
-		const uint32_t mb = s_qf & ~63u, eb = s_j; // stage markers from the front's window, evictions from s_j
-		// 8 loads in flight per thread (a load-then-store loop waited a full latency per word)
-		for (uint32_t k0 = 0; k0 < kGrM; k0 += 256 * 8) {
-			uint32_t v[8];
+	for (uint32_t c0 = 0; c0 < nm && s_x < nj; c0 += kTkM) {
+		const uint32_t cn = min(kTkM, nm - c0);
+		for (uint32_t k0 = 0; k0 < kTkM; k0 += kThT * 16) {
+			uint32_t v[16];
 #pragma unroll
-			for (uint32_t u = 0; u < 8; u++) {
-				const uint32_t k = k0 + u * 256 + t;
-				v[u] = mb + k < nmk ? mk_e[mb + k] : 0u;
+			for (uint32_t u = 0; u < 16; u++) {
+				const uint32_t k = k0 + u * kThT + t;
+				v[u] = k < cn ? mx[c0 + k] : 0u;
 			}
 #pragma unroll
-			for (uint32_t u = 0; u < 8; u++)
-				se[k0 + u * 256 + t] = v[u];
-		}
-		{
-			uint32_t v[kGrE / 256];
-#pragma unroll
-			for (uint32_t u = 0; u < kGrE / 256; u++) {
-				const uint32_t k = u * 256 + t;
-				v[u] = eb + k < nev ? ev_t[eb + k] : ~0u;
-			}
-#pragma unroll
-			for (uint32_t u = 0; u < kGrE / 256; u++)
-				sv[u * 256 + t] = v[u];
+			for (uint32_t u = 0; u < 16; u++)
+				sx[k0 + u * kThT + t] = v[u];
 		}
 		__syncthreads();
-		if (wave == 0) {
-			uint32_t qf = s_qf, j = eb, bad = 0, restage = 0, stop = 0, rec = s_rec;
-			const uint32_t jlim = min(nev, eb + kGrE);
-			while (j < jlim && !bad && !restage && !stop) {
-				const uint32_t nj0 = min(64u, jlim - j);
-				const uint32_t tv = lane < nj0 ? sv[j - eb + lane] : ~0u;
-				const uint32_t nj = (uint32_t)__popcll(__ballot(lane < nj0 && tv < tend)); // times ascend
-				if (nj == 0) {
-					stop = 1; // the window ends at eviction j
-					break;
-				}
-				uint32_t k = 0; // evictions of the block done
-				uint32_t wb = qf & ~63u, p = qf - wb;
-				if (wb >= nmk)
-					bad = 1; // a full cache and no live marker
-				else if (wb + 64 > mb + kGrM)
-					restage = 1; // the staged markers are used up
-				if (!bad && !restage && j >= rec) { // the front before the block's first eviction
-					if (lane == 0)
-						qfe[j] = qf;
-					rec = j + 1;
-				}
-				while (k < nj && !bad && !restage) {
-					const uint32_t e = wb + lane < nmk ? se[wb - mb + lane] : 0u;
-					// most windows between the queue's front and the window end hold only dead
-					// markers: one compare at eviction k's time passes over them
-					const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)tv, (int)k);
-					if (__ballot(lane >= p && e > tk) == 0) {
-						wb += 64;
-						p = 0;
-						if (wb >= nmk) {
-							bad = 1;
-							break;
-						}
-						if (wb + 64 > mb + kGrM) {
-							restage = 1;
-							break;
-						}
-						continue;
-					}
-					// c: the block's evictions at whose times this marker is alive (e > time), a
-					// prefix of them since the times ascend: a binary search over the lanes' times
-					uint32_t c = 0;
-					for (uint32_t st = 64; st > 0; st >>= 1) {
-						const uint32_t mid = c + st;
-						const uint32_t tm = (uint32_t)__shfl((int)tv, (int)((mid - 1) & 63u), 64);
-						if (mid <= nj && tm < e)
-							c = mid;
-					}
-					if (lane < p)
-						c = 0; // taken or passed over already
-					// the greedy over the window's markers in order, in scalar registers: marker L
-					// is taken by eviction A (the evictions done so far) when it is alive then
-					unsigned long long cons = 0;
-					uint32_t A = k;
+		if (t < 64) {
+			uint32_t x = s_x;
+			for (uint32_t b = 0; b < cn && x < nj; b += 8 * 64) {
+				uint32_t xv[8];
 #pragma unroll
-					for (uint32_t L = 0; L < 64; L++) {
-						const uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)L);
-						const uint32_t take = (A - cl) >> 31; // A < cl (both at most 64): integer ops, so
-						cons |= (unsigned long long)take << L; // the chain stays in scalar registers
-						A += take;
-					}
-					// marker lane L taken by eviction a: the victim, and the front before eviction
-					// a + 1 (a later round resumes there); one scattered vector store each
-					if ((cons >> lane) & 1ull) {
-						const uint32_t a = k + __builtin_amdgcn_mbcnt_hi((uint32_t)(cons >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cons, 0));
-						vict[j + a] = wb + lane;
-						if (a + 1 < nj)
-							qfe[j + a + 1] = wb + lane + 1;
-					}
-					rec = max(rec, j + min(A + 1, nj));
-					if (A == nj) { // the block is done: the front follows its last victim
-						p = 64u - (uint32_t)__builtin_clzll(cons);
-						k = A;
-						break;
-					}
-					k = A; // every marker of the window is taken or dead: the next window
-					wb += 64;
-					p = 0;
-					if (wb >= nmk) {
-						bad = 1;
-						break;
-					}
-					if (wb + 64 > mb + kGrM) {
-						restage = 1;
-						break;
-					}
+				for (uint32_t u = 0; u < 8; u++)
+					xv[u] = sx[b + 64u * u + lane]; // past cn: 0, never taken
+#pragma unroll
+				for (uint32_t u = 0; u < 8; u++) {
+					const unsigned long long tk = __ballot(x < xv[u]);
+					if (x < xv[u])
+						vict[j0 + x + __builtin_amdgcn_mbcnt_hi((uint32_t)(tk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tk, 0))] =
+								qf + c0 + b + 64u * u + lane;
+					x += (uint32_t)__popcll(tk);
 				}
-				qf = wb + p;
-				j += k;
 			}
-			if (lane == 0) {
-				s_qf = qf;
-				s_j = j;
-				s_rec = rec;
-				s_bad = bad;
-				s_more = !bad && !stop && j < nev;
-			}
+			if (t == 0)
+				s_x = x;
 		}
 		__syncthreads();
 	}
 	if (t == 0) {
-		qfe[s_j] = s_qf; // the front after the window: where the next window resumes
-		tot[2] = s_j;
+		const uint32_t x = s_x;
+		tot[2] = j0 + x; // jend unless the markers ran out
 		cnt[0] = nev;
-		if (s_bad)
-			atomicOr((uint32_t*)&cnt[1], 1u);
+		if (x < nj)
+			atomicOr((uint32_t*)&cnt[1], 1u); // a full cache and no live marker
 	}
 }
 
-// Phase 6b: the world the evictions before the window's end imply, by event (nf_t zeroed
-// before): the victim's next find, or the victims with none (tot[4] of them) in vic.
-__global__ void k_lru_victims(const uint32_t* tot, const uint32_t* vict, const uint32_t* mk_ref, const uint32_t* mk_e,
-		const uint32_t* ev_t, uint8_t* nf_t, uint32_t* vic, uint32_t* vtot, unsigned long long* cnt, const LruCtrl* ctl) {
+// Phase 6b: the world the evictions before the window's end imply, by event in nf_t (zero
+// before): 1 at the victim's next find; for a victim with none, 2 at its session's first event
+// (evicted after its last event: not carried out), or for a carried session with no event in
+// the batch ncf (zeroed before).  Every position gets at most one of them: a marker's next
+// find follows it in its session, so it is never a batch session's first event, and only a
+// session's last marker has none.
+__global__ void k_lru_victims(Dev d, const uint32_t* tot, const uint32_t* vict, const uint32_t* mk_ref, const uint32_t* mk_e,
+		const uint32_t* ev_t, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head, uint8_t* nf_t, uint8_t* ncf,
+		unsigned long long* cnt, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
 	const uint32_t ne = tot[2];
@@ -2533,54 +2447,43 @@ __global__ void k_lru_victims(const uint32_t* tot, const uint32_t* vict, const u
 		const uint32_t q = vict[j], vr = mk_ref[q], ve = mk_e[q];
 		if (!(vr & 0x80000000u) && vr >= ev_t[j])
 			atomicOr((uint32_t*)&cnt[1], 1u); // the oldest live marker is not older than the insert
-		if (ve != kNone)
+		if (ve != kNone) {
 			nf_t[ve] = 1; // find() misses at the session's next find
-		else
-			vic[atomicAdd(vtot, 1u)] = vr;
-	}
-}
-
-// Phase 6c: the round's flags by sorted position: bit 0 from nf_t, then bit 1 (after the
-// session's last event) or the carry flag for the listed victims (ncf zeroed before).
-__global__ void k_lru_flags(Dev d, uint32_t nslow, const uint8_t* nf_t, uint8_t* nf, const LruCtrl* ctl) {
-	if (ctl->done)
-		return;
-	for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nslow; j += gridDim.x * blockDim.x)
-		nf[j] = nf_t[(uint32_t)d.slow_keys[j]];
-}
-__global__ void k_lru_tails(const uint32_t* vtot, const uint32_t* vic, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head,
-		uint8_t* nf, uint8_t* ncf, const LruCtrl* ctl) {
-	if (ctl->done)
-		return;
-	const uint32_t nv = *vtot;
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nv; k += gridDim.x * blockDim.x) {
-		const uint32_t vr = vic[k];
-		if (vr & 0x80000000u) {
+		} else if (vr & 0x80000000u) {
 			const uint32_t c = vr & 0x7fffffffu;
 			if (cm_head[c] != kNone)
-				nf[cm_head[c]] |= 2u;
+				nf_t[(uint32_t)d.slow_keys[cm_head[c]]] = 2;
 			else
 				ncf[c] = 1;
 		} else {
-			nf[head[jpos[vr]]] |= 2u; // after the session's last event: not carried out
+			nf_t[(uint32_t)d.slow_keys[head[jpos[vr]]]] = 2;
 		}
 	}
 }
 
-// Phase 7: how many flags the round changed (cnt[2]), the first event whose eviction bit
-// changed (cnt[3]: the new frontier), and where each session's walk must start again (cpos).
-__global__ void k_lru_diff(const uint8_t* f, const uint8_t* nf, uint32_t n1, const uint8_t* cf, const uint8_t* ncf, uint32_t n2,
-		const unsigned long long* keys, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt, const LruCtrl* ctl) {
+// Phase 7: the round's flags by sorted position (nf, from nf_t, which is cleared behind the
+// read: every position nf_t can hold is a session event), how many flags changed (cnt[2],
+// carried ones included), the first event whose eviction bit changed (cnt[3]: the new
+// frontier), and where each session's walk must start again (cpos).
+__global__ void k_lru_flags(Dev d, uint32_t nslow, uint8_t* nf_t, const uint8_t* f, uint8_t* nf, const uint8_t* cf, const uint8_t* ncf,
+		uint32_t ncc, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
 	uint32_t x = 0, first = kNone;
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n1 + n2; k += gridDim.x * blockDim.x) {
-		const bool dk = k < n1 ? (f[k] != nf[k]) : (cf[k - n1] != ncf[k - n1]);
-		x += dk ? 1u : 0u;
-		if (k < n1 && ((f[k] ^ nf[k]) & 1u)) { // the walk changes only with bit 0
-			atomicMin(&cpos[head[k]], k); // its session walks again from here
-			const uint32_t tk = (uint32_t)keys[k];
-			first = tk < first ? tk : first;
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nslow + ncc; k += gridDim.x * blockDim.x) {
+		if (k < nslow) {
+			const uint32_t i = (uint32_t)d.slow_keys[k];
+			const uint8_t v = nf_t[i], o = f[k];
+			if (v)
+				nf_t[i] = 0;
+			nf[k] = v;
+			x += o != v ? 1u : 0u;
+			if ((o ^ v) & 1u) { // the walk changes only with bit 0
+				atomicMin(&cpos[head[k]], k); // its session walks again from here
+				first = i < first ? i : first;
+			}
+		} else {
+			x += cf[k - nslow] != ncf[k - nslow] ? 1u : 0u;
 		}
 	}
 	if (__any(x != 0))
@@ -3681,7 +3584,7 @@ hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipS
 			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cpos, 0xff, (size_t)nslow * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.opt, 0, d.n, st)) != hipSuccess || (e = hipMemsetAsync(w.f[0], 0, nslow, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess)
+			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess || (e = hipMemsetAsync(w.nf_t, 0, d.n, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.jpos, w.head);
@@ -3697,20 +3600,18 @@ hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipS
 // where flags changed or the last walk stopped), then the world the evictions before the
 // horizon imply in nf / ncf; cnt[1] inconsistency, cnt[2] flags changed, cnt[3] the new
 // frontier.
-// A round's counters: the walk list (tot[3]), the victims listed (tot[4]), and cnt (evictions,
-// inconsistency, flags changed, first changed event).
-__global__ void k_lru_round_reset(uint32_t* tot, unsigned long long* cnt, const LruCtrl* ctl) {
-	if (threadIdx.x == 0 && !ctl->done) {
-		tot[3] = tot[4] = 0;
-		cnt[0] = cnt[1] = cnt[2] = 0;
-		cnt[3] = ~0ull;
-	}
+// A round's counters (the walk list tot[3]; cnt: evictions, inconsistency, flags changed,
+// first changed event), cleared for the next round by k_lru_advance / k_lru_ctl_init.
+__device__ __forceinline__ void lru_round_reset(uint32_t* tot, unsigned long long* cnt) {
+	tot[3] = 0;
+	cnt[0] = cnt[1] = cnt[2] = 0;
+	cnt[3] = ~0ull;
 }
 
 // The end of a round (one thread): the world derived is the world walked up to the batch's
 // end -> settled in world cur; an inconsistent world -> done, not settled (the one-lane replay
 // takes the batch); else the frontier moves past every event the round settled.
-__global__ void k_lru_advance(LruCtrl* ctl, const unsigned long long* cnt, uint32_t window, uint32_t n, uint32_t cur) {
+__global__ void k_lru_advance(LruCtrl* ctl, unsigned long long* cnt, uint32_t* tot, uint32_t window, uint32_t n, uint32_t cur) {
 	if (threadIdx.x != 0 || ctl->done)
 		return;
 	ctl->rounds++;
@@ -3725,7 +3626,7 @@ __global__ void k_lru_advance(LruCtrl* ctl, const unsigned long long* cnt, uint3
 		ctl->done = 1;
 		ctl->settled = 1;
 		ctl->cur_final = cur;
-		return;
+		return; // cnt[0] (the evictions) stays for the host
 	}
 	unsigned long long front = ctl->front;
 	if (changed == 0)
@@ -3735,50 +3636,47 @@ __global__ void k_lru_advance(LruCtrl* ctl, const unsigned long long* cnt, uint3
 	const unsigned long long tend = front + window;
 	ctl->front = (uint32_t)front;
 	ctl->tend = (uint32_t)(tend < 0xffffffffull ? tend : 0xffffffffull);
+	lru_round_reset(tot, cnt);
 }
 
-__global__ void k_lru_ctl_init(LruCtrl* ctl, uint32_t window) {
+// bs[0]: the batch starts with the carried sessions in the LRU (and their markers first).
+__global__ void k_lru_ctl_init(LruCtrl* ctl, uint32_t window, uint32_t* tot, unsigned long long* cnt, LsState* bs, uint32_t nc) {
 	if (threadIdx.x == 0) {
 		ctl->front = 0;
 		ctl->tend = window;
 		ctl->done = ctl->settled = ctl->cur_final = ctl->rounds = 0;
+		lru_round_reset(tot, cnt);
+		bs[0] = LsState{(int)nc, nc, 0u, 0u};
 	}
 }
 
-hipError_t launch_lru_ctl_init(const LruRound& w, uint32_t window, hipStream_t st) {
-	hipLaunchKernelGGL(k_lru_ctl_init, dim3(1), dim3(64), 0, st, w.ctl, window);
+hipError_t launch_lru_ctl_init(const Dev& d, const LruRound& w, uint32_t window, hipStream_t st) {
+	hipLaunchKernelGGL(k_lru_ctl_init, dim3(1), dim3(64), 0, st, w.ctl, window, w.tot, w.cnt, w.bs, d.n_carry_in);
 	return hipGetLastError();
 }
 
 hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t window, hipStream_t st, int cus) {
-	const uint32_t n = d.n, nb = (n + kLsBlk - 1) / kLsBlk, nc = d.n_carry_in;
+	const uint32_t n = d.n;
 	const uint8_t* f = w.f[cur];
 	uint8_t* nf = w.f[cur ^ 1];
 	const uint8_t* cf = w.cf[cur];
 	uint8_t* ncf = w.cf[cur ^ 1];
 	const LruCtrl* ctl = w.ctl;
-	hipLaunchKernelGGL(k_lru_round_reset, dim3(1), dim3(64), 0, st, w.tot, w.cnt, ctl);
-	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, ctl, w.rlist, w.tot);
+	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, ctl, w.rlist, w.tot, ncf,
+			d.carry_cap);
 	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
 			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, ctl}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
-	hipLaunchKernelGGL(k_lru_scan_part, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (LFn*)w.bf, w.bm, w.nf_t, ctl);
-	hipLaunchKernelGGL(k_lru_scan_top, dim3(1), dim3(kLsT), 0, st, (const LFn*)w.bf, (const uint32_t*)w.bm, nb, (long long)nc, nc, w.lst,
-			w.moff, w.tot, ncf, d.carry_cap, ctl);
-	hipLaunchKernelGGL(k_lru_scan_apply, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, n, d.carry_cap, (const long long*)w.lst,
-			w.evt, w.be, ctl);
-	hipLaunchKernelGGL(k_lru_scan_top2, dim3(1), dim3(kLsT), 0, st, (const uint32_t*)w.be, nb, w.eoff, w.tot, ctl);
-	hipLaunchKernelGGL(k_lru_compact, dim3(nb), dim3(kLsT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, (const uint8_t*)w.evt, n,
-			(const uint32_t*)w.moff, (const uint32_t*)w.eoff, ctl, w.mk_ref, w.mk_e, w.ev_t, w.tot);
-	hipLaunchKernelGGL(k_lru_greedy, dim3(1), dim3(256), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.tot, ctl, w.vict,
-			w.qfe, w.cnt);
-	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
-			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, w.nf_t, w.vic, w.tot + 4, w.cnt, ctl);
-	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, (const uint8_t*)w.nf_t, nf, ctl);
-	hipLaunchKernelGGL(k_lru_tails, dim3(cus), dim3(256), 0, st, (const uint32_t*)(w.tot + 4), (const uint32_t*)w.vic, (const uint32_t*)w.jpos,
-			(const uint32_t*)w.head, (const uint32_t*)w.cm_head, nf, ncf, ctl);
-	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(nslow + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, f, (const uint8_t*)nf, nslow, cf,
-			(const uint8_t*)ncf, d.carry_cap, (const unsigned long long*)d.slow_keys, (const uint32_t*)w.head, w.cpos, w.cnt, ctl);
-	hipLaunchKernelGGL(k_lru_advance, dim3(1), dim3(64), 0, st, w.ctl, (const unsigned long long*)w.cnt, window, n, (uint32_t)cur);
+	hipLaunchKernelGGL(k_lru_scan, dim3(1), dim3(kScT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, n, d.carry_cap, w.bs,
+			w.mk_ref, w.mk_e, w.ev_t, w.evc, w.tot, ctl);
+	hipLaunchKernelGGL(k_lru_thresh, dim3(cus), dim3(kThT), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.evc, (const uint32_t*)w.tot,
+			ctl, (const uint32_t*)w.vict, w.mx);
+	hipLaunchKernelGGL(k_lru_take, dim3(1), dim3(kThT), 0, st, (const uint32_t*)w.mx, w.tot, ctl, w.vict, w.cnt);
+	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, d, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
+			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, (const uint32_t*)w.jpos, (const uint32_t*)w.head,
+			(const uint32_t*)w.cm_head, w.nf_t, ncf, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow + d.carry_cap, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.nf_t, f, nf, cf,
+			(const uint8_t*)ncf, d.carry_cap, (const uint32_t*)w.head, w.cpos, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_advance, dim3(1), dim3(64), 0, st, w.ctl, w.cnt, w.tot, window, n, (uint32_t)cur);
 	return hipGetLastError();
 }
 // The final walk of the exact path in the converged world (with output), then the carried
@@ -3791,6 +3689,7 @@ hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, con
 	return hipGetLastError();
 }
 size_t lru_scan_blocks(uint32_t n) { return (n + kLsBlk - 1) / kLsBlk; }
+int lru_size_limit() { return kLInf / 2; }
 hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
 	hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, (const uint8_t*)nullptr);
 	return hipGetLastError();

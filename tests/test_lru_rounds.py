@@ -195,3 +195,69 @@ def test_rounds_settle_quickly_on_a_keepalive_trace():
     ops, nev, _, r = rounds(ev, car, 100)
     assert ops == want_ops and nev == want_ev
     assert want_ev > 1000 and r < 50
+
+
+def merge_queue(ends, times):
+    """derive()'s merge: each eviction time takes the first untaken marker alive then."""
+    vict, q = [], 0
+    for t in times:
+        while q < len(ends) and not ends[q] > t:
+            q += 1
+        if q == len(ends):
+            return vict, False
+        vict.append(q)
+        q += 1
+    return vict, True
+
+
+def merge_thresholds(ends, times, block=64):
+    """k_lru_thresh + k_lru_take: c_m = evictions before the marker's end; per block of markers
+    the thresholds X_k = min{x : x + #{k' < k : x < X_k'} >= c_k} (searched in [c_k - k, c_k]);
+    the blocks chained by A += #{k : A < X_k}, marker k taken by eviction A + rank.  X_k as the
+    kernel finds it: the (c_k - ms)-th positive integer missing from the sorted positive
+    thresholds S so far, r + #{j : S_j - j < r} (1-based j), or 0 when c_k <= ms; the binary
+    search over [c_k - k, c_k] is the definition it is checked against."""
+    import bisect
+    nj = len(times)
+    X = []
+    for b0 in range(0, len(ends), block):
+        xs, S = [], []
+        for k, e in enumerate(ends[b0:b0 + block]):
+            c = bisect.bisect_left(times, e)
+            lo, hi = max(0, c - k), c
+            while lo < hi:
+                mid = (lo + hi) // 2
+                if mid + sum(1 for x in xs if x > mid) >= c:
+                    hi = mid
+                else:
+                    lo = mid + 1
+            want = lo if c > 0 else 0
+            r = c - len(S)
+            x = r + sum(1 for j, sj in enumerate(S, 1) if sj - j < r) if r > 0 else 0
+            assert x == want
+            if x:
+                bisect.insort(S, x)
+            xs.append(x)
+        X += xs
+    vict, A = [None] * nj, 0
+    for b0 in range(0, len(ends), block):
+        taken = [b0 + k for k, x in enumerate(X[b0:b0 + block]) if A < x]
+        for r, m in enumerate(taken):
+            vict[A + r] = m
+        A += len(taken)
+    return vict[:A], A == nj
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_threshold_merge_equals_the_queue_merge(seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 700))
+    ends = [int(x) for x in rng.integers(0, 2000, n)]
+    if seed % 3 == 0:
+        ends = [e if rng.random() < 0.5 else 1 << 30 for e in ends]  # never found again
+    times = sorted(int(x) for x in rng.choice(2000, int(rng.integers(0, 400)), replace=False))
+    want, ok = merge_queue(ends, times)
+    got, ok2 = merge_thresholds(ends, times, block=int(rng.choice([1, 3, 64])))
+    assert ok == ok2
+    if ok:
+        assert got == want
