@@ -362,6 +362,8 @@ static void ctx_free(ebd_ctx* c) {
 		(void)hipHostFree(c->h_end);
 	if (c->lr_mem)
 		(void)hipFree(c->lr_mem);
+	if (c->lr.stat)
+		(void)hipFree(c->lr.stat);
 	if (c->h_lr)
 		(void)hipHostFree(c->h_lr);
 	for (int k = 0; k < 2; k++) {
@@ -623,7 +625,7 @@ static int lru_alloc(ebd_ctx* c) {
 			{(void**)&w.ev_t, 4 * n}, {(void**)&w.evc, 4 * n}, {(void**)&w.cm_end, 4 * cc}, {(void**)&w.cm_head, 4 * cc},
 			{(void**)&w.f[0], n}, {(void**)&w.f[1], n}, {(void**)&w.cf[0], cc}, {(void**)&w.cf[1], cc}, {(void**)&w.bs, sizeof(LsState) * (nb + 1)},
 			{(void**)&w.ctl, sizeof(LruCtrl)}, {(void**)&w.tot, 32}, {(void**)&w.jpos, 4 * n}, {(void**)&w.head, 4 * n}, {(void**)&w.cnt, 32},
-			{(void**)&w.nf_t, n}, {(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
+			{(void**)&w.cpos, 4 * n}, {(void**)&w.rlist, 4 * n}, {(void**)&w.vict, 4 * (n + 1)},
 			{(void**)&w.mx, 4 * (n + cc + 64)}, {(void**)&w.wto, 4 * n}, {(void**)&w.snap, sess_state_bytes() * n}};
 	size_t total = 0;
 	for (const Part& q : parts)
@@ -670,6 +672,10 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	// chunk: no host round trip per round (a settled chunk's remaining rounds exit at once).
 	constexpr int kRoundChunk = 8;
 	HIP_TRY(launch_lru_ctl_init(d, w, window, c->stream));
+	if (lru_trace && !w.stat) {
+		HIP_TRY(hipMalloc(&w.stat, 8 * sizeof(unsigned long long)));
+		HIP_TRY(hipMemsetAsync(w.stat, 0, 8 * sizeof(unsigned long long), c->stream));
+	}
 	LruCtrl* h = (LruCtrl*)c->h_lr;
 	static_assert(sizeof(LruCtrl) <= 8 * sizeof(unsigned long long), "the control word fits the host read buffer");
 	int r = 0;
@@ -685,6 +691,12 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 			break;
 	}
 	c->lru_rounds += h->rounds;
+	if (lru_trace) {
+		unsigned long long sv[8];
+		HIP_TRY(hipMemcpy(sv, w.stat, sizeof(sv), hipMemcpyDeviceToHost));
+		std::fprintf(stderr, "ebd lru walks (cumulative): %llu rounds, sessions %llu, events %llu, bytes %llu, longest lane's bytes summed %llu\n",
+				(unsigned long long)c->lru_rounds, sv[4], sv[0], sv[1], sv[2]);
+	}
 	if (!h->done || !h->settled)
 		return 0;
 	*settled = 1;

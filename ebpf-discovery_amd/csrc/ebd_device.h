@@ -152,20 +152,20 @@ struct LruRound {
 	uint32_t* evc;   // per event: the evictions before it
 	uint32_t* cm_end;
 	uint32_t* cm_head;
-	uint8_t* f[2];
-	uint8_t* cf[2];
+	uint8_t* f[2];   // the worlds walked / derived, by event (bit 0 evicted before it, bit 1 after the session's last)
+	uint8_t* cf[2];  // by carried session: evicted with no event in the batch
 	LsState* bs;     // per scan block: its start state
 	uint32_t* tot; // 1 evictions (to the span's end), 2 window end, 3 next walk list, 5 evictions before the frontier, 6 markers born before the horizon, 7 evictions before it
 	uint32_t* jpos;
 	uint32_t* head;
 	unsigned long long* cnt;
-	uint8_t* nf_t; // the round's eviction flags by event
 	uint32_t* vict; // per eviction: its victim marker
 	uint32_t* mx;   // per marker from the round's queue front: its threshold (k_lru_thresh)
 	uint32_t* cpos;  // per session (first sorted position): its first changed position, kNone
 	uint32_t* rlist; // the round's walks: start positions
 	uint32_t* wto;   // per session: where its last walk stopped (kNone: at its end)
 	void* snap;      // per sorted position: the session's state before it (SessState)
+	unsigned long long* stat; // EBD_LRU_TRACE only (else null): the walks' statistics, k_walk<true> / k_lru_advance
 };
 
 struct Dev {

@@ -1598,9 +1598,9 @@ __device__ __forceinline__ void session_carry_out(const Dev& d, const SessState&
 
 // The parallel session path: one lane per session (k_walk_heads lists them), events in
 // order.  Exact while no LRU eviction can happen (run_batch checks an upper bound of the
-// live sessions first), or with the evictions the exact-LRU rounds derived: evf[j] bit 0 =
-// the session was evicted before its event j (it parses that buffer as a new session), bit 1
-// at a session's first position = evicted after its last event (not carried out).  DRY (the
+// live sessions first), or with the evictions the exact-LRU rounds derived, by event: evf[i]
+// bit 0 = the session was evicted before its event i (it parses that buffer as a new
+// session), bit 1 at a session's first event = evicted after its last event (not carried out).  DRY (the
 // rounds' walks): no outputs, only each event's LRU operation in ops[j].  The header-key trie
 // and the byte classes sit in LDS: the walk reads them once per byte.
 // The exact-LRU rounds' walks (DRY): a list entry is the sorted position a session's walk
@@ -1614,6 +1614,7 @@ struct DryWalk {
 	uint32_t* wto;
 	uint8_t* opt;
 	const LruCtrl* ctl;   // the round's horizon (ctl->tend); nothing to do once ctl->done
+	unsigned long long* stat; // EBD_LRU_TRACE: events and bytes walked, the longest lane's bytes (summed over rounds)
 };
 
 template <bool DRY>
@@ -1654,6 +1655,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
 	unsigned long long pf_off = 0;
 	uint32_t inserts = 0; // CTR_INSERTS: one atomic per wave when it ends
+	uint32_t st_ev = 0, st_by = 0; // DRY with dw.stat: this lane's events and bytes walked
 	for (;;) {
 		const unsigned long long busy = __ballot(in_ev), wait = __ballot(!in_ev && (ended || h < nh));
 		if (busy == 0 && wait == 0)
@@ -1713,12 +1715,16 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 							continue;
 						}
 					}
-					if (evf && (evf[jj] & 1u))
+					if (evf && (evf[i] & 1u))
 						S.live = 0; // evicted since its previous event: find() misses
 					if (ev_begin(d, S, jj, i, fl, L, off, e)) {
 						dfa_walk_load(S.g, A[S.g.ds], w);
 						pos0 = w.pos;
 						ne = dfa_allow(pos0, e.L);
+						if (DRY) {
+							st_ev++;
+							st_by += ne;
+						}
 						const uintptr_t p = (uintptr_t)(d.payload + off);
 						b0 = p & ~(uintptr_t)15;
 						k0 = (uint32_t)(p & 15u);
@@ -1738,7 +1744,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 					}
 					jj++;
 				} else {
-					if (!DRY && S.live && !(evf && (evf[jhead] & 2u)))
+					if (!DRY && S.live && !(evf && (evf[slow_event(d, jhead)] & 2u)))
 						session_carry_out(d, S, jhead, jj - 1);
 					if (DRY)
 						dw.wto[jhead] = kNone; // walked to its end
@@ -1770,6 +1776,18 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 			inserts += __shfl_xor(inserts, o, 64);
 		if ((threadIdx.x & 63) == 0 && inserts)
 			atomicAdd(&d.ctr[CTR_INSERTS], (unsigned long long)inserts);
+	} else if (dw.stat) {
+		uint32_t mx = st_by;
+		for (int o = 32; o > 0; o >>= 1) {
+			st_ev += __shfl_xor(st_ev, o, 64);
+			st_by += __shfl_xor(st_by, o, 64);
+			mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+		}
+		if ((threadIdx.x & 63) == 0) {
+			atomicAdd(&dw.stat[0], (unsigned long long)st_ev);
+			atomicAdd(&dw.stat[1], (unsigned long long)st_by);
+			atomicMax(&dw.stat[3], (unsigned long long)mx);
+		}
 	}
 }
 
@@ -2182,43 +2200,69 @@ __device__ __forceinline__ LsSpan lru_span(const LruCtrl* ctl, uint32_t n) {
 	return LsSpan{first, last};
 }
 
-// Phases 1-5 in one workgroup, block by block over the span (about window / kLsBlk + 1 of
-// them): the LRU's size before each event (maps x -> min(a, x + b) scanned in event order, from
-// the block's start state), the evictions (an insert that finds the cache full), and the
-// markers (event, end) and eviction times in order, numbered on from the block's start
-// state; evc[i] = the evictions before event i.  bs[b + 1] = the state after block b.
-// tot[5] = the evictions before the frontier, tot[6] / tot[7] = the markers / evictions
-// before the horizon, tot[1] = the evictions up to the span's end.
+// Phases 1-5 in one workgroup over the span (about window / kLsBlk + 1 blocks), up to
+// kScChunk blocks per pass, each thread a run of consecutive events: the LRU's size before
+// each event (maps x -> min(a, x + b) scanned in event order from the span's start state), the
+// evictions (an insert that finds the cache full), and the markers (event, end) and eviction
+// times in order, numbered on from the start state; evc[i] = the evictions before event i;
+// bs[b] = the state at each block start passed.  tot[5] = the evictions before the frontier,
+// tot[6] / tot[7] = the markers / evictions before the horizon, tot[1] = the evictions up to
+// the span's end.  The outputs gather in LDS and leave in coalesced rows (one workgroup's
+// scattered 4-byte stores were what the kernel spent its time on).
+constexpr uint32_t kScChunk = 2, kScEv = kScChunk * kLsBlk; // events per pass
 __device__ __forceinline__ LFn lfn_shfl_up(LFn f, uint32_t o) { return LFn{__shfl_up(f.a, o, 64), __shfl_up(f.b, o, 64)}; }
 __global__ __launch_bounds__(kScT) void k_lru_scan(const uint8_t* opt, const uint32_t* mend, uint32_t n, uint32_t cap, LsState* bs,
 		uint32_t* mk_ref, uint32_t* mk_e, uint32_t* ev_t, uint32_t* evc, uint32_t* tot, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
-	constexpr uint32_t kW = kScT / 64;
+	constexpr uint32_t kW = kScT / 64, kPer = kScPer * kScChunk;
 	const LsSpan sp = lru_span(ctl, n);
 	const uint32_t front = ctl->front, tend = ctl->tend;
-	__shared__ LFn wf[kW];
-	__shared__ uint32_t wm[kW], we[kW];
+	// one LDS object: [evc | marker events | marker ends | eviction times] of a pass, then the
+	// waves' totals
+	__shared__ uint32_t lds[4 * kScEv + 4 * kW];
+	uint32_t* s_evc = lds;
+	uint32_t* s_mref = lds + kScEv;
+	uint32_t* s_me = lds + 2 * kScEv;
+	uint32_t* s_ev = lds + 3 * kScEv;
+	LFn* wf = (LFn*)(lds + 4 * kScEv);
+	uint32_t* wm = lds + 4 * kScEv + 2 * kW;
+	uint32_t* we = lds + 4 * kScEv + 3 * kW;
 	const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
 	LsState st = bs[sp.first];
-	for (uint32_t blk = sp.first; blk <= sp.last; blk++) {
-		const uint32_t i0 = blk * kLsBlk + t * kScPer;
-		uint32_t ops4 = 0; // OP_NONE past the batch
-		if (i0 + kScPer <= n) {
-			ops4 = *(const uint32_t*)(opt + i0);
-		} else {
-			for (uint32_t k = 0; k < kScPer; k++)
-				if (i0 + k < n)
-					ops4 |= (uint32_t)opt[i0 + k] << (8 * k);
+	for (uint32_t b0 = sp.first; b0 <= sp.last; b0 += kScChunk) {
+		const uint32_t nbk = min(kScChunk, sp.last + 1 - b0), per = kScPer * nbk; // events per thread
+		const uint32_t ib = b0 * kLsBlk, i0 = ib + t * per;
+		uint32_t ow[kScChunk]; // the thread's operations, 4 per word (OP_NONE past the batch)
+#pragma unroll
+		for (uint32_t q = 0; q < kScChunk; q++) {
+			const uint32_t iq = i0 + 4 * q;
+			ow[q] = 0;
+			if (q < nbk) {
+				if (iq + 4 <= n) {
+					ow[q] = *(const uint32_t*)(opt + iq);
+				} else {
+					for (uint32_t k = 0; k < 4; k++)
+						if (iq + k < n)
+							ow[q] |= (uint32_t)opt[iq + k] << (8 * k);
+				}
+			}
 		}
+		// the markers' ends (loads in flight across the scans)
+		uint32_t me[kPer];
+#pragma unroll
+		for (uint32_t k = 0; k < kPer; k++)
+			me[k] = k < per && i0 + k < n && op_marks((ow[k >> 2] >> (8 * (k & 3u))) & 0xffu) ? mend[i0 + k] : 0u;
 		LFn f = lfn_id();
 		uint32_t mk = 0;
 #pragma unroll
-		for (uint32_t k = 0; k < kScPer; k++) {
-			const uint32_t op = (ops4 >> (8 * k)) & 0xffu;
-			f = lfn_then(f, lfn_op(op, cap));
-			mk += op_marks(op) ? 1u : 0u;
-		}
+		for (uint32_t q = 0; q < kScChunk; q++)
+#pragma unroll
+			for (uint32_t k = 0; k < 4; k++) {
+				const uint32_t op = (ow[q] >> (8 * k)) & 0xffu;
+				f = lfn_then(f, lfn_op(op, cap));
+				mk += op_marks(op) ? 1u : 0u;
+			}
 		LFn fi = f; // inclusive over the wave
 		uint32_t mi = mk;
 #pragma unroll
@@ -2236,27 +2280,30 @@ __global__ __launch_bounds__(kScT) void k_lru_scan(const uint8_t* opt, const uin
 		}
 		__syncthreads();
 		LFn pre = lfn_id();
-		uint32_t m = st.m;
+		uint32_t ml = 0; // markers of the pass before the thread's
 		for (uint32_t w = 0; w < wv; w++) {
 			pre = lfn_then(pre, wf[w]);
-			m += wm[w];
+			ml += wm[w];
 		}
 		const LFn fx = lfn_shfl_up(fi, 1);
 		const uint32_t mx_ = __shfl_up(mi, 1, 64);
 		if (lane) {
 			pre = lfn_then(pre, fx);
-			m += mx_;
+			ml += mx_;
 		}
-		int x = lfn_apply(pre, st.x);
-		uint32_t evs = 0, ne = 0;
+		const int x0 = lfn_apply(pre, st.x);
+		int x = x0;
+		uint32_t evs = 0, ne = 0; // the thread's evictions, bit k = its event k
 #pragma unroll
-		for (uint32_t k = 0; k < kScPer; k++) {
-			const uint32_t op = (ops4 >> (8 * k)) & 0xffu;
-			const bool ev = op == OP_INSERT && x >= (int)cap;
-			evs |= (ev ? 1u : 0u) << k;
-			ne += ev ? 1u : 0u;
-			x = lfn_apply(lfn_op(op, cap), x);
-		}
+		for (uint32_t q = 0; q < kScChunk; q++)
+#pragma unroll
+			for (uint32_t k = 0; k < 4; k++) {
+				const uint32_t op = (ow[q] >> (8 * k)) & 0xffu;
+				const bool ev = op == OP_INSERT && x >= (int)cap;
+				evs |= (ev ? 1u : 0u) << (4 * q + k);
+				ne += ev ? 1u : 0u;
+				x = lfn_apply(lfn_op(op, cap), x);
+			}
 		uint32_t ni = ne;
 #pragma unroll
 		for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -2267,38 +2314,55 @@ __global__ __launch_bounds__(kScT) void k_lru_scan(const uint8_t* opt, const uin
 		if (lane == 63)
 			we[wv] = ni;
 		__syncthreads();
-		uint32_t e = st.e + ni - ne;
+		uint32_t el = ni - ne; // evictions of the pass before the thread's
 		for (uint32_t w = 0; w < wv; w++)
-			e += we[w];
-		for (uint32_t k = 0; k < kScPer; k++) {
+			el += we[w];
+		x = x0;
+#pragma unroll
+		for (uint32_t k = 0; k < kPer; k++) {
 			const uint32_t i = i0 + k;
-			if (i >= n)
-				break;
+			if (k >= per || i >= n)
+				continue;
+			const uint32_t op = (ow[k >> 2] >> (8 * (k & 3u))) & 0xffu;
+			if ((i & (kLsBlk - 1u)) == 0)
+				bs[i / kLsBlk] = LsState{x, st.m + ml, st.e + el, 0u}; // a block start: a later round may start there
 			if (i == front)
-				tot[5] = e;
+				tot[5] = st.e + el;
 			if (i == tend) {
-				tot[6] = m;
-				tot[7] = e;
+				tot[6] = st.m + ml;
+				tot[7] = st.e + el;
 			}
-			evc[i] = e;
-			if (op_marks((ops4 >> (8 * k)) & 0xffu)) {
-				mk_ref[m] = i;
-				mk_e[m] = mend[i];
-				m++;
+			s_evc[i - ib] = st.e + el;
+			if (op_marks(op)) {
+				s_mref[ml] = i;
+				s_me[ml] = me[k];
+				ml++;
 			}
 			if ((evs >> k) & 1u)
-				ev_t[e++] = i;
+				s_ev[el++] = i;
+			x = lfn_apply(lfn_op(op, cap), x);
 		}
 		LFn tf = lfn_id();
+		uint32_t pm = 0, pe = 0;
 		for (uint32_t w = 0; w < kW; w++) {
 			tf = lfn_then(tf, wf[w]);
-			st.m += wm[w];
-			st.e += we[w];
+			pm += wm[w];
+			pe += we[w];
 		}
+		__syncthreads();
+		const uint32_t nev_pass = min(nbk * kLsBlk, n - ib);
+		for (uint32_t k = t; k < nev_pass; k += kScT)
+			evc[ib + k] = s_evc[k];
+		for (uint32_t k = t; k < pm; k += kScT) {
+			mk_ref[st.m + k] = s_mref[k];
+			mk_e[st.m + k] = s_me[k];
+		}
+		for (uint32_t k = t; k < pe; k += kScT)
+			ev_t[st.e + k] = s_ev[k];
 		st.x = lfn_apply(tf, st.x);
-		if (t == 0)
-			bs[blk + 1] = st;
-		__syncthreads(); // wf / wm / we are reused
+		st.m += pm;
+		st.e += pe;
+		__syncthreads(); // the LDS is reused
 	}
 	if (t == 0) {
 		if (tend >= n) {
@@ -2431,14 +2495,14 @@ __global__ __launch_bounds__(kThT) void k_lru_take(const uint32_t* mx, uint32_t*
 	}
 }
 
-// Phase 6b: the world the evictions before the window's end imply, by event in nf_t (zero
+// Phase 6b: the world the evictions before the window's end imply, by event in nf (zero
 // before): 1 at the victim's next find; for a victim with none, 2 at its session's first event
 // (evicted after its last event: not carried out), or for a carried session with no event in
 // the batch ncf (zeroed before).  Every position gets at most one of them: a marker's next
 // find follows it in its session, so it is never a batch session's first event, and only a
 // session's last marker has none.
 __global__ void k_lru_victims(Dev d, const uint32_t* tot, const uint32_t* vict, const uint32_t* mk_ref, const uint32_t* mk_e,
-		const uint32_t* ev_t, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head, uint8_t* nf_t, uint8_t* ncf,
+		const uint32_t* ev_t, const uint32_t* jpos, const uint32_t* head, const uint32_t* cm_head, uint8_t* nf, uint8_t* ncf,
 		unsigned long long* cnt, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
@@ -2448,42 +2512,58 @@ __global__ void k_lru_victims(Dev d, const uint32_t* tot, const uint32_t* vict, 
 		if (!(vr & 0x80000000u) && vr >= ev_t[j])
 			atomicOr((uint32_t*)&cnt[1], 1u); // the oldest live marker is not older than the insert
 		if (ve != kNone) {
-			nf_t[ve] = 1; // find() misses at the session's next find
+			nf[ve] = 1; // find() misses at the session's next find
 		} else if (vr & 0x80000000u) {
 			const uint32_t c = vr & 0x7fffffffu;
 			if (cm_head[c] != kNone)
-				nf_t[(uint32_t)d.slow_keys[cm_head[c]]] = 2;
+				nf[(uint32_t)d.slow_keys[cm_head[c]]] = 2;
 			else
 				ncf[c] = 1;
 		} else {
-			nf_t[(uint32_t)d.slow_keys[head[jpos[vr]]]] = 2;
+			nf[(uint32_t)d.slow_keys[head[jpos[vr]]]] = 2;
 		}
 	}
 }
 
-// Phase 7: the round's flags by sorted position (nf, from nf_t, which is cleared behind the
-// read: every position nf_t can hold is a session event), how many flags changed (cnt[2],
-// carried ones included), the first event whose eviction bit changed (cnt[3]: the new
-// frontier), and where each session's walk must start again (cpos).
-__global__ void k_lru_flags(Dev d, uint32_t nslow, uint8_t* nf_t, const uint8_t* f, uint8_t* nf, const uint8_t* cf, const uint8_t* ncf,
-		uint32_t ncc, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt, const LruCtrl* ctl) {
+// Phase 7 (by event, coalesced): how many flags the round changed (cnt[2], carried ones
+// included), the first event whose eviction bit changed (cnt[3]: the new frontier), and where
+// each session's walk must start again (cpos).  The walked world f is cleared behind the read:
+// it is the next round's zeroed target.
+__global__ void k_lru_diff(uint32_t n, uint8_t* f, const uint8_t* nf, const uint8_t* cf, const uint8_t* ncf, uint32_t ncc,
+		const uint32_t* jpos, const uint32_t* head, uint32_t* cpos, unsigned long long* cnt, const LruCtrl* ctl) {
 	if (ctl->done)
 		return;
 	uint32_t x = 0, first = kNone;
-	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nslow + ncc; k += gridDim.x * blockDim.x) {
-		if (k < nslow) {
-			const uint32_t i = (uint32_t)d.slow_keys[k];
-			const uint8_t v = nf_t[i], o = f[k];
-			if (v)
-				nf_t[i] = 0;
-			nf[k] = v;
-			x += o != v ? 1u : 0u;
-			if ((o ^ v) & 1u) { // the walk changes only with bit 0
-				atomicMin(&cpos[head[k]], k); // its session walks again from here
-				first = i < first ? i : first;
+	const uint32_t n4 = n / 4u;
+	for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n4 + ncc; q += gridDim.x * blockDim.x) {
+		if (q < n4) {
+			const uint32_t o4 = ((const uint32_t*)f)[q], v4 = ((const uint32_t*)nf)[q];
+			if (o4)
+				((uint32_t*)f)[q] = 0;
+			if (o4 == v4)
+				continue;
+			for (uint32_t k = 0; k < 4; k++) {
+				const uint32_t o = (o4 >> (8 * k)) & 0xffu, v = (v4 >> (8 * k)) & 0xffu, i = 4 * q + k;
+				x += o != v ? 1u : 0u;
+				if ((o ^ v) & 1u) { // the walk changes only with bit 0
+					const uint32_t j = jpos[i];
+					atomicMin(&cpos[head[j]], j); // its session walks again from here
+					first = i < first ? i : first;
+				}
 			}
 		} else {
-			x += cf[k - nslow] != ncf[k - nslow] ? 1u : 0u;
+			x += cf[q - n4] != ncf[q - n4] ? 1u : 0u;
+		}
+	}
+	if (blockIdx.x == 0 && threadIdx.x < n - 4u * n4) { // the last events (n % 4)
+		const uint32_t i = 4u * n4 + threadIdx.x;
+		const uint8_t o = f[i], v = nf[i];
+		f[i] = 0;
+		x += o != v ? 1u : 0u;
+		if ((o ^ v) & 1u) {
+			const uint32_t j = jpos[i];
+			atomicMin(&cpos[head[j]], j);
+			first = i < first ? i : first;
 		}
 	}
 	if (__any(x != 0))
@@ -3583,8 +3663,9 @@ hipError_t launch_lru_init(const Dev& d, uint32_t nslow, const LruRound& w, hipS
 			(e = hipMemsetAsync(w.cm_end, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cm_head, 0xff, (size_t)d.carry_cap * 4, st)) != hipSuccess ||
 			(e = hipMemsetAsync(w.cpos, 0xff, (size_t)nslow * 4, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.opt, 0, d.n, st)) != hipSuccess || (e = hipMemsetAsync(w.f[0], 0, nslow, st)) != hipSuccess ||
-			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess || (e = hipMemsetAsync(w.nf_t, 0, d.n, st)) != hipSuccess)
+			(e = hipMemsetAsync(w.opt, 0, d.n, st)) != hipSuccess || (e = hipMemsetAsync(w.f[0], 0, d.n, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.f[1], 0, d.n, st)) != hipSuccess ||
+			(e = hipMemsetAsync(w.cf[0], 0, d.carry_cap, st)) != hipSuccess)
 		return e;
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
 	hipLaunchKernelGGL(k_lru_index, dim3(grid_for(nslow, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.jpos, w.head);
@@ -3611,10 +3692,16 @@ __device__ __forceinline__ void lru_round_reset(uint32_t* tot, unsigned long lon
 // The end of a round (one thread): the world derived is the world walked up to the batch's
 // end -> settled in world cur; an inconsistent world -> done, not settled (the one-lane replay
 // takes the batch); else the frontier moves past every event the round settled.
-__global__ void k_lru_advance(LruCtrl* ctl, unsigned long long* cnt, uint32_t* tot, uint32_t window, uint32_t n, uint32_t cur) {
+__global__ void k_lru_advance(LruCtrl* ctl, unsigned long long* cnt, uint32_t* tot, uint32_t window, uint32_t n, uint32_t cur,
+		unsigned long long* stat) {
 	if (threadIdx.x != 0 || ctl->done)
 		return;
 	ctl->rounds++;
+	if (stat) { // EBD_LRU_TRACE: the longest lane summed over rounds, the sessions walked
+		stat[2] += stat[3];
+		stat[3] = 0;
+		stat[4] += tot[3];
+	}
 	const unsigned long long changed = cnt[2], first = cnt[3];
 	const unsigned long long wend = (unsigned long long)ctl->front + window;
 	if (cnt[1]) { // operations with a full cache and no victim: not a world to walk on
@@ -3625,7 +3712,7 @@ __global__ void k_lru_advance(LruCtrl* ctl, unsigned long long* cnt, uint32_t* t
 	if (changed == 0 && wend >= n) {
 		ctl->done = 1;
 		ctl->settled = 1;
-		ctl->cur_final = cur;
+		ctl->cur_final = cur ^ 1; // the derived world (equal to the walked one, which k_lru_diff cleared)
 		return; // cnt[0] (the evictions) stays for the host
 	}
 	unsigned long long front = ctl->front;
@@ -3658,14 +3745,14 @@ hipError_t launch_lru_ctl_init(const Dev& d, const LruRound& w, uint32_t window,
 hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int cur, uint32_t window, hipStream_t st, int cus) {
 	const uint32_t n = d.n;
 	const uint8_t* f = w.f[cur];
-	uint8_t* nf = w.f[cur ^ 1];
+	uint8_t* nf = w.f[cur ^ 1]; // zero: cleared by the last round's k_lru_diff (or launch_lru_init)
 	const uint8_t* cf = w.cf[cur];
 	uint8_t* ncf = w.cf[cur ^ 1];
 	const LruCtrl* ctl = w.ctl;
 	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, ctl, w.rlist, w.tot, ncf,
 			d.carry_cap);
 	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
-			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, ctl}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
+			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, ctl, w.stat}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
 	hipLaunchKernelGGL(k_lru_scan, dim3(1), dim3(kScT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, n, d.carry_cap, w.bs,
 			w.mk_ref, w.mk_e, w.ev_t, w.evc, w.tot, ctl);
 	hipLaunchKernelGGL(k_lru_thresh, dim3(cus), dim3(kThT), 0, st, (const uint32_t*)w.mk_e, (const uint32_t*)w.evc, (const uint32_t*)w.tot,
@@ -3673,10 +3760,10 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 	hipLaunchKernelGGL(k_lru_take, dim3(1), dim3(kThT), 0, st, (const uint32_t*)w.mx, w.tot, ctl, w.vict, w.cnt);
 	hipLaunchKernelGGL(k_lru_victims, dim3(cus * 2), dim3(256), 0, st, d, (const uint32_t*)w.tot, (const uint32_t*)w.vict,
 			(const uint32_t*)w.mk_ref, (const uint32_t*)w.mk_e, (const uint32_t*)w.ev_t, (const uint32_t*)w.jpos, (const uint32_t*)w.head,
-			(const uint32_t*)w.cm_head, w.nf_t, ncf, w.cnt, ctl);
-	hipLaunchKernelGGL(k_lru_flags, dim3(grid_for(nslow + d.carry_cap, 256, cus * 8)), dim3(256), 0, st, d, nslow, w.nf_t, f, nf, cf,
-			(const uint8_t*)ncf, d.carry_cap, (const uint32_t*)w.head, w.cpos, w.cnt, ctl);
-	hipLaunchKernelGGL(k_lru_advance, dim3(1), dim3(64), 0, st, w.ctl, w.cnt, w.tot, window, n, (uint32_t)cur);
+			(const uint32_t*)w.cm_head, nf, ncf, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_diff, dim3(grid_for(n / 4 + d.carry_cap, 256, cus * 4)), dim3(256), 0, st, n, w.f[cur], (const uint8_t*)nf, cf,
+			(const uint8_t*)ncf, d.carry_cap, (const uint32_t*)w.jpos, (const uint32_t*)w.head, w.cpos, w.cnt, ctl);
+	hipLaunchKernelGGL(k_lru_advance, dim3(1), dim3(64), 0, st, w.ctl, w.cnt, w.tot, window, n, (uint32_t)cur, w.stat);
 	return hipGetLastError();
 }
 // The final walk of the exact path in the converged world (with output), then the carried
