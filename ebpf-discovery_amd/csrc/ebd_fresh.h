@@ -317,7 +317,10 @@ EBD_HD void dfa_walk_block(const Tab& T, const At& A, DfaWalk& w, const uint32_t
 	for (int k = 0; k < 16; k++) {
 		const uint32_t b = (wd[k >> 2] >> (8 * (k & 3))) & 0xffu;
 		const bool v = base + (uint32_t)k < ne;
-		const uint32_t ns = v ? (uint32_t)T[(s << 8) | b] : s;
+		// the read is unconditional (every index is valid): a read inside the condition made the
+		// device code branch per byte and wait for both table reads before the next byte's
+		const uint32_t t = (uint32_t)T[(s << 8) | b];
+		const uint32_t ns = v ? t : s;
 		const uint32_t an = A[ns];
 		chg |= an != a ? 1u << k : 0u;
 		P[k >> 2] |= an << (8 * (k & 3));

@@ -1617,8 +1617,13 @@ struct DryWalk {
 	unsigned long long* stat; // EBD_LRU_TRACE: events and bytes walked, the longest lane's bytes (summed over rounds)
 };
 
+#ifdef EBD_WALK_WPE // experiment: waves per SIMD the register budget must allow
+#define EBD_WALK_ATTR __attribute__((amdgpu_waves_per_eu(EBD_WALK_WPE, 8)))
+#else
+#define EBD_WALK_ATTR
+#endif
 template <bool DRY>
-__global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
+__global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
 		const uint32_t* hcount) {
 	if (DRY && dw.ctl->done) // the rounds have settled: later rounds' kernels do nothing
 		return;
@@ -1635,23 +1640,30 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 	const uint32_t* heads = hlist ? hlist : d.heads;
 	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	const uint32_t stride = gridDim.x * kWalkThreads;
-	// A lane walks its sessions one 16-byte block per iteration.  A lane whose event ended
-	// waits until 60 of the 64 lanes have (or none is still parsing); then the wave ends those
-	// events and starts the next ones together: one buffer per lane and step made each wave
-	// step as long as its longest buffer, while ending and starting events one lane at a time
-	// ran the long end-of-event path (outcome, emission, next event's loads) for a few lanes
-	// at a time.
+	// A lane walks its sessions one 64-byte window (four 16-byte blocks) per iteration.  A lane
+	// whose event ended waits until 60 of the 64 lanes have (or none is still parsing); then the
+	// wave ends those events and starts the next ones together: one buffer per lane and step
+	// made each wave step as long as its longest buffer, while ending and starting events one
+	// lane at a time ran the long end-of-event path (outcome, emission, next event's loads) for
+	// a few lanes at a time.
+	// Every iteration every lane issues the loads of the window it will need next (its event's
+	// next window, else its session's next event's first) and walks the window loaded the
+	// iteration before, so the loads' latency hides behind a window's walk.  They are issued
+	// unconditionally and in the same order each iteration: with a load issued only on some
+	// paths (a 16-byte block rotated through registers), the compiler waited for every load in
+	// flight before each block, and each block then cost a memory round trip (clock stamps:
+	// 5,600 cycles per block).
 	uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x;
 	bool have = false, in_ev = false, ended = false;
 	SessState S;
 	uint32_t grp = 0, jj = 0, jhead = 0;
 	EvCtx e;
 	DfaWalk w;
-	uint32_t pos0 = 0, ne = 0, k0 = 0, nb = 0, bi = 0;
+	uint32_t pos0 = 0, ne = 0, k0 = 0, nb = 0, wi = 0;
 	uintptr_t b0 = 0;
-	// the event's next four 16-byte blocks: a block's walk is far shorter than a load's latency,
-	// so one block in flight left every block of a fragment paying the full latency
-	uint4 cur = uint4{0u, 0u, 0u, 0u}, n1 = cur, n2 = cur, n3 = cur;
+	// the window in flight: event tag_i's window tag_w (kNone: nothing useful)
+	uint4 Wv[4] = {uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}};
+	uint32_t tag_i = kNone, tag_w = 0;
 	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
 	unsigned long long pf_off = 0;
 	uint32_t inserts = 0; // CTR_INSERTS: one atomic per wave when it ends
@@ -1729,13 +1741,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 						b0 = p & ~(uintptr_t)15;
 						k0 = (uint32_t)(p & 15u);
 						nb = ne ? (k0 + ne + 15u) >> 4 : 0u;
-						bi = 0;
-						if (nb) {
-							cur = *(const uint4*)b0;
-							n1 = nb > 1 ? *(const uint4*)(b0 + 16u) : cur;
-							n2 = nb > 2 ? *(const uint4*)(b0 + 32u) : cur;
-							n3 = nb > 3 ? *(const uint4*)(b0 + 48u) : cur;
-						}
+						wi = 0;
 						in_ev = true;
 					} else {
 						const uint32_t op = ev_end<DRY>(d, S, e, 0);
@@ -1753,19 +1759,44 @@ __global__ __launch_bounds__(kWalkThreads) void k_walk(Dev d, const uint8_t* evf
 				}
 			}
 		}
-		if (in_ev) {
-			if (bi < nb) { // one block (dfa_parse_dev's)
-				const uint4 nx = bi + 4 < nb ? *(const uint4*)(b0 + 16u * (bi + 4)) : cur;
-				const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-				const uint32_t base = 16u * bi - k0;
-				dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
-				cur = n1;
-				n1 = n2;
-				n2 = n3;
-				n3 = nx;
-				bi++;
+		// the window loaded last iteration (the copy waits for those loads only)
+		const uint4 X[4] = {Wv[0], Wv[1], Wv[2], Wv[3]};
+		const bool valid = in_ev && (nb == 0 || (tag_i == e.i && tag_w == wi)); // nb = 0: nothing to walk
+		{ // the next window: this event's next one, or the session's next event's first
+			uintptr_t nbase = (uintptr_t)d.payload;
+			uint32_t nlast = 0, ni = kNone, nw = 0;
+			if (in_ev && (!valid || 4u * (wi + 1) < nb)) {
+				nbase = b0;
+				nlast = nb ? nb - 1u : 0u;
+				ni = e.i;
+				nw = valid ? wi + 1 : wi;
+			} else if (pf_j != kNone && (pf_fl & FLAG_NEW) && pf_L != EBD_NO_BUFFER && pf_L && buf_in(d, pf_L, pf_off)) {
+				const uintptr_t pp = (uintptr_t)(d.payload + pf_off);
+				nbase = pp & ~(uintptr_t)15;
+				nlast = ((uint32_t)(pp & 15u) + pf_L - 1u) >> 4;
+				ni = pf_i;
+				nw = 0;
 			}
-			if (bi >= nb || w.tpos != kNone) {
+#pragma unroll
+			for (uint32_t k = 0; k < 4; k++) { // global (not flat) loads: counted by vmcnt alone
+				const v4u v = *(const __attribute__((address_space(1))) v4u*)(nbase + 16u * min(4u * nw + k, nlast));
+				Wv[k] = uint4{v.x, v.y, v.z, v.w};
+			}
+			tag_i = ni;
+			tag_w = nw;
+		}
+		if (valid) {
+#pragma unroll
+			for (uint32_t k = 0; k < 4; k++) { // dfa_parse_dev's blocks
+				const uint32_t bk = 4u * wi + k;
+				if (bk < nb && w.tpos == kNone) {
+					const uint32_t wd[4] = {X[k].x, X[k].y, X[k].z, X[k].w};
+					const uint32_t base = 16u * bk - k0;
+					dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
+				}
+			}
+			wi++;
+			if (4u * wi >= nb || w.tpos != kNone) {
 				in_ev = false;
 				ended = true;
 			}
