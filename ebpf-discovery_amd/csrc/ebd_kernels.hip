@@ -1550,13 +1550,12 @@ __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S
 	return ev_end(d, S, e, c);
 }
 
-// The session's state at its first event of the batch (sorted position j).
-__device__ __forceinline__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t slot) {
-	SSlot* ss = d.sset + slot;
-	ss->visited = 1;
+// The session's state at its first event of the batch (sorted position j); carry: its
+// session-set slot's carry word (1 + carried index, 0: none).
+__device__ __forceinline__ void session_begin_c(const Dev& d, SessState& S, uint32_t j, uint32_t slot, uint32_t carry) {
+	d.sset[slot].visited = 1;
 	S.w = Walk{nullptr, 0, j};
 	S.li = kNone;
-	const uint32_t carry = ss->carry;
 	if (carry) { // saved session from an earlier batch (LRU entry)
 		const Carry& c = d.carry_in[carry - 1];
 		S.g = c.g;
@@ -1569,6 +1568,9 @@ __device__ __forceinline__ void session_begin(const Dev& d, SessState& S, uint32
 		S.live = 0;
 		S.stamp = 0;
 	}
+}
+__device__ __forceinline__ void session_begin(const Dev& d, SessState& S, uint32_t j, uint32_t slot) {
+	session_begin_c(d, S, j, slot, d.sset[slot].carry);
 }
 
 // A session still in the LRU after the batch, with the bytes of its request in progress
@@ -1630,16 +1632,25 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	if (DRY && blockIdx.x * kWalkThreads >= *hcount)
 		return; // a round walks few sessions: the workgroups past them skip the table load
 	const uint32_t hz = DRY ? dw.ctl->tend : 0u;
-	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256];
-	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
-		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
-	__syncthreads();
-	const LdsTable T{tabs};
-	const ByteTab A{tabs + kLdsTableBytes};
+	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256 + 16];
+	uint32_t* s_next = (uint32_t*)(tabs + kLdsTableBytes + 256); // the workgroup's next session to hand out
 	// the sessions to walk: every one (k_walk_heads), or the exact-LRU round's list
 	const uint32_t* heads = hlist ? hlist : d.heads;
 	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
 	const uint32_t stride = gridDim.x * kWalkThreads;
+	// Sessions: the rounds' walks (DRY, a few per lane at most) take every stride-th; the batch
+	// walk gives each workgroup a contiguous share and its lanes take the next one from an LDS
+	// counter when they start a session, so that a lane with long sessions takes fewer of them
+	// (striding had the slowest lanes of a workgroup at 1.7x its mean).
+	const uint32_t wper = (uint32_t)(((unsigned long long)nh + gridDim.x - 1) / gridDim.x);
+	const uint32_t wbeg = min(nh, blockIdx.x * wper), wend = min(nh, wbeg + wper);
+	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
+		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
+	if (threadIdx.x == 0)
+		*s_next = wbeg + kWalkThreads;
+	__syncthreads();
+	const LdsTable T{tabs};
+	const ByteTab A{tabs + kLdsTableBytes};
 	// A lane walks its sessions one 64-byte window (four 16-byte blocks) per iteration.  A lane
 	// whose event ended waits until 60 of the 64 lanes have (or none is still parsing); then the
 	// wave ends those events and starts the next ones together: one buffer per lane and step
@@ -1653,7 +1664,7 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	// paths (a 16-byte block rotated through registers), the compiler waited for every load in
 	// flight before each block, and each block then cost a memory round trip (clock stamps:
 	// 5,600 cycles per block).
-	uint32_t h = blockIdx.x * kWalkThreads + threadIdx.x;
+	uint32_t h = DRY ? blockIdx.x * kWalkThreads + threadIdx.x : (wbeg + threadIdx.x < wend ? wbeg + threadIdx.x : kNone);
 	bool have = false, in_ev = false, ended = false;
 	SessState S;
 	uint32_t grp = 0, jj = 0, jhead = 0;
@@ -1665,7 +1676,12 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	uint4 Wv[4] = {uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}, uint4{0u, 0u, 0u, 0u}};
 	uint32_t tag_i = kNone, tag_w = 0;
 	uint32_t pf_j = kNone, pf_i = 0, pf_fl = 0, pf_L = 0; // the session's next event, prefetched
-	unsigned long long pf_off = 0;
+	unsigned long long pf_off = 0, nk1 = ~0ull;           // and the sort key after it
+	// the lane's next session, one dependent load per refill while the current one is walked,
+	// so that starting it waits for nothing: its head position, sort key, first event's words,
+	// the key after it, its session-set slot (or, DRY, its first position) and the slot's carry
+	uint32_t nx_h = kNone, nx_st = 0, nx_jj = 0, nx_fl = 0, nx_L = 0, nx_slot = 0, nx_carry = 0;
+	unsigned long long nx_key = 0, nx_k1 = 0, nx_off = 0;
 	uint32_t inserts = 0; // CTR_INSERTS: one atomic per wave when it ends
 	uint32_t st_ev = 0, st_by = 0; // DRY with dw.stat: this lane's events and bytes walked
 	for (;;) {
@@ -1685,38 +1701,78 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 					dw.opt[e.i] = (uint8_t)op;
 				ended = false;
 			}
+			if (have && nx_h < nh && nx_st < 4) { // the next session's pipeline: one stage per refill
+				if (nx_st == 0) {
+					nx_jj = heads[nx_h];
+				} else if (nx_st == 1) {
+					nx_key = d.slow_keys[nx_jj];
+				} else if (nx_st == 2) {
+					const uint32_t i0 = (uint32_t)nx_key;
+					nx_fl = d.ev[i0].flags;
+					nx_L = d.len[i0];
+					nx_off = d.off[i0];
+					nx_k1 = nx_jj + 1 < nslow ? d.slow_keys[nx_jj + 1] : ~0ull;
+					nx_slot = DRY ? dw.head[nx_jj] : d.ev_slot[i0];
+				} else if (!DRY) {
+					nx_carry = d.sset[nx_slot].carry;
+				}
+				nx_st++;
+			}
 			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
 				if (!have) {
-					jhead = jj = heads[h];
-					grp = (uint32_t)(d.slow_keys[jj] >> 32);
-					if (DRY)
-						jhead = dw.head[jj];
-					if (jj == jhead)
-						session_begin(d, S, jj, d.ev_slot[slow_event(d, jj)]);
-					else
-						S = dw.snap[jj]; // the state before event jj, as the last walk left it
-					have = true;
-				}
-				if (jj < nslow && (uint32_t)(d.slow_keys[jj] >> 32) == grp) {
-					uint32_t i, fl, L;
-					unsigned long long off;
-					if (pf_j == jj) { // loaded while the session's previous event was walked
-						i = pf_i, fl = pf_fl, L = pf_L, off = pf_off;
+					const bool ready = nx_h == h && nx_st == 4;
+					unsigned long long key;
+					if (ready) {
+						jj = nx_jj;
+						key = nx_key;
+						nk1 = nx_k1;
 					} else {
-						i = slow_event(d, jj);
-						fl = d.ev[i].flags, L = d.len[i], off = d.off[i];
+						jj = heads[h];
+						key = d.slow_keys[jj];
+						nk1 = jj + 1 < nslow ? d.slow_keys[jj + 1] : ~0ull;
 					}
-					// the session's next event: its loads travel while this one is walked
+					jhead = jj;
+					grp = (uint32_t)(key >> 32);
+					if (DRY)
+						jhead = ready ? nx_slot : dw.head[jj];
+					if (jj == jhead) {
+						if (!DRY && ready)
+							session_begin_c(d, S, jj, nx_slot, nx_carry);
+						else
+							session_begin(d, S, jj, d.ev_slot[(uint32_t)key]);
+					} else {
+						S = dw.snap[jj]; // the state before event jj, as the last walk left it
+					}
+					pf_j = jj; // the first event's words
+					pf_i = (uint32_t)key;
+					if (ready) {
+						pf_fl = nx_fl, pf_L = nx_L, pf_off = nx_off;
+					} else {
+						pf_fl = d.ev[pf_i].flags, pf_L = d.len[pf_i], pf_off = d.off[pf_i];
+					}
+					have = true;
+					if (DRY) {
+						nx_h = h + stride;
+					} else {
+						nx_h = atomicAdd(s_next, 1u);
+						nx_h = nx_h < wend ? nx_h : kNone;
+					}
+					nx_st = 0;
+				}
+				if (pf_j == jj) { // the session's next event (pf_j is set only inside its group)
+					const uint32_t i = pf_i, fl = pf_fl, L = pf_L;
+					const unsigned long long off = pf_off;
+					// the session's next event: its loads (and the sort key after it) travel while
+					// this one is walked
 					pf_j = kNone;
-					if (jj + 1 < nslow) {
-						const unsigned long long k2 = d.slow_keys[jj + 1];
-						if ((uint32_t)(k2 >> 32) == grp) {
-							pf_j = jj + 1;
-							pf_i = (uint32_t)k2;
-							pf_fl = d.ev[pf_i].flags;
-							pf_L = d.len[pf_i];
-							pf_off = d.off[pf_i];
-						}
+					const unsigned long long k2 = nk1;
+					if (jj + 1 < nslow && (uint32_t)(k2 >> 32) == grp) {
+						pf_j = jj + 1;
+						pf_i = (uint32_t)k2;
+						pf_fl = d.ev[pf_i].flags;
+						pf_L = d.len[pf_i];
+						pf_off = d.off[pf_i];
+						nk1 = jj + 2 < nslow ? d.slow_keys[jj + 2] : ~0ull;
 					}
 					if (DRY) {
 						dw.snap[jj] = S; // the state before event jj: a later walk may start here
@@ -1755,7 +1811,7 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 					if (DRY)
 						dw.wto[jhead] = kNone; // walked to its end
 					have = false;
-					h += stride;
+					h = DRY ? h + stride : nx_h;
 				}
 			}
 		}

@@ -49,12 +49,12 @@ def main():
 						}
 						W_evs++;""")
     s = sub(s, """					have = false;
-					h += stride;
+					h = DRY ? h + stride : nx_h;
 				}
 			}
 		}
-		if (in_ev) {""", """					have = false;
-					h += stride;
+		// the window loaded last iteration""", """					have = false;
+					h = DRY ? h + stride : nx_h;
 				}
 			}
 			W_rc += clock64() - R0;
@@ -65,7 +65,7 @@ def main():
 			W_it++;
 			W_act += (unsigned long long)__popcll(busy2);
 		}
-		if (in_ev) {""")
+		// the window loaded last iteration""")
     s = sub(s, """	if (!DRY) { // the loop ends for the whole wave at once
 		for (int o = 32; o > 0; o >>= 1)
 			inserts += __shfl_xor(inserts, o, 64);""", """	if (!DRY) {
@@ -79,12 +79,14 @@ def main():
 		for (int o = 32; o > 0; o >>= 1)
 			inserts += __shfl_xor(inserts, o, 64);""")
     # the block step's time: from B0 to the loop's end
-    s = sub(s, """			if (bi >= nb || w.tpos != kNone) {
+    s = sub(s, """			wi++;
+			if (4u * wi >= nb || w.tpos != kNone) {
 				in_ev = false;
 				ended = true;
 			}
 		}
-	}""", """			if (bi >= nb || w.tpos != kNone) {
+	}""", """			wi++;
+			if (4u * wi >= nb || w.tpos != kNone) {
 				in_ev = false;
 				ended = true;
 			}
