@@ -180,6 +180,10 @@ struct ebd_ctx {
 	LruRound lr{};              // the exact-LRU rounds' scratch (allocated on first need)
 	void* lr_mem = nullptr;
 	unsigned long long* h_lr = nullptr; // pinned: a round's counters
+	uint8_t* h_ps = nullptr;            // pinned: ebd_parse_streams' calls and bytes, both ways
+	size_t h_ps_cap = 0;
+	uint8_t* d_ps = nullptr;            // their device copy (grown as needed, kept)
+	size_t d_ps_cap = 0;
 	// network counters (EBD_CFG_NETWORK_COUNTERS): map entries (two tables: a clear rebuilds
 	// into the other), the v6 prefix dictionary, and the network-counter clear's scratch
 	int net_on = 0;
@@ -366,6 +370,10 @@ static void ctx_free(ebd_ctx* c) {
 		(void)hipFree(c->lr.stat);
 	if (c->h_lr)
 		(void)hipHostFree(c->h_lr);
+	if (c->h_ps)
+		(void)hipHostFree(c->h_ps);
+	if (c->d_ps)
+		(void)hipFree(c->d_ps);
 	for (int k = 0; k < 2; k++) {
 		auto& g = c->stg[k];
 		void* sp[] = {g.ev, g.len, g.off, g.payload};
@@ -2143,17 +2151,40 @@ int ebd_parse_streams(ebd_ctx* c, ebd_parse_call* calls, uint32_t n, const uint8
 		return 0;
 	std::lock_guard<std::mutex> lk(c->mu);
 	HIP_TRY(hipSetDevice(c->device));
-	AsyncBuf calls_b{c->stream}, data_b{c->stream};
-	HIP_TRY(hipMallocAsync(&calls_b.p, (size_t)n * sizeof(ebd_parse_call), c->stream));
-	HIP_TRY(hipMallocAsync(&data_b.p, (size_t)data_len + 16, c->stream));
-	HIP_TRY(hipMemcpyAsync(calls_b.p, calls, (size_t)n * sizeof(ebd_parse_call), hipMemcpyHostToDevice, c->stream));
+	// both directions through one pinned buffer of this context (copies from and to pageable
+	// memory are left to the runtime's staging otherwise, and the caller's buffers are not
+	// ours to pin)
+	const size_t cb = (size_t)n * sizeof(ebd_parse_call), need = cb + (size_t)data_len;
+	if (c->h_ps_cap < need) {
+		if (c->h_ps)
+			HIP_TRY(hipHostFree(c->h_ps));
+		c->h_ps = nullptr;
+		c->h_ps_cap = 0;
+		HIP_TRY(hipHostMalloc((void**)&c->h_ps, need, hipHostMallocDefault));
+		c->h_ps_cap = need;
+	}
+	// a device buffer kept by the context (stream-ordered allocations freed and reused every
+	// call returned another call's results now and then: 1 fresh process in 7 saw a stale state)
+	const size_t dneed = cb + (size_t)data_len + 16;
+	if (c->d_ps_cap < dneed) {
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		if (c->d_ps)
+			HIP_TRY(hipFree(c->d_ps));
+		c->d_ps = nullptr;
+		c->d_ps_cap = 0;
+		HIP_TRY(hipMalloc((void**)&c->d_ps, dneed));
+		c->d_ps_cap = dneed;
+	}
+	std::memcpy(c->h_ps, calls, cb);
 	if (data_len)
-		HIP_TRY(hipMemcpyAsync(data_b.p, data, (size_t)data_len, hipMemcpyHostToDevice, c->stream));
-	HIP_TRY(launch_parse_streams(c->d_trie, (ebd_parse_call*)calls_b.p, n, (const uint8_t*)data_b.p, c->stream));
-	HIP_TRY(hipMemcpyAsync(calls, calls_b.p, (size_t)n * sizeof(ebd_parse_call), hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(calls_b.release());
-	HIP_TRY(data_b.release());
+		std::memcpy(c->h_ps + cb, data, (size_t)data_len);
+	ebd_parse_call* dcalls = (ebd_parse_call*)c->d_ps;
+	const uint8_t* ddata = c->d_ps + cb;
+	HIP_TRY(hipMemcpyAsync(c->d_ps, c->h_ps, cb + (size_t)data_len, hipMemcpyHostToDevice, c->stream));
+	HIP_TRY(launch_parse_streams(c->d_trie, dcalls, n, ddata, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_ps, dcalls, cb, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	std::memcpy(calls, c->h_ps, cb);
 	return 0;
 }
 

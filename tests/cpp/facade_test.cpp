@@ -17,6 +17,7 @@
 #include "ebpf_discovery_amd.hpp"
 
 #include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <map>
 #include <sstream>
@@ -285,6 +286,7 @@ void parser_test_cases() {
 			{{"GET /"}, "GET", "/", "", "", {}, false, false},
 			{{"", ""}, "", "", "", "", {}, false, false},
 	};
+	size_t ci = 0;
 	for (const ValidCase& c : valid) {
 		ebdamd::HttpRequestParser parser;
 		size_t total = 0, all = 0;
@@ -292,6 +294,10 @@ void parser_test_cases() {
 			total += parser.parse(ch, c.isHttps ? EBD_FLAG_SESSION_SSL_HTTP : EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
 			all += ch.size();
 		}
+		if (parser.isInvalidState() || total != (c.total ? c.total : all))
+			std::fprintf(stderr, "valid case %zu: %zu chunks, total %zu of %zu, host '%s'\n", ci, c.chunks.size(), total, all,
+					parser.result.host.c_str());
+		ci++;
 		CHECK(parser.isFinished() == c.finished);
 		CHECK(!parser.isInvalidState());
 		CHECK(total == (c.total ? c.total : all));
@@ -442,6 +448,9 @@ int main(int argc, char** argv) {
 	try {
 		if (mode == "gpu")
 			run_gpu();
+		else if (mode == "parser-repeat") // the parser cases many times in one process
+			for (int k = 0; k < (argc > 2 ? std::atoi(argv[2]) : 100); k++)
+				parser_test_cases();
 		else
 			run_cpu();
 	} catch (const std::exception& e) {
