@@ -184,6 +184,10 @@ struct ebd_ctx {
 	size_t h_ps_cap = 0;
 	uint8_t* d_ps = nullptr;            // their device copy (grown as needed, kept)
 	size_t d_ps_cap = 0;
+	// device scratch of the C-ABI calls (scratch_get): chunks kept until the context goes, so
+	// that no call frees and re-allocates memory a copy of the same stream still reads
+	std::vector<std::pair<uint8_t*, size_t>> scr;
+	size_t scr_ci = 0, scr_off = 0;
 	// network counters (EBD_CFG_NETWORK_COUNTERS): map entries (two tables: a clear rebuilds
 	// into the other), the v6 prefix dictionary, and the network-counter clear's scratch
 	int net_on = 0;
@@ -374,6 +378,8 @@ static void ctx_free(ebd_ctx* c) {
 		(void)hipHostFree(c->h_ps);
 	if (c->d_ps)
 		(void)hipFree(c->d_ps);
+	for (auto& ch : c->scr)
+		(void)hipFree(ch.first);
 	for (int k = 0; k < 2; k++) {
 		auto& g = c->stg[k];
 		void* sp[] = {g.ev, g.len, g.off, g.payload};
@@ -1384,18 +1390,46 @@ static int ensure_verify(ebd_ctx* c, uint32_t n) {
 	return 0;
 }
 
-// offs = the exclusive scan of nb (n entries); the scan's scratch is allocated on the stream.
+// Device scratch for one C-ABI call: pieces carved from the context's chunks in order, the
+// carving restarting at every call (ScratchScope).  Every user runs on the context stream, so a
+// call may reuse an earlier call's bytes in stream order; chunks are only added (a freed and
+// re-allocated stream-ordered buffer had handed ebd_parse_streams a stale result now and then).
+static hipError_t scratch_get(ebd_ctx* c, size_t bytes, void** out) {
+	bytes = (bytes + 255) & ~(size_t)255;
+	while (c->scr_ci < c->scr.size() && c->scr_off + bytes > c->scr[c->scr_ci].second) {
+		c->scr_ci++;
+		c->scr_off = 0;
+	}
+	if (c->scr_ci == c->scr.size()) {
+		const size_t cap = std::max(bytes, c->scr.empty() ? (size_t)(1 << 20) : 2 * c->scr.back().second);
+		uint8_t* p = nullptr;
+		hipError_t e = hipMalloc((void**)&p, cap);
+		if (e != hipSuccess)
+			return e;
+		c->scr.emplace_back(p, cap);
+		c->scr_off = 0;
+	}
+	*out = c->scr[c->scr_ci].first + c->scr_off;
+	c->scr_off += bytes;
+	return hipSuccess;
+}
+struct ScratchScope {
+	explicit ScratchScope(ebd_ctx* c) {
+		c->scr_ci = 0;
+		c->scr_off = 0;
+	}
+};
+
+// offs = the exclusive scan of nb (n entries), its scratch from the call's scratch.
 static hipError_t excl_scan(ebd_ctx* c, const unsigned long long* nb, unsigned long long* offs, uint32_t n) {
 	hipError_t e;
 	size_t tb = 0;
 	if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nb, offs, (int)n, c->stream)) != hipSuccess)
 		return e;
 	void* tmp = nullptr;
-	if ((e = hipMallocAsync(&tmp, tb + 16, c->stream)) != hipSuccess)
+	if ((e = scratch_get(c, tb + 16, &tmp)) != hipSuccess)
 		return e;
-	e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nb, offs, (int)n, c->stream);
-	const hipError_t f = hipFreeAsync(tmp, c->stream);
-	return e != hipSuccess ? e : f;
+	return hipcub::DeviceScan::ExclusiveSum(tmp, tb, nb, offs, (int)n, c->stream);
 }
 
 // The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
@@ -1405,16 +1439,12 @@ static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_
 	return e != hipSuccess ? e : excl_scan(c, nb, offs, n);
 }
 
-// A stream-ordered scratch allocation, freed on every return path.
+// A piece of the call's scratch (scratch_get); nothing to free.
 struct AsyncBuf {
-	hipStream_t st;
+	ebd_ctx* c;
 	void* p = nullptr;
-	hipError_t release() {
-		void* q = p;
-		p = nullptr;
-		return q ? hipFreeAsync(q, st) : hipSuccess;
-	}
-	~AsyncBuf() { (void)release(); }
+	hipError_t alloc(size_t bytes) { return scratch_get(c, bytes, &p); }
+	hipError_t release() { return hipSuccess; }
 };
 
 int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
@@ -1422,11 +1452,12 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 	if (!c || world == 0 || world > 64 || !counts || !str_counts)
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
 	if (!c->d_collect)
 		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
-	AsyncBuf own_b{c->stream}; // cnt, bytes, cur: world each
-	HIP_TRY(hipMallocAsync(&own_b.p, 3 * 64 * sizeof(unsigned long long), c->stream));
+	AsyncBuf own_b{c}; // cnt, bytes, cur: world each
+	HIP_TRY(own_b.alloc(3 * 64 * sizeof(unsigned long long)));
 	unsigned long long* own = (unsigned long long*)own_b.p;
 	HIP_TRY(hipMemsetAsync(own, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
 	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
@@ -1449,8 +1480,8 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 		} else {
 			// records by owner, then their bytes at the scan of their sizes: owner w's bytes are
 			// the str_counts[w] after the earlier owners', in its records' order
-			AsyncBuf tmp_b{c->stream}; // srcoff, nb, offs: total each
-			HIP_TRY(hipMallocAsync(&tmp_b.p, 3 * total * sizeof(unsigned long long), c->stream));
+			AsyncBuf tmp_b{c}; // srcoff, nb, offs: total each
+			HIP_TRY(tmp_b.alloc(3 * total * sizeof(unsigned long long)));
 			unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
 			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, own + 128, recs, tmp, c->stream, c->cus));
@@ -1468,6 +1499,7 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 	if (!c || (n && (!recs || (!strings && strlen))))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
@@ -1476,8 +1508,8 @@ int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t
 		return rc;
 	Dev d = make_dev(c);
 	d.n = 0;
-	AsyncBuf tmp_b{c->stream}; // nb, offs
-	HIP_TRY(hipMallocAsync(&tmp_b.p, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c}; // nb, offs
+	HIP_TRY(tmp_b.alloc(2 * (size_t)n * sizeof(unsigned long long)));
 	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(hipMemsetAsync(c->d_ctr + CTR_VERIFY, 0, sizeof(unsigned long long), c->stream));
@@ -1512,12 +1544,13 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 	if (!c || !out_len || (n && (!recs || !need || (!strings && strlen))))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
 	*out_len = 0;
 	if (n == 0)
 		return 0;
-	AsyncBuf tmp_b{c->stream}; // nb, soff, nbn, doff
-	HIP_TRY(hipMallocAsync(&tmp_b.p, 4 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c}; // nb, soff, nbn, doff
+	HIP_TRY(tmp_b.alloc(4 * (size_t)n * sizeof(unsigned long long)));
 	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(launch_wire_bytes_needed(recs, n, need, nullptr, tmp + 2 * (size_t)n, c->stream, c->cus));
@@ -1546,13 +1579,14 @@ int ebd_merge_service_bytes_device(ebd_ctx* c, const ebd_wire_service* recs, uin
 	if (!c || (n && (!recs || !dst || (!strings && strlen))))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
 	if (n == 0)
 		return 0;
 	Dev d = make_dev(c);
 	d.n = 0;
-	AsyncBuf tmp_b{c->stream}; // nb, offs
-	HIP_TRY(hipMallocAsync(&tmp_b.p, 2 * (size_t)n * sizeof(unsigned long long), c->stream));
+	AsyncBuf tmp_b{c}; // nb, offs
+	HIP_TRY(tmp_b.alloc(2 * (size_t)n * sizeof(unsigned long long)));
 	unsigned long long* tmp = (unsigned long long*)tmp_b.p;
 	HIP_TRY(launch_wire_bytes_needed(recs, n, nullptr, (const unsigned long long*)dst, tmp, c->stream, c->cus));
 	HIP_TRY(excl_scan(c, tmp, tmp + n, n));
@@ -1574,6 +1608,7 @@ int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, cons
 			return -EINVAL;
 	}
 	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
 	if (int rc = finish_pending(c))
 		return rc;
@@ -1584,8 +1619,8 @@ int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, cons
 	d.now = ctx_now(c);
 	ebd_request* drq = nullptr;
 	uint8_t* dstr = nullptr; // 16 bytes of slack: the key reads 8-byte pieces
-	HIP_TRY(hipMallocAsync((void**)&drq, (size_t)n * sizeof(ebd_request), c->stream));
-	HIP_TRY(hipMallocAsync((void**)&dstr, (size_t)strings_len + 16, c->stream));
+	HIP_TRY(scratch_get(c, (size_t)n * sizeof(ebd_request), (void**)&drq));
+	HIP_TRY(scratch_get(c, (size_t)strings_len + 16, (void**)&dstr));
 	hipError_t e = hipMemcpyAsync(drq, reqs, (size_t)n * sizeof(ebd_request), hipMemcpyHostToDevice, c->stream);
 	if (e == hipSuccess && strings_len)
 		e = hipMemcpyAsync(dstr, strings, (size_t)strings_len, hipMemcpyHostToDevice, c->stream);
@@ -1597,8 +1632,6 @@ int ebd_aggregate_requests(ebd_ctx* c, const ebd_request* reqs, uint32_t n, cons
 		e = launch_agg_requests(d, drq, n, dstr, c->stream, c->cus);
 	if (e == hipSuccess)
 		e = launch_verify(d, c->stream, c->cus);
-	(void)hipFreeAsync(drq, c->stream);
-	(void)hipFreeAsync(dstr, c->stream);
 	HIP_TRY(e);
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	c->seq_base += n;
