@@ -151,6 +151,7 @@ struct ebd_ctx {
 	uint32_t* d_evslot = nullptr;
 	uint32_t* d_smask = nullptr; // the session set's mask for the batch (k_sset_size)
 	unsigned long long* d_slow[2] = {nullptr, nullptr};
+	unsigned long long* d_pieces = nullptr; // Dev::pieces
 	void* d_sort_tmp = nullptr;
 	size_t sort_tmp_bytes = 0;
 	Carry* d_carry[2] = {nullptr, nullptr};
@@ -327,6 +328,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.dirty = c->d_dirty;
 	d.ev_slot = c->d_evslot;
 	d.slow_keys = c->d_slow[0];
+	d.pieces = c->d_pieces;
 	d.carry_in = c->d_carry[c->carry_cur];
 	d.n_carry_in = c->n_carry;
 	d.carry_out = c->d_carry[c->carry_cur ^ 1];
@@ -357,7 +359,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
-			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
@@ -532,6 +534,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMalloc(&c->d_smask, sizeof(uint32_t)));
 	CTX_TRY(hipMalloc(&c->d_slow[0], n * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_slow[1], n * sizeof(unsigned long long)));
+	CTX_TRY(hipMalloc(&c->d_pieces, n * sizeof(unsigned long long)));
 	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
 			c->stream));
 	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes ? c->sort_tmp_bytes : 16));

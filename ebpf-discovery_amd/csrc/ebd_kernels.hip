@@ -1305,14 +1305,13 @@ __device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_
 		pos = w.clen;
 	}
 	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
-		const uint32_t i = slow_event(d, j);
-		const uint32_t L = d.len[i];
-		uint32_t pl = ((d.ev[i].flags & FLAG_NEW) && L != EBD_NO_BUFFER && buf_in(d, L, d.off[i])) ? L : 0; // piece_len
+		const unsigned long long pc = d.pieces[j]; // the walker's record of the piece (one line for a request's pieces)
+		uint32_t pl = (uint32_t)(pc & 0xffffffu);
 		if (j == jend)
 			pl = cend;
 		if (pl == 0)
 			continue;
-		piece(d.payload + d.off[i], pos, pl);
+		piece(d.payload + (pc >> 24), pos, pl);
 		pos += pl;
 	}
 }
@@ -1541,8 +1540,19 @@ __device__ __forceinline__ uint32_t ev_end(const Dev& d, SessState& S, const EvC
 
 // Event jj (sorted position) of a session: handleNewEvent (Discovery.cpp:92-198) with the
 // session's state in S, the whole buffer at once (the exact LRU walker's form).
+// The piece record of sorted position jj (Dev::pieces): k_emit copies a request's spans from them.
+__device__ __forceinline__ void piece_record(const Dev& d, uint32_t jj, uint32_t fl, uint32_t L, unsigned long long off) {
+	uint32_t pl = ((fl & FLAG_NEW) && L != EBD_NO_BUFFER && buf_in(d, L, off)) ? L : 0; // piece_len
+	if (pl > 0xffffffu || (off >> 40)) { // beyond the record's fields (a buffer is at most 8 KiB): reported
+		set_error(d, EBD_ERR_BAD_INPUT);
+		pl = 0;
+	}
+	d.pieces[jj] = (off << 24) | pl;
+}
+
 __device__ uint32_t session_event(const Dev& d, const SessTabs& tb, SessState& S, uint32_t jj) {
 	const uint32_t i = slow_event(d, jj);
+	piece_record(d, jj, d.ev[i].flags, d.len[i], d.off[i]);
 	EvCtx e;
 	uint32_t c = 0;
 	if (ev_begin(d, S, jj, i, d.ev[i].flags, d.len[i], d.off[i], e))
@@ -1783,6 +1793,8 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 							continue;
 						}
 					}
+					if (!DRY)
+						piece_record(d, jj, fl, L, off);
 					if (evf && (evf[i] & 1u))
 						S.live = 0; // evicted since its previous event: find() misses
 					if (ev_begin(d, S, jj, i, fl, L, off, e)) {
