@@ -146,7 +146,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 		if (t == 0) {
 			t = atomicCAS(&s->tag, 0ull, h.lo);
 			if (t == 0) {
-				atomicExch(&s->hi, h.hi);
+				atomicExch(&s->hi, h.hi); // (a write-through store instead was slower: DESIGN.md round 5)
 				*claimed = true;
 				seen_first = ~0ull;
 				found = true;
@@ -856,11 +856,10 @@ void k_fresh(Dev d) {
 	const uint32_t sl = wave * 64 + lane; // scan lane
 	uint32_t* stg = sh.stage + sl;        // this lane's staging row (word j at stg[j * kScanLanes])
 	auto grab = [&]() -> uint32_t { return atomicAdd(&sh.next_ev, 1u); };
-	// The lane's current event (e0), the next one (e1, decoded: its first window is loaded while
-	// e0's last one is scanned) and the one after (n2, its words as loaded).  n2 is decoded only
-	// at the next hand-off, an event later, so a hand-off never waits for the loads it issues:
-	// waiting for them (and, the counter being in order, for the window issued before them)
-	// had cost the scan waves 23 % of their time (clock stamps).
+	// The lane's current event (e0) and the next one (e1, decoded: its first window is loaded
+	// while e0's last one is scanned).  Holding a third event's words as loaded, decoded only at
+	// the next hand-off so that a hand-off never waits for the loads it issues, was measured
+	// neutral: 2.97-3.02 against 2.98 ms per 20 M config-3 events (round 5, same box).
 	LaneEv e0 = lane_ev(d, lane_load(d, rb + sl, re));
 	LaneEv e1 = lane_ev(d, lane_load(d, rb + kScanLanes + sl, re));
 	uint32_t w0 = 0; // e0's window to scan next
