@@ -152,6 +152,7 @@ struct ebd_ctx {
 	uint32_t* d_smask = nullptr; // the session set's mask for the batch (k_sset_size)
 	unsigned long long* d_slow[2] = {nullptr, nullptr};
 	unsigned long long* d_pieces = nullptr; // Dev::pieces
+	uint4* d_hrec = nullptr;                // Dev::hrec (allocated with the first session-path batch)
 	void* d_sort_tmp = nullptr;
 	size_t sort_tmp_bytes = 0;
 	Carry* d_carry[2] = {nullptr, nullptr};
@@ -329,6 +330,7 @@ static Dev make_dev(ebd_ctx* c) {
 	d.ev_slot = c->d_evslot;
 	d.slow_keys = c->d_slow[0];
 	d.pieces = c->d_pieces;
+	d.hrec = c->d_hrec;
 	d.carry_in = c->d_carry[c->carry_cur];
 	d.n_carry_in = c->n_carry;
 	d.carry_out = c->d_carry[c->carry_cur ^ 1];
@@ -359,7 +361,7 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
-			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_hrec, c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
@@ -547,8 +549,9 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	if (c->sstr_cap > (4ull << 30))
 		c->sstr_cap = 4ull << 30;
 	CTX_TRY(hipMalloc(&c->d_sstr, c->sstr_cap + 64)); // k_reps reads whole 8-byte words
-	CTX_TRY(hipMalloc(&c->d_ctr, CTR_COUNT * sizeof(unsigned long long)));
-	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, CTR_COUNT * sizeof(unsigned long long), c->stream));
+	// one word past the counters: k_walk's chunk counter (zeroed before each walk)
+	CTX_TRY(hipMalloc(&c->d_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long)));
+	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, (CTR_COUNT + 1) * sizeof(unsigned long long), c->stream));
 	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
 	CTX_TRY(hipHostMalloc(&c->h_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long), hipHostMallocDefault));
 	CTX_TRY(hipHostMalloc(&c->h_end, CTR_COUNT * sizeof(unsigned long long), hipHostMallocDefault));
@@ -782,6 +785,9 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		}));
 		d.slow_keys = c->d_slow[1];
 		d.heads = (uint32_t*)c->d_slow[0]; // the sort's input, free after it
+		if (!c->d_hrec)
+			HIP_TRY(hipMalloc(&c->d_hrec, (size_t)c->max_events * sizeof(uint4)));
+		d.hrec = c->d_hrec;
 		// LRU eviction possible?  Only if more sessions than its capacity could be live at once
 		// (k_walk_lru's comment): first the cheap count of candidate sessions, then the bound.
 		bool exact = false;

@@ -213,6 +213,7 @@ struct Dev {
 	unsigned long long* slow_keys; // session group << 32 | event (k_slow_collect), sorted
 	uint32_t* ev_slot;             // per event: its session's session-set slot (session-path events only)
 	uint32_t* heads; // sorted position of each session's first event (k_walk_heads)
+	uint4* hrec;     // per head (k_walk_heads): its sorted position, first event, session-set slot, group
 	unsigned long long* pieces; // per sorted position: its buffer's payload offset << 24 | the bytes a parse may take (the walkers write it, k_emit reads it)
 	Carry* carry_in;
 	uint32_t n_carry_in;

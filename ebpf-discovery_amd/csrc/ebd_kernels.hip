@@ -1160,8 +1160,9 @@ constexpr int kWalkThreads = 256;
 #endif
 constexpr int kWalkRefill = EBD_WALK_REFILL; // lanes of a wave waiting before it ends and starts events
 #ifndef EBD_WALK_BLOCKS
-#define EBD_WALK_BLOCKS 3 // k_walk blocks per CU
+#define EBD_WALK_BLOCKS 4 // k_walk blocks per CU (EBD_WALK_WPE waves per SIMD)
 #endif
+constexpr int kWalkDryBlocks = 3; // k_walk_dry blocks per CU (3 waves per SIMD at its register count)
 
 struct Walk {
 	const uint8_t* cb; // carried bytes of the request in progress
@@ -1628,21 +1629,84 @@ struct DryWalk {
 	unsigned long long* stat; // EBD_LRU_TRACE: events and bytes walked, the longest lane's bytes (summed over rounds)
 };
 
-#ifdef EBD_WALK_WPE // experiment: waves per SIMD the register budget must allow
+// k_walk's LDS tables: the DFA image (LdsTable's byte-major layout) with one more column,
+// kWalkIdCol, in which every state steps to itself, then the state attributes.  A byte outside
+// the parse (before the buffer in its first block, past the allowed bytes in its last) reads the
+// identity column, so the state chain carries no select: one v_mad_u32_u24 and one ds_read_u8
+// per byte.
+constexpr uint32_t kWalkIdCol = kLdsCols;
+constexpr uint32_t kWalkAttrOff = ((kLdsCols + 1) * kLdsStride + 15u) & ~15u;
+// Sessions of the batch walk are handed out in chunks of kWalkChunk: chunk 0 of each workgroup
+// is fixed (blockIdx.x), the later ones are claimed from a global counter (d.ctr[CTR_COUNT],
+// zeroed before each launch) by the lane that draws their first ticket.  A fixed share per
+// workgroup had the walk end with its slowest workgroups: with the same sessions, events and
+// bytes each, some took twice the median's time (80 M config-4 events, tools/walk_balance.py).
+constexpr uint32_t kWalkChunk = kWalkThreads, kWalkSlots = 8; // chunk bases kept in LDS
+constexpr uint32_t kWalkLdsBytes = kWalkAttrOff + 256 + 16 + 8 * kWalkSlots; // + ticket counter, chunk bases and tags
+
+// dfa_walk_block (ebd_fresh.h) on k_walk's tables: the same walk, with the valid bytes' count
+// computed once per block, and the attribute changes found from the packed attributes (four
+// bytes per word) instead of a compare per byte.
+__device__ __forceinline__ void walk_block(const uint8_t* tabs, DfaWalk& w, const uint32_t (&wd)[4], uint32_t base, uint32_t pbase,
+		uint32_t ne) {
+	const uint32_t a0 = w.a;
+	uint32_t s = w.s;
+	uint32_t P[4] = {0u, 0u, 0u, 0u}; // the attribute after each byte
+#pragma unroll
+	for (int k = 0; k < 16; k++) {
+		const uint32_t b = (wd[k >> 2] >> (8 * (k & 3))) & 0xffu;
+		const uint32_t col = base + (uint32_t)k < ne ? min(b, kLdsCols - 1) : kWalkIdCol;
+		s = tabs[col * kLdsStride + s];
+		P[k >> 2] |= (uint32_t)tabs[kWalkAttrOff + s] << (8 * (k & 3));
+	}
+	// valid bytes: base + k < ne, consecutive (base wraps below 0 in a buffer's first block)
+	const uint32_t nv = (int)base < 0 ? min(16u - min(0u - base, 16u), ne) : base < ne ? min(16u, ne - base) : 0u;
+	uint32_t chg = 0, prev = a0 << 24;
+#pragma unroll
+	for (int q = 0; q < 4; q++) { // bytes whose attribute differs from the one before
+		const uint32_t x = P[q] ^ __builtin_amdgcn_alignbyte(P[q], prev, 3u);
+		const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+		chg |= ((((nz >> 7) * 0x00204081u) >> 21) & 0xfu) << (4 * q);
+		prev = P[q];
+	}
+	if (nv) {
+		if (w.pos == 0) // P:162: handleCharMethod: the request's first byte is the method candidate
+			w.mcand = blk_byte(wd[0], wd[1], wd[2], wd[3], 0u - pbase);
+		if ((a0 & A_TERM) && w.tpos == kNone)
+			w.tpos = w.pos + 1;
+	}
+	for (uint32_t m = chg; m; m &= m - 1u) {
+		const uint32_t k = (uint32_t)__builtin_ctz(m);
+		dfa_walk_change(w, k ? blk_byte(P[0], P[1], P[2], P[3], k - 1u) : a0, blk_byte(P[0], P[1], P[2], P[3], k), pbase + k);
+	}
+	w.s = s;
+	w.a = prev >> 24;
+	w.pos += nv;
+}
+
+// Waves per SIMD the walker's register budget must allow (0: the compiler's choice).  At 4
+// (128 VGPRs, a few spills outside the byte loop; 4 workgroups per CU) k_walk took 20.1-20.4 ms
+// per 80 M config-4 events against 21.3-21.4 at 3 (150 VGPRs).
+#ifndef EBD_WALK_WPE
+#define EBD_WALK_WPE 4
+#endif
+#if EBD_WALK_WPE
 #define EBD_WALK_ATTR __attribute__((amdgpu_waves_per_eu(EBD_WALK_WPE, 8)))
 #else
 #define EBD_WALK_ATTR
 #endif
 template <bool DRY>
-__global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
+__device__ __forceinline__ void walk_sessions(const Dev& d, const uint8_t* evf, const DryWalk& dw, const uint32_t* hlist,
 		const uint32_t* hcount) {
 	if (DRY && dw.ctl->done) // the rounds have settled: later rounds' kernels do nothing
 		return;
 	if (DRY && blockIdx.x * kWalkThreads >= *hcount)
 		return; // a round walks few sessions: the workgroups past them skip the table load
 	const uint32_t hz = DRY ? dw.ctl->tend : 0u;
-	__shared__ __attribute__((aligned(16))) uint8_t tabs[kLdsTableBytes + 256 + 16];
-	uint32_t* s_next = (uint32_t*)(tabs + kLdsTableBytes + 256); // the workgroup's next session to hand out
+	__shared__ __attribute__((aligned(16))) uint8_t tabs[kWalkLdsBytes];
+	uint32_t* s_next = (uint32_t*)(tabs + kWalkAttrOff + 256); // the workgroup's next ticket
+	uint32_t* s_base = s_next + 4;                            // chunk c's first session, at c % kWalkSlots
+	uint32_t* s_tag = s_base + kWalkSlots;                    // the chunk s_base holds
 	// the sessions to walk: every one (k_walk_heads), or the exact-LRU round's list
 	const uint32_t* heads = hlist ? hlist : d.heads;
 	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
@@ -1651,15 +1715,18 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	// walk gives each workgroup a contiguous share and its lanes take the next one from an LDS
 	// counter when they start a session, so that a lane with long sessions takes fewer of them
 	// (striding had the slowest lanes of a workgroup at 1.7x its mean).
-	const uint32_t wper = (uint32_t)(((unsigned long long)nh + gridDim.x - 1) / gridDim.x);
-	const uint32_t wbeg = min(nh, blockIdx.x * wper), wend = min(nh, wbeg + wper);
-	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes + 256; k += kWalkThreads * 16u)
+	for (uint32_t k = threadIdx.x * 16u; k < kLdsTableBytes; k += kWalkThreads * 16u)
 		*(uint4*)(tabs + k) = *(const uint4*)(d.dfa + k);
+	if (threadIdx.x < kLdsStride)
+		tabs[kWalkIdCol * kLdsStride + threadIdx.x] = (uint8_t)threadIdx.x; // the identity column
+	if (threadIdx.x < 256 / 16)
+		*(uint4*)(tabs + kWalkAttrOff + 16u * threadIdx.x) = *(const uint4*)(d.dfa + kLdsTableBytes + 16u * threadIdx.x);
+	if (threadIdx.x < kWalkSlots)
+		s_tag[threadIdx.x] = 0; // chunk 0 is never looked up
 	if (threadIdx.x == 0)
-		*s_next = wbeg + kWalkThreads;
+		*s_next = kWalkThreads; // the lanes' first sessions are chunk 0
 	__syncthreads();
-	const LdsTable T{tabs};
-	const ByteTab A{tabs + kLdsTableBytes};
+	const ByteTab A{tabs + kWalkAttrOff};
 	// A lane walks its sessions one 64-byte window (four 16-byte blocks) per iteration.  A lane
 	// whose event ended waits until 60 of the 64 lanes have (or none is still parsing); then the
 	// wave ends those events and starts the next ones together: one buffer per lane and step
@@ -1673,7 +1740,28 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	// paths (a 16-byte block rotated through registers), the compiler waited for every load in
 	// flight before each block, and each block then cost a memory round trip (clock stamps:
 	// 5,600 cycles per block).
-	uint32_t h = DRY ? blockIdx.x * kWalkThreads + threadIdx.x : (wbeg + threadIdx.x < wend ? wbeg + threadIdx.x : kNone);
+	// The next session for a lane of the batch walk (kNone: none left).  The claim precedes the
+	// wait in every call, so a lane never waits for a claim by a lane of its own wave that has
+	// not run; a claim by another wave is one global atomic away.
+	auto take = [&]() -> uint32_t {
+		const uint32_t t = atomicAdd(s_next, 1u);
+		const uint32_t c = t / kWalkChunk, o = t % kWalkChunk, k = c % kWalkSlots;
+		if (o == 0) {
+			s_base[k] = gridDim.x * kWalkChunk + (uint32_t)atomicAdd(d.ctr + CTR_COUNT, (unsigned long long)kWalkChunk);
+			lds_store_rel(&s_tag[k], c);
+		}
+		for (uint32_t spins = 0; lds_load_acq(&s_tag[k]) != c; spins++) {
+			if (spins > (1u << 22)) { // cannot happen (the claimer runs unconditionally): reported, never hung on
+				set_error(d, EBD_ERR_INTERNAL);
+				return kNone;
+			}
+			__builtin_amdgcn_s_sleep(1);
+		}
+		const uint32_t hh = s_base[k] + o;
+		return hh < nh ? hh : kNone;
+	};
+	const uint32_t h0 = blockIdx.x * kWalkThreads + threadIdx.x;
+	uint32_t h = DRY ? h0 : (h0 < nh ? h0 : kNone);
 	bool have = false, in_ev = false, ended = false;
 	SessState S;
 	uint32_t grp = 0, jj = 0, jhead = 0;
@@ -1690,6 +1778,9 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 	// so that starting it waits for nothing: its head position, sort key, first event's words,
 	// the key after it, its session-set slot (or, DRY, its first position) and the slot's carry
 	uint32_t nx_h = kNone, nx_st = 0, nx_jj = 0, nx_fl = 0, nx_L = 0, nx_slot = 0, nx_carry = 0;
+	// the batch walk reads the head record k_walk_heads wrote (two stages); the rounds' walks
+	// follow their own list in four (head, key, event words and slot)
+	constexpr uint32_t kNxStages = DRY ? 4u : 2u;
 	unsigned long long nx_key = 0, nx_k1 = 0, nx_off = 0;
 	uint32_t inserts = 0; // CTR_INSERTS: one atomic per wave when it ends
 	uint32_t st_ev = 0, st_by = 0; // DRY with dw.stat: this lane's events and bytes walked
@@ -1710,8 +1801,20 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 					dw.opt[e.i] = (uint8_t)op;
 				ended = false;
 			}
-			if (have && nx_h < nh && nx_st < 4) { // the next session's pipeline: one stage per refill
-				if (nx_st == 0) {
+			if (have && nx_h < nh && nx_st < kNxStages) { // the next session's pipeline: one stage per refill
+				if (!DRY && nx_st == 0) { // its head record (k_walk_heads): position, first event, slot, group
+					const uint4 r = d.hrec[nx_h];
+					nx_jj = r.x;
+					nx_key = ((unsigned long long)r.w << 32) | r.y;
+					nx_slot = r.z;
+				} else if (!DRY) { // its first event's words, the key after it, the slot's carry word
+					const uint32_t i0 = (uint32_t)nx_key;
+					nx_fl = d.ev[i0].flags;
+					nx_L = d.len[i0];
+					nx_off = d.off[i0];
+					nx_k1 = nx_jj + 1 < nslow ? d.slow_keys[nx_jj + 1] : ~0ull;
+					nx_carry = d.sset[nx_slot].carry;
+				} else if (nx_st == 0) {
 					nx_jj = heads[nx_h];
 				} else if (nx_st == 1) {
 					nx_key = d.slow_keys[nx_jj];
@@ -1721,15 +1824,13 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 					nx_L = d.len[i0];
 					nx_off = d.off[i0];
 					nx_k1 = nx_jj + 1 < nslow ? d.slow_keys[nx_jj + 1] : ~0ull;
-					nx_slot = DRY ? dw.head[nx_jj] : d.ev_slot[i0];
-				} else if (!DRY) {
-					nx_carry = d.sset[nx_slot].carry;
+					nx_slot = dw.head[nx_jj];
 				}
 				nx_st++;
 			}
 			while (!in_ev && h < nh) { // the next event that needs a parse, finishing the others
 				if (!have) {
-					const bool ready = nx_h == h && nx_st == 4;
+					const bool ready = nx_h == h && nx_st == kNxStages;
 					unsigned long long key;
 					if (ready) {
 						jj = nx_jj;
@@ -1763,8 +1864,7 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 					if (DRY) {
 						nx_h = h + stride;
 					} else {
-						nx_h = atomicAdd(s_next, 1u);
-						nx_h = nx_h < wend ? nx_h : kNone;
+						nx_h = take();
 					}
 					nx_st = 0;
 				}
@@ -1859,7 +1959,7 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 				if (bk < nb && w.tpos == kNone) {
 					const uint32_t wd[4] = {X[k].x, X[k].y, X[k].z, X[k].w};
 					const uint32_t base = 16u * bk - k0;
-					dfa_walk_block(T, A, w, wd, base, pos0 + base, ne);
+					walk_block(tabs, w, wd, base, pos0 + base, ne);
 				}
 			}
 			wi++;
@@ -1887,6 +1987,18 @@ __global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, cons
 			atomicMax(&dw.stat[3], (unsigned long long)mx);
 		}
 	}
+}
+
+// The batch walk (with output) and the exact-LRU rounds' dry walks: one body, two kernels, so
+// that the register budget (EBD_WALK_WPE) binds the batch walk alone; the dry walk kept at the
+// compiler's budget was faster (1 M-event exact LRU: 83 against 87 ms per batch).
+__global__ __launch_bounds__(kWalkThreads) EBD_WALK_ATTR void k_walk(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
+		const uint32_t* hcount) {
+	walk_sessions<false>(d, evf, dw, hlist, hcount);
+}
+__global__ __launch_bounds__(kWalkThreads) void k_walk_dry(Dev d, const uint8_t* evf, DryWalk dw, const uint32_t* hlist,
+		const uint32_t* hcount) {
+	walk_sessions<true>(d, evf, dw, hlist, hcount);
 }
 
 // After a walker: every sorted session event was replayed once (Discovery::handleNewEvent)
@@ -2182,7 +2294,7 @@ __global__ __launch_bounds__(kLruThreads) void k_walk_lru(Dev d, uint32_t nslow,
 // ---------------------------------------------------------------------------------
 // Exact LRU in rounds (the parallel form of k_walk_lru).  A world is a set of evictions, as
 // flags on the session events at which a session finds itself evicted (k_walk's evf).  A
-// round walks sessions in the current world without output (k_walk<true>), which gives every
+// round walks sessions in the current world without output (k_walk_dry), which gives every
 // session event its LRU operation, then derives the evictions those operations imply:
 //  * the LRU's size after each event follows from the operation types alone: an insert makes
 //    it min(cap, L + 1) (a full cache evicts first, LRUCache.h:54-60), an erase L - 1.  Maps
@@ -2841,7 +2953,7 @@ __global__ __launch_bounds__(kPubThreads) void k_walk_heads(Dev d, uint32_t nslo
 		if (a < nslow) {
 			uint32_t prev = a == 0 ? 0xffffffffu : (uint32_t)(d.slow_keys[a - 1] >> 32);
 			for (uint32_t k = 0; k < kHeadsPer && a + k < nslow; k++) {
-				const uint32_t s = (uint32_t)(d.slow_keys[a + k] >> 32);
+				const uint32_t s = (uint32_t)(d.slow_keys[a + k] >> 32); // the session group
 				if (s != prev)
 					mask |= 1u << k;
 				prev = s;
@@ -2857,6 +2969,11 @@ __global__ __launch_bounds__(kPubThreads) void k_walk_heads(Dev d, uint32_t nslo
 		while (mask) {
 			const uint32_t k = (uint32_t)__ffs(mask) - 1u;
 			mask &= mask - 1u;
+			if (d.hrec) { // what k_walk's next-session prefetch would otherwise load in two dependent steps
+				const unsigned long long key = d.slow_keys[a + k];
+				const uint32_t i0 = (uint32_t)key;
+				d.hrec[at] = uint4{(uint32_t)(a + k), i0, d.ev_slot[i0], (uint32_t)(key >> 32)};
+			}
 			d.heads[at++] = (uint32_t)(a + k);
 		}
 		__syncthreads(); // base is rewritten for the next tile
@@ -3741,7 +3858,10 @@ hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
 }
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_walk_heads, dim3(grid_for(nslow, kPubThreads * kHeadsPer, cus * 4)), dim3(kPubThreads), 0, st, d, nslow);
-	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d,
+	hipError_t e = hipMemsetAsync(d.ctr + CTR_COUNT, 0, sizeof(unsigned long long), st); // k_walk's chunk counter
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d,
 			(const uint8_t*)nullptr, DryWalk{}, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 
 	return hipGetLastError();
@@ -3849,7 +3969,7 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 	const LruCtrl* ctl = w.ctl;
 	hipLaunchKernelGGL(k_lru_walklist, dim3(cus * 4), dim3(256), 0, st, d, w.cpos, (const uint32_t*)w.wto, ctl, w.rlist, w.tot, ncf,
 			d.carry_cap);
-	hipLaunchKernelGGL(k_walk<true>, dim3(cus * EBD_WALK_BLOCKS), dim3(kWalkThreads), 0, st, d, f,
+	hipLaunchKernelGGL(k_walk_dry, dim3(cus * kWalkDryBlocks), dim3(kWalkThreads), 0, st, d, f,
 			DryWalk{w.head, (SessState*)w.snap, w.wto, w.opt, ctl, w.stat}, (const uint32_t*)w.rlist, (const uint32_t*)(w.tot + 3));
 	hipLaunchKernelGGL(k_lru_scan, dim3(1), dim3(kScT), 0, st, (const uint8_t*)w.opt, (const uint32_t*)w.mend, n, d.carry_cap, w.bs,
 			w.mk_ref, w.mk_e, w.ev_t, w.evc, w.tot, ctl);
@@ -3867,7 +3987,10 @@ hipError_t launch_lru_round(const Dev& d, uint32_t nslow, const LruRound& w, int
 // The final walk of the exact path in the converged world (with output), then the carried
 // sessions it did not meet.
 hipError_t launch_walk_flags(const Dev& d, uint32_t nslow, const uint8_t* f, const uint8_t* cf, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_walk<false>, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f,
+	const hipError_t e = hipMemsetAsync(d.ctr + CTR_COUNT, 0, sizeof(unsigned long long), st); // k_walk's chunk counter
+	if (e != hipSuccess)
+		return e;
+	hipLaunchKernelGGL(k_walk, dim3(grid_for(nslow, kWalkThreads, cus * EBD_WALK_BLOCKS)), dim3(kWalkThreads), 0, st, d, f,
 			DryWalk{}, (const uint32_t*)nullptr, (const uint32_t*)nullptr);
 	if (d.n_carry_in)
 		hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, cf);

@@ -10,3 +10,10 @@ print(f"waves {len(a)}; per wave: iterations {it.mean():.0f}, active lanes per i
       f"refills {ref.mean():.0f} of {(refl / ref).mean():.1f} lanes, events {evs.mean():.0f}")
 print(f"cycles per wave: walk {blk.mean():.0f}, refill {rc.mean():.0f}, total {tot.mean():.0f}; "
       f"per iteration {(blk / it).mean():.0f}, per refill {(rc / ref).mean():.0f}")
+
+ref = [l.split() for l in open(sys.argv[1]) if l.startswith("WREF")]
+if ref:
+    b = np.array([[int(x) for x in r[3:]] for r in ref], dtype=float)
+    ce, cp, cl, ss, nr = b.T
+    print(f"refill cycles per wave: ending events {ce.mean():.0f}, pipeline stage {cp.mean():.0f}, starting events {cl.mean():.0f}; "
+          f"sessions started per wave {ss.mean():.0f}, before their prefetch finished {nr.mean():.0f}")
