@@ -540,8 +540,9 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
 			c->stream));
 	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes ? c->sort_tmp_bytes : 16));
-	CTX_TRY(hipMalloc(&c->d_carry[0], (size_t)lru * sizeof(Carry)));
-	CTX_TRY(hipMalloc(&c->d_carry[1], (size_t)lru * sizeof(Carry)));
+	// + 64: stream_copy3 reads a carried request's bytes up to 8 past their end
+	CTX_TRY(hipMalloc(&c->d_carry[0], (size_t)lru * sizeof(Carry) + 64));
+	CTX_TRY(hipMalloc(&c->d_carry[1], (size_t)lru * sizeof(Carry) + 64));
 	CTX_TRY(hipMalloc(&c->d_sreq, n * sizeof(SessReq)));
 	c->sstr_cap = n * 160;
 	if (c->sstr_cap < (64ull << 20))

@@ -100,6 +100,7 @@ typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_a1 __attribute__((aligned(1)));
 typedef unsigned long long u64a1 __attribute__((aligned(1)));
 typedef unsigned int u32a1 __attribute__((aligned(1)));
+typedef unsigned short u16a1 __attribute__((aligned(1)));
 // 8 bytes at any alignment: global_load_dwordx2 (gfx950 runs in unaligned-access mode)
 __device__ __forceinline__ unsigned long long gload8u(const uint8_t* a) {
 	return *(const __attribute__((address_space(1))) u64a1*)a;
@@ -1283,12 +1284,40 @@ __device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_
 		b = n[k] && a[k] + n[k] > b ? a[k] + n[k] : b;
 	if (b == 0)
 		return;
+	// 32 bytes at a time: the four 8-byte loads are issued before any store (one memory round
+	// trip per 32 bytes; a load-store pair per 8 bytes and a byte loop for the tail waited on
+	// every load), at in-span offsets (a source is readable 8 bytes past its end); the tail is
+	// stored in 4-, 2- and 1-byte pieces
 	auto copy = [](const uint8_t* src, uint8_t* out, uint32_t len) {
-		uint32_t k = 0;
-		for (; k + 8 <= len; k += 8)
-			*(u64a1*)(out + k) = gload8u(src + k);
-		for (; k < len; k++)
-			out[k] = src[k];
+		for (uint32_t k = 0; k < len; k += 32) {
+			unsigned long long v[4];
+#pragma unroll
+			for (uint32_t m = 0; m < 4; m++)
+				v[m] = gload8u(src + min(k + 8u * m, len - 1u));
+#pragma unroll
+			for (uint32_t m = 0; m < 4; m++) {
+				const uint32_t o = k + 8u * m;
+				if (o + 8u <= len) {
+					*(u64a1*)(out + o) = v[m];
+				} else if (o < len) {
+					uint8_t* p = out + o;
+					unsigned long long x = v[m];
+					const uint32_t t = len - o;
+					if (t & 4u) {
+						*(u32a1*)p = (uint32_t)x;
+						p += 4;
+						x >>= 32;
+					}
+					if (t & 2u) {
+						*(u16a1*)p = (uint16_t)x;
+						p += 2;
+						x >>= 16;
+					}
+					if (t & 1u)
+						*p = (uint8_t)x;
+				}
+			}
+		}
 	};
 	// the spans' parts inside piece [pos, pos + pl), whose bytes start at src
 	auto piece = [&](const uint8_t* src, uint32_t pos, uint32_t pl) {
