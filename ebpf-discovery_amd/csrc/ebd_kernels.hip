@@ -1333,15 +1333,22 @@ __device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_
 		piece(w.cb, 0, w.clen);
 		pos = w.clen;
 	}
-	for (uint32_t j = w.j0; j <= jend && pos < b; j++) {
-		const unsigned long long pc = d.pieces[j]; // the walker's record of the piece (one line for a request's pieces)
-		uint32_t pl = (uint32_t)(pc & 0xffffffu);
-		if (j == jend)
-			pl = cend;
-		if (pl == 0)
-			continue;
-		piece(d.payload + (pc >> 24), pos, pl);
-		pos += pl;
+	// the walker's records of the pieces (one line for a request's pieces), four loaded at a time
+	for (uint32_t j = w.j0; j <= jend && pos < b; j += 4) {
+		unsigned long long pc[4];
+#pragma unroll
+		for (uint32_t m = 0; m < 4; m++)
+			pc[m] = d.pieces[min(j + m, jend)];
+#pragma unroll
+		for (uint32_t m = 0; m < 4; m++) {
+			uint32_t pl = (uint32_t)(pc[m] & 0xffffffu);
+			if (j + m == jend)
+				pl = cend;
+			if (j + m > jend || pos >= b || pl == 0)
+				continue;
+			piece(d.payload + (pc[m] >> 24), pos, pl);
+			pos += pl;
+		}
 	}
 }
 
@@ -1382,12 +1389,19 @@ __device__ void defer_emit(const Dev& d, const Walk& w, uint32_t jend, const Gen
 
 // handleSuccessfulParse -> handleNewRequest -> Aggregator::newRequest
 // (Discovery.cpp:161-192, 210-212) for the session path's request q.
+#ifndef EBD_EMIT_BLOCKS
+#define EBD_EMIT_BLOCKS 8 // k_emit workgroups per CU
+#endif
 __global__ __launch_bounds__(256) void k_emit(Dev d) {
 	__shared__ __attribute__((aligned(8))) uint8_t rows[256 * kCipStride];
 	uint8_t* row = rows + threadIdx.x * kCipStride; // this lane's client-IP value, parsed from LDS
-	const uint32_t nq = (uint32_t)d.ctr[CTR_SREQ];
-	for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-		const EmitRec e = *(const EmitRec*)(d.sreq + q);
+	const uint32_t nq = (uint32_t)d.ctr[CTR_SREQ], stride = gridDim.x * blockDim.x;
+	const uint32_t q0 = blockIdx.x * blockDim.x + threadIdx.x;
+	// the lane's next record is loaded while the current one is emitted
+	EmitRec en = *(const EmitRec*)(d.sreq + (q0 < nq ? q0 : 0u));
+	for (uint32_t q = q0; q < nq; q += stride) {
+		const EmitRec e = en;
+		en = *(const EmitRec*)(d.sreq + (q + stride < nq ? q + stride : q));
 		const uint32_t i = e.i;
 		const Walk w{e.carry ? d.carry_in[e.carry - 1].bytes : nullptr, e.carry ? d.carry_in[e.carry - 1].nbytes : 0u, e.j0};
 		const uint32_t cend = d.res[i].consumed;
@@ -3881,7 +3895,7 @@ hipError_t launch_walk_lru(const Dev& d, uint32_t nslow, uint32_t* jpos, uint32_
 size_t sess_state_bytes() { return sizeof(SessState); }
 // After either walker: the session requests' emission, then the tallies.
 hipError_t launch_emit(const Dev& d, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_emit, dim3(cus * 8), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_emit, dim3(cus * EBD_EMIT_BLOCKS), dim3(256), 0, st, d);
 	hipLaunchKernelGGL(k_sess_tally, dim3(1), dim3(1), 0, st, d);
 	return hipGetLastError();
 }
