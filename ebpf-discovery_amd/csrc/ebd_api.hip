@@ -155,6 +155,9 @@ struct ebd_ctx {
 	uint4* d_hrec = nullptr;                // Dev::hrec (allocated with the first session-path batch)
 	void* d_sort_tmp = nullptr;
 	size_t sort_tmp_bytes = 0;
+	void* d_sel_tmp = nullptr; // compaction of the session-path keys when they are few
+	size_t sel_tmp_bytes = 0;
+	int* d_sel_cnt = nullptr;
 	Carry* d_carry[2] = {nullptr, nullptr};
 	int carry_cur = 0;
 	uint32_t n_carry = 0;
@@ -359,9 +362,19 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 	return t ? t : 1;
 }
 
+// The session-path keys are sorted in place (all n) when at least 1/EBD_SLOW_DENSE of the events
+// take the path, else compacted first (0: always compacted, a test build).
+#ifndef EBD_SLOW_DENSE
+#define EBD_SLOW_DENSE 4
+#endif
+// A session-path key of k_slow_collect (other events hold ~0).
+struct SlowKey {
+	__host__ __device__ bool operator()(unsigned long long k) const { return k != ~0ull; }
+};
+
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
-			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_hrec, c->d_sort_tmp, c->d_carry[0], c->d_carry[1], c->d_sreq,
+			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_hrec, c->d_sort_tmp, c->d_sel_tmp, c->d_sel_cnt, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
 			c->d_v6d[0], c->d_v6d[1], c->d_keep, c->d_kbytes, c->d_remap, c->d_netdump};
@@ -540,6 +553,9 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
 			c->stream));
 	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes ? c->sort_tmp_bytes : 16));
+	CTX_TRY(hipcub::DeviceSelect::If(nullptr, c->sel_tmp_bytes, c->d_slow[0], c->d_slow[1], c->d_sel_cnt, (int)n, SlowKey{}, c->stream));
+	CTX_TRY(hipMalloc(&c->d_sel_tmp, c->sel_tmp_bytes ? c->sel_tmp_bytes : 16));
+	CTX_TRY(hipMalloc(&c->d_sel_cnt, sizeof(int)));
 	// + 64: stream_copy3 reads a carried request's bytes up to 8 past their end
 	CTX_TRY(hipMalloc(&c->d_carry[0], (size_t)lru * sizeof(Carry) + 64));
 	CTX_TRY(hipMalloc(&c->d_carry[1], (size_t)lru * sizeof(Carry) + 64));
@@ -776,16 +792,31 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	const uint64_t dirty = c->h_ctr[CTR_DIRTY];
 	if (nslow > 0) {
 		c->last_slow_ran = 1;
-		int end_bit = 32; // session groups: carried index or carry_cap + first unfinished event
-		while ((1ull << (end_bit - 32)) < (uint64_t)c->carry_cap + c->max_events)
+		// session groups (carried index, or carry_cap + first unfinished event) in bits [32,
+		// end_bit), every group below the all-ones pattern of the ~0 keys of other events
+		int end_bit = 32;
+		while ((1ull << (end_bit - 32)) <= (uint64_t)c->carry_cap + c->max_events)
 			end_bit++;
-		size_t bytes = c->sort_tmp_bytes;
+		// k_slow_collect left every event's key at its index, so the keys enter the sort in event
+		// order and the (stable) radix sort needs only the group bits: 4 passes instead of 8.  When
+		// few events take the session path they are compacted first (order kept).
+		const bool dense = nslow * EBD_SLOW_DENSE >= n;
+		unsigned long long* sorted = dense ? c->d_slow[1] : c->d_slow[0];
 		HIP_TRY(timed(c, KT_SORT, [&] {
-			return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[0], c->d_slow[1], (int)nslow, 0,
-					end_bit, c->stream);
+			size_t bytes = c->sort_tmp_bytes;
+			if (dense)
+				return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[0], c->d_slow[1], (int)n, 32, end_bit,
+						c->stream);
+			size_t sb = c->sel_tmp_bytes;
+			hipError_t e = hipcub::DeviceSelect::If(c->d_sel_tmp, sb, c->d_slow[0], c->d_slow[1], c->d_sel_cnt, (int)n, SlowKey{},
+					c->stream);
+			if (e != hipSuccess)
+				return e;
+			return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[1], c->d_slow[0], (int)nslow, 32, end_bit,
+					c->stream);
 		}));
-		d.slow_keys = c->d_slow[1];
-		d.heads = (uint32_t*)c->d_slow[0]; // the sort's input, free after it
+		d.slow_keys = sorted;
+		d.heads = (uint32_t*)(dense ? c->d_slow[0] : c->d_slow[1]); // the sort's input, free after it
 		if (!c->d_hrec)
 			HIP_TRY(hipMalloc(&c->d_hrec, (size_t)c->max_events * sizeof(uint4)));
 		d.hrec = c->d_hrec;

@@ -1117,18 +1117,17 @@ __global__ __launch_bounds__(256) void k_slow_collect(Dev d) {
 		return; // no session needs the sequential path in this batch
 	const uint32_t tile = 256u * kCollectPer;
 	for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < d.n; t0 += (uint64_t)gridDim.x * tile) { // uniform
-		unsigned long long key[kCollectPer];
 		uint32_t has = 0;
 #pragma unroll
 		for (uint32_t u = 0; u < kCollectPer; u++) {
 			const uint64_t i = t0 + u * 256u + threadIdx.x;
-			key[u] = 0;
 			if (i >= d.n)
 				continue;
+			// every event's key at its own index (~0: not on the session path), so that the keys
+			// enter the sort in event order and the sort (stable) orders only the group bits
+			unsigned long long key = ~0ull;
 			const EventRec& e = d.ev[i];
-			if (!(e.flags & (FLAG_NEW | FLAG_END)))
-				continue;
-			const int slot = sset_find(d, e.pid, e.fd, e.sessionID);
+			const int slot = (e.flags & (FLAG_NEW | FLAG_END)) ? sset_find(d, e.pid, e.fd, e.sessionID) : -1;
 			if (slot >= 0) {
 				d.res[i].info |= EBD_INFO_SESSION; // k_walk's, not k_agg_fast's (which may run first)
 				// grouped by session, sessions in the order of their first UNFINISHED fresh parse
@@ -1137,16 +1136,13 @@ __global__ __launch_bounds__(256) void k_slow_collect(Dev d) {
 				// the session-set slot order (a hash) sent them all over the batch
 				const SSlot& ss = d.sset[slot];
 				const uint32_t grp = ss.carry ? ss.carry - 1 : d.carry_cap + ~ss.first_c;
-				key[u] = ((unsigned long long)grp << 32) | i;
+				key = ((unsigned long long)grp << 32) | i;
 				has |= 1u << u;
 				d.ev_slot[i] = (uint32_t)slot;
 			}
+			d.slow_keys[i] = key;
 		}
-		unsigned long long at = block_reserve(&d.ctr[CTR_SLOW], (uint32_t)__popc(has), part, &base);
-#pragma unroll
-		for (uint32_t u = 0; u < kCollectPer; u++)
-			if (has & (1u << u))
-				d.slow_keys[at++] = key[u];
+		(void)block_reserve(&d.ctr[CTR_SLOW], (uint32_t)__popc(has), part, &base); // the count
 	}
 }
 
