@@ -451,7 +451,9 @@ const char* ebd_strerror(int err) {
 }
 
 int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
-	if (!cfg || !out || cfg->max_events == 0)
+	// lru_capacity: a carried request's index travels in 24 bits (EmitRec); 2^24 carried
+	// sessions would be 140 GB of carry buffers
+	if (!cfg || !out || cfg->max_events == 0 || cfg->lru_capacity >= (1u << 24))
 		return -EINVAL;
 	*out = nullptr;
 	int ndev = 0;

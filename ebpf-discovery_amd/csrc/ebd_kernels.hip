@@ -1356,9 +1356,14 @@ __device__ void stream_copy3(const Dev& d, const Walk& w, uint32_t jend, uint32_
 // for all of the batch's session requests at once in k_emit, on full waves, instead of
 // for the few lanes of a walker wave whose event happened to finish a request.
 struct EmitRec {
-	uint32_t i, jend, j0, carry; // finishing event, its sorted position, the request's first; carried bytes: 1 + index
+	uint32_t i, jend, j0; // finishing event, its sorted position, the request's first
+	uint32_t cc;          // carried bytes (1 + index, bits 0-23; ebd_ctx_create bounds the LRU) | cend bits 8-13 << 24
 	uint16_t host_start, host_len, url_start, url_len, cip_start, cip_len;
-	uint8_t f, mcand, info, pad; // GenParser::f and mcand; the result's info bits so far
+	uint8_t f, mcand, info, cend_lo; // GenParser::f and mcand; the result's info bits so far; cend bits 0-7
+	// the bytes event i's parse consumed (its piece's end in the request), carried here so that
+	// k_emit needs no read of the event's result
+	__device__ __forceinline__ uint32_t carry() const { return cc & 0xffffffu; }
+	__device__ __forceinline__ uint32_t cend() const { return (uint32_t)cend_lo | ((cc >> 24) << 8); }
 };
 static_assert(sizeof(EmitRec) == sizeof(SessReq), "an emission record fills a session-request slot");
 
@@ -1368,7 +1373,10 @@ __device__ void defer_emit(const Dev& d, const Walk& w, uint32_t jend, const Gen
 	e.i = i;
 	e.jend = jend;
 	e.j0 = w.j0;
-	e.carry = w.cb ? (uint32_t)(((const uint8_t*)w.cb - (const uint8_t*)d.carry_in) / sizeof(Carry)) + 1u : 0u;
+	const uint32_t carry = w.cb ? (uint32_t)(((const uint8_t*)w.cb - (const uint8_t*)d.carry_in) / sizeof(Carry)) + 1u : 0u;
+	const uint32_t cend = r.consumed; // at most EBD_BUFFER_MAX_DATA_SIZE: 14 bits
+	e.cc = carry | ((cend >> 8) << 24);
+	e.cend_lo = (uint8_t)cend;
 	e.host_start = (uint16_t)g.host_start;
 	e.host_len = (uint16_t)g.host_len;
 	e.url_start = (uint16_t)g.url_start;
@@ -1378,7 +1386,6 @@ __device__ void defer_emit(const Dev& d, const Walk& w, uint32_t jend, const Gen
 	e.f = g.f;
 	e.mcand = g.mcand;
 	e.info = r.info;
-	e.pad = 0;
 	*(EmitRec*)(d.sreq + q) = e;
 	r.u.session.index = (uint32_t)q;
 }
@@ -1399,8 +1406,9 @@ __global__ __launch_bounds__(256) void k_emit(Dev d) {
 		const EmitRec e = en;
 		en = *(const EmitRec*)(d.sreq + (q + stride < nq ? q + stride : q));
 		const uint32_t i = e.i;
-		const Walk w{e.carry ? d.carry_in[e.carry - 1].bytes : nullptr, e.carry ? d.carry_in[e.carry - 1].nbytes : 0u, e.j0};
-		const uint32_t cend = d.res[i].consumed;
+		const uint32_t carry = e.carry();
+		const Walk w{carry ? d.carry_in[carry - 1].bytes : nullptr, carry ? d.carry_in[carry - 1].nbytes : 0u, e.j0};
+		const uint32_t cend = e.cend();
 		const EventRec& ev = d.ev[i];
 		const uint32_t hl = (e.f & GPF_HOST) ? e.host_len : 0, ul = e.url_len;
 		const uint32_t cl = (e.f & GPF_CIP_FOUND) ? e.cip_len : 0; // the whole first client-IP value
