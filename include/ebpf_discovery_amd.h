@@ -199,7 +199,7 @@ typedef struct ebd_config {
 	uint64_t max_payload;      /* largest payload arena (bytes) of a host batch */
 	uint32_t service_capacity; /* service hash slots (power of two, 0 = default 1<<22) */
 	uint64_t string_arena;     /* bytes for service endpoint strings (0 = default 256 MiB) */
-	uint32_t lru_capacity;     /* 0 = EBD_MAX_SESSIONS (Discovery.cpp:39) */
+	uint32_t lru_capacity;     /* 0 = EBD_MAX_SESSIONS (Discovery.cpp:39); below 2^24 (-EINVAL) */
 	uint32_t flags;            /* EBD_CFG_* */
 	/* Secret key of the 128-bit service-key PRF (SipHash-1-3-128 over pid + endpoint bytes).
 	 * {0, 0} = draw one from getrandom().  Contexts whose tables are merged (shards of one

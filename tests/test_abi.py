@@ -53,6 +53,17 @@ def test_ctx_create_without_gpu_fails_loudly():
         ebd.Context(max_events=16)
 
 
+def test_ctx_create_rejects_an_lru_beyond_the_emission_record():
+    """A carried request's index travels in 24 bits of k_emit's record: ebd_ctx_create refuses
+    lru_capacity >= 2^24 with -EINVAL before it looks for a device (so this runs on CPU too)."""
+    cfg = ebd.Config()
+    cfg.max_events = 16
+    cfg.lru_capacity = 1 << 24
+    h = C.c_void_p()
+    assert ebd.lib().ebd_ctx_create(C.byref(cfg), C.byref(h)) == -22
+    assert not h.value
+
+
 def test_parser_state_init_and_reset_keep_the_client_ip_key():
     """ebd_parser_init / ebd_parser_reset are host-only (HttpRequestParser.cpp:82-83, 374-379):
     reset returns the state machine to METHOD with nothing parsed, and keeps clientIPKey."""
