@@ -38,11 +38,16 @@ __device__ __forceinline__ unsigned long long wave_add(unsigned long long* ctr, 
 	const unsigned long long act = __ballot(1);
 	const uint32_t lane = __lane_id(), leader = (uint32_t)__ffsll((long long)act) - 1u;
 	unsigned long long pre = 0, tot = 0;
-	for (unsigned long long m = act; m; m &= m - 1) { // uniform: the active lanes' sizes, in lane order
-		const uint32_t l = (uint32_t)__ffsll((long long)m) - 1u;
-		const unsigned long long v = __shfl(size, (int)l);
-		pre += l < lane ? v : 0ull;
-		tot += v;
+	if (__ballot(size != 1ull) == 0) { // every size 1 (a constant 1 folds to this path): ranks by mbcnt
+		pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+		tot = (unsigned long long)__popcll(act);
+	} else {
+		for (unsigned long long m = act; m; m &= m - 1) { // uniform: the active lanes' sizes, in lane order
+			const uint32_t l = (uint32_t)__ffsll((long long)m) - 1u;
+			const unsigned long long v = __shfl(size, (int)l);
+			pre += l < lane ? v : 0ull;
+			tot += v;
+		}
 	}
 	unsigned long long base = 0;
 	if (lane == leader)
