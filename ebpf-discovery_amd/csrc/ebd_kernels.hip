@@ -41,6 +41,15 @@ __device__ __forceinline__ unsigned long long wave_add(unsigned long long* ctr, 
 	if (__ballot(size != 1ull) == 0) { // every size 1 (a constant 1 folds to this path): ranks by mbcnt
 		pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
 		tot = (unsigned long long)__popcll(act);
+	} else if (act == ~0ull) { // a full wave: a log-step inclusive scan
+		unsigned long long x = size;
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const unsigned long long y = __shfl_up(x, (unsigned)o);
+			x += lane >= (uint32_t)o ? y : 0ull;
+		}
+		pre = x - size;
+		tot = __shfl(x, 63);
 	} else {
 		for (unsigned long long m = act; m; m &= m - 1) { // uniform: the active lanes' sizes, in lane order
 			const uint32_t l = (uint32_t)__ffsll((long long)m) - 1u;
