@@ -16,9 +16,11 @@
 
 #include "ebd_device.h"
 #include "ebd_fresh.h"
+#include "ebd_scan.h"
 
 namespace ebd {
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_fresh_dfa(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus);
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
@@ -463,6 +465,8 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		return -EINVAL;
 	ebd_ctx* c = new ebd_ctx();
 	c->cfg = *cfg;
+	if (const char* f = std::getenv("EBD_FRESH")) // A/B: EBD_FRESH=dfa runs k_fresh_dfa
+		c->cfg.flags = std::strcmp(f, "dfa") == 0 ? (c->cfg.flags | EBD_CFG_FRESH_DFA) : (c->cfg.flags & ~EBD_CFG_FRESH_DFA);
 	c->device = cfg->device;
 	c->max_events = cfg->max_events;
 	if (hipSetDevice(c->device) != hipSuccess) {
@@ -780,7 +784,9 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		c->batch_valid = 1;
 		return 0;
 	}
-	HIP_TRY(timed(c, KT_FRESH, [&] { return launch_fresh(d, c->stream, c->cus); }));
+	HIP_TRY(timed(c, KT_FRESH, [&] {
+		return (c->cfg.flags & EBD_CFG_FRESH_DFA) ? launch_fresh_dfa(d, c->stream, c->cus) : launch_fresh(d, c->stream, c->cus);
+	}));
 	HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_sset_build(d, c->sset_cap, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
 	HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, CTR_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
@@ -2113,6 +2119,84 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 		key[1] = fr.key.hi;
 	}
 	return 0;
+}
+
+// scan_event's source on the host: the buffer at byte `shift` of a tile whose other bytes
+// are "\r\n" filler (the most hostile bytes to find past a buffer: they can end a request),
+// with the tile's piece bitmap computed as k_fresh's wave computes it.
+struct HostTile {
+	std::vector<uint8_t> t;
+	std::vector<unsigned long long> nv;
+	uint8_t nc[256];
+	uint32_t byte(uint32_t p) const { return t[p]; }
+	uint32_t dw(uint32_t p) const {
+		uint32_t v = 0;
+		for (uint32_t b = 0; b < 4; b++)
+			v |= (uint32_t)t[p + b] << (8 * b);
+		return v;
+	}
+	unsigned long long ld8(uint32_t p) const { return (unsigned long long)dw(p) | ((unsigned long long)dw(p + 4) << 32); }
+	void piece(uint32_t pc, uint32_t (&w)[4]) const {
+		for (uint32_t k = 0; k < 4; k++)
+			w[k] = dw(16 * pc + 4 * k);
+	}
+	unsigned long long nvword(uint32_t j) const { return nv[j]; }
+	uint32_t ncls(uint32_t b) const { return nc[b & 0xffu]; }
+};
+
+int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid, uint8_t flags, const uint8_t* src16,
+		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, const uint64_t hash_key[2],
+		ebd_event_result* out, uint64_t key[2]) {
+	const KeyTrie* trie;
+	if (!host_dfa(&trie) || !out || !hash_key || (len && !buf) || len > EBD_BUFFER_MAX_DATA_SIZE || shift > 15)
+		return -EINVAL;
+	static Interfaces ifs;
+	fill_ifs(ifs, v4, n4, v6, n6);
+	HostTile s;
+	const uint32_t pieces = (shift + len + 15) / 16 + 4;
+	s.t.assign(16 * pieces, 0);
+	for (uint32_t k = 0; k < s.t.size(); k++)
+		s.t[k] = (k & 1) ? '\n' : '\r';
+	if (len)
+		std::memcpy(s.t.data() + shift, buf, len);
+	s.nv.assign((pieces + 63) / 64, 0ull);
+	for (uint32_t pc = 0; pc < pieces; pc++) {
+		uint32_t w[4];
+		s.piece(pc, w);
+		if (nv4(w[0]) | nv4(w[1]) | nv4(w[2]) | nv4(w[3]))
+			s.nv[pc >> 6] |= 1ull << (pc & 63);
+	}
+	for (uint32_t b = 0; b < 256; b++)
+		s.nc[b] = (uint8_t)(~trie->cls[b] & 0x1fu);
+	ScanOut o;
+	scan_event(s, shift, len, o);
+	const bool slow = o.slow != 0;
+	if (slow)
+		scan_slow(s, trie, shift, len, o);
+	ebd_event_result r = scan_result(o, flags);
+	Hash128 h{0, 0};
+	if (r.status == EBD_STATUS_FINISHED) {
+		const auto& sp = r.u.span;
+		h = endpoint_key<2>(HashKey{hash_key[0], hash_key[1]}, pid, sp.host_off, sp.host_len, sp.url_off, sp.url_len,
+				[&](uint32_t o8) { return s.ld8(shift + o8); });
+		uint8_t zero[16] = {0};
+		if (!(r.info & EBD_INFO_CIP)) { // what k_fresh does for this event
+			r.info = (uint8_t)(r.info | (classify_source(ifs, flags, src16 ? src16 : zero) << EBD_INFO_CLASS_SHIFT));
+		} else { // what k_agg_fast (cip_classify) does for this event
+			uint32_t tb, te;
+			uint8_t cls;
+			cip_token(ifs, [buf](uint32_t b) { return (uint32_t)buf[b]; }, r.u.span.cip_off, r.consumed, &tb, &te, &cls);
+			r.u.span.cip_off = (uint16_t)tb;
+			r.u.span.cip_len = (uint16_t)(te - tb);
+			r.info = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT));
+		}
+	}
+	*out = r;
+	if (key) {
+		key[0] = h.lo;
+		key[1] = h.hi;
+	}
+	return slow ? 1 : 0;
 }
 
 int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,

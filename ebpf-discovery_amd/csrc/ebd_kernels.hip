@@ -17,6 +17,7 @@
 
 #include "ebd_device.h"
 #include "ebd_fresh.h"
+#include "ebd_scan.h"
 
 namespace ebd {
 
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(kFreshThreads)
 #if EBD_FRESH_WGS > 1
 __attribute__((amdgpu_waves_per_eu(EBD_FRESH_WGS * kFreshThreads / 256, 8)))
 #endif
-void k_fresh(Dev d) {
+void k_fresh_dfa(Dev d) {
 	__shared__ __attribute__((aligned(16))) FreshLds lds;
 	uint8_t* T = lds.T;
 	FreshShared& sh = lds.sh;
@@ -1038,6 +1039,230 @@ void k_fresh(Dev d) {
 	}
 	if (lane == 0)
 		atomicAdd(&sh.scan_done, 1u);
+}
+
+// ---------------------------------------------------------------------------------
+// k_fresh: the structural scan (ebd_scan.h) over LDS tiles of whole buffers.
+//
+// Every workgroup is one wave with a contiguous range of the batch and no partner: it never
+// waits for another wave.  Per tile:
+//   1. the next up-to-64 events' words are in the lanes (loaded one tile ahead); a prefix sum
+//      of their 16-byte piece counts takes the events whose buffers fit kTileBytes;
+//   2. the buffers land in the wave's LDS tile in one LDS-DMA stream (global_load_lds, 16 B
+//      per lane, consecutive: the whole-line read shape) when they lie back to back in the
+//      payload, as a batch from the ring buffer does; other layouts are copied buffer by buffer;
+//   3. the wave marks the pieces that hold a byte outside [0x20, 0x7e] (nv4 + __ballot: one
+//      64-bit word per 1 KiB of tile);
+//   4. each lane scans one buffer from LDS (scan_event): request line, header keys, Host and
+//      client-IP values byte-class-tested 16 bytes at a time, other header values skipped to
+//      their CR through the piece bitmap;
+//   5. result, key and client class go out in event order (16-B rows of consecutive lanes:
+//      whole lines), UNFINISHED events to the session list through an LDS ring, 256 at a time.
+// The payload is read once, from HBM, in lines; everything after the DMA is LDS traffic.
+// ---------------------------------------------------------------------------------
+#ifndef EBD_SCAN_TILE
+#define EBD_SCAN_TILE 16384
+#endif
+#ifndef EBD_SCAN_WGS
+#define EBD_SCAN_WGS 8 // one-wave workgroups per CU (LDS-bound: 8 x 18.4 KiB)
+#endif
+constexpr uint32_t kTileBytes = EBD_SCAN_TILE, kTilePieces = kTileBytes / 16, kTileWords = kTilePieces / 64;
+static_assert(kTilePieces % 64 == 0 && kTilePieces >= (EBD_BUFFER_MAX_DATA_SIZE + 30) / 16, "a tile holds any one buffer");
+constexpr uint32_t kUnfRing = 512; // UNFINISHED events waiting to be listed (a flush takes 256)
+
+struct ScanLds {
+	uint8_t tile[kTileBytes + 64]; // + reads a few bytes past the last buffer (key words, protocol)
+	unsigned long long nvw[kTileWords];
+	uint8_t ncls[256]; // ~byte_class (ebd_scan.h NB_*)
+	uint32_t unf[kUnfRing];
+};
+
+// scan_event's source: the wave's tile in LDS.
+struct TileSrc {
+	const uint8_t* t;
+	const unsigned long long* nv;
+	const uint8_t* nc;
+	__device__ __forceinline__ uint32_t byte(uint32_t p) const { return t[p]; }
+	__device__ __forceinline__ uint32_t dw(uint32_t p) const {
+		const uint32_t* a = (const uint32_t*)(t + (p & ~3u));
+		return __builtin_amdgcn_alignbyte(a[1], a[0], p & 3u);
+	}
+	__device__ __forceinline__ unsigned long long ld8(uint32_t p) const {
+		const uint32_t* a = (const uint32_t*)(t + (p & ~3u));
+		const uint32_t x0 = a[0], x1 = a[1], x2 = a[2];
+		return (unsigned long long)__builtin_amdgcn_alignbyte(x1, x0, p & 3u) |
+				((unsigned long long)__builtin_amdgcn_alignbyte(x2, x1, p & 3u) << 32);
+	}
+	__device__ __forceinline__ void piece(uint32_t pc, uint32_t (&w)[4]) const {
+		const uint4 v = *(const uint4*)(t + 16 * pc);
+		w[0] = v.x;
+		w[1] = v.y;
+		w[2] = v.z;
+		w[3] = v.w;
+	}
+	__device__ __forceinline__ unsigned long long nvword(uint32_t j) const { return nv[j]; }
+	__device__ __forceinline__ uint32_t ncls(uint32_t b) const { return nc[b]; }
+};
+
+// An event's words as a lane of k_fresh holds them (Discovery.cpp:92-110: flags, pid, the
+// saved buffer; the source address classifies a client without a client-IP header).
+struct ScanMeta {
+	uint32_t L, pid, fw, valid; // fw: the event's word at byte 32 (flags in its low byte)
+	unsigned long long off;
+	uint32_t src[4];
+};
+
+// Branch-free: a position past the range loads event rb's words (marked invalid), so every
+// call issues the same loads.
+__device__ __forceinline__ ScanMeta scan_meta(const Dev& d, uint32_t i, uint32_t rb, uint32_t re) {
+	ScanMeta m;
+	m.valid = i < re ? 1u : 0u;
+	const uint32_t j = i < re ? i : rb;
+	const uint8_t* e = (const uint8_t*)(d.ev + j);
+	m.pid = *(const uint32_t*)e;
+	const v4u s = *(const __attribute__((address_space(1))) v4u_a1*)(e + 16);
+	m.src[0] = s.x;
+	m.src[1] = s.y;
+	m.src[2] = s.z;
+	m.src[3] = s.w;
+	m.fw = *(const uint32_t*)(e + 32);
+	m.L = d.len[j];
+	m.off = d.off[j];
+	return m;
+}
+
+__global__ __launch_bounds__(64) void k_fresh(Dev d) {
+	__shared__ __attribute__((aligned(16))) ScanLds lds;
+	const uint32_t lane = threadIdx.x;
+	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
+	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per);
+	((uint32_t*)lds.ncls)[lane] = ~((const uint32_t*)d.trie->cls)[lane] & 0x1f1f1f1fu;
+	const TileSrc src{lds.tile, lds.nvw, lds.ncls};
+	uint32_t uh = 0, un = 0; // the UNFINISHED ring: head and entries (wave-uniform)
+	uint32_t base = rb;
+	ScanMeta m = scan_meta(d, base + lane, rb, re);
+	while (base < re) {
+		const uint32_t flags = m.fw & 0xffu;
+		const bool has = m.valid && (flags & FLAG_NEW) && m.L != EBD_NO_BUFFER; // Discovery.cpp:92-110
+		const bool bad = has && !buf_in(d, m.L, m.off);
+		const bool parse = has && !bad && m.L > 0;
+		const unsigned long long a = (unsigned long long)(uintptr_t)(d.payload + (parse ? m.off : 0ull));
+		const uint32_t np = parse ? (uint32_t)(((a & 15u) + m.L + 15u) >> 4) : 0u;
+		uint32_t S = np; // inclusive prefix of the piece counts
+#pragma unroll
+		for (int o = 1; o < 64; o <<= 1) {
+			const uint32_t y = __shfl_up(S, (unsigned)o, 64);
+			S += lane >= (uint32_t)o ? y : 0u;
+		}
+		const uint32_t k = (uint32_t)__popcll(__ballot(m.valid && S <= kTilePieces)); // >= 1: a buffer fits alone
+		const bool mine = lane < k;
+		const uint32_t P = S - np; // the buffer's first tile piece
+		const uint32_t N = __shfl(S, (int)k - 1);
+		const ScanMeta nm = scan_meta(d, base + k + lane, rb, re); // the next tile's events
+		if (N > 0) {
+			const unsigned long long a16 = a & ~15ull, g = a16 - 16ull * P;
+			const unsigned long long act = __ballot(mine && np > 0);
+			const unsigned long long g0 = __shfl(g, __ffsll((long long)act) - 1);
+			if (__ballot(mine && np > 0 && g != g0) == 0) { // back to back: one stream of N pieces
+				for (uint32_t j0 = 0; j0 < N; j0 += 64)
+					if (j0 + lane < N)
+						__builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(uintptr_t)(g0 + 16ull * (j0 + lane)),
+								(__attribute__((address_space(3))) void*)(lds.tile + 16 * j0), 16, 0, 0);
+			} else { // buffer by buffer, through registers
+				uint32_t mx = mine ? np : 0u;
+#pragma unroll
+				for (int o = 32; o > 0; o >>= 1)
+					mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+				for (uint32_t q = 0; q < mx; q += 4) {
+					Chunk c[4];
+#pragma unroll
+					for (uint32_t t = 0; t < 4; t++)
+						if (mine && q + t < np)
+							c[t] = gload16((uintptr_t)(a16 + 16ull * (q + t)));
+#pragma unroll
+					for (uint32_t t = 0; t < 4; t++)
+						if (mine && q + t < np)
+							*(uint4*)(lds.tile + 16 * (P + q + t)) = make_uint4(c[t].w[0], c[t].w[1], c[t].w[2], c[t].w[3]);
+				}
+			}
+		}
+		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+		wave_sync();
+		// the piece bitmap: bit j of word w = piece 64 w + j holds a byte outside [0x20, 0x7e]
+		for (uint32_t j0 = 0; j0 < N; j0 += 64) {
+			const uint4 v = *(const uint4*)(lds.tile + 16 * min(j0 + lane, N - 1));
+			const unsigned long long b = __ballot((nv4(v.x) | nv4(v.y) | nv4(v.z) | nv4(v.w)) != 0u);
+			if (lane == 0)
+				lds.nvw[j0 >> 6] = b;
+		}
+		wave_sync();
+		bool unf = false;
+		if (mine) {
+			const uint32_t i = base + lane;
+			ebd_event_result r;
+			Hash128 key{0, 0};
+			if (parse) {
+				const uint32_t B = 16 * P + (uint32_t)(a & 15u);
+				ScanOut o;
+				scan_event(src, B, m.L, o);
+				if (o.slow)
+					scan_slow(src, d.trie, B, m.L, o);
+				r = scan_result(o, (uint8_t)flags);
+				if (o.status == EBD_STATUS_FINISHED) {
+					key = endpoint_key<2>(d.hkey, m.pid, o.host_off, o.host_len, o.url_off, o.url_len,
+							[&](uint32_t x) { return src.ld8(B + x); });
+					if (!(o.info & EBD_INFO_CIP)) { // the client is the session's source address (Aggregator.cpp:57-63)
+						uint8_t s16[16];
+						__builtin_memcpy(s16, m.src, 16);
+						r.info = (uint8_t)(r.info | (classify_source(*d.ifs, (uint8_t)flags, s16) << EBD_INFO_CLASS_SHIFT));
+					}
+				}
+				unf = o.status == EBD_STATUS_UNFINISHED;
+			} else {
+				// an empty buffer: a fresh parser consumes nothing and waits (Discovery.cpp:148-150);
+				// no buffer (or one out of range): no parse at all
+				if (bad)
+					set_error(d, EBD_ERR_BAD_INPUT);
+				unf = has && !bad;
+				r.consumed = 0;
+				r.status = unf ? EBD_STATUS_UNFINISHED : EBD_STATUS_NONE;
+				r.info = 0;
+				r.u.span.url_off = r.u.span.url_len = r.u.span.host_off = r.u.span.host_len = r.u.span.cip_off = r.u.span.cip_len = 0;
+			}
+			d.res[i] = r;
+			d.keys[i] = key;
+		}
+		// UNFINISHED events to the session-set list (k_sset_build), 256 per counter atomic
+		const unsigned long long ub = __ballot(unf);
+		if (unf)
+			lds.unf[(uh + un + __builtin_amdgcn_mbcnt_hi((uint32_t)(ub >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ub, 0))) &
+					(kUnfRing - 1)] = base + lane;
+		un += (uint32_t)__popcll(ub);
+		if (un >= kUnfRing / 2) {
+			wave_sync();
+			unsigned long long at = 0;
+			if (lane == 0)
+				at = atomicAdd(&d.ctr[CTR_UNFINISHED], (unsigned long long)(kUnfRing / 2));
+			at = __shfl(at, 0);
+			for (uint32_t t = 0; t < kUnfRing / 2; t += 64)
+				d.ev_slot[at + t + lane] = lds.unf[(uh + t + lane) & (kUnfRing - 1)];
+			uh += kUnfRing / 2;
+			un -= kUnfRing / 2;
+			wave_sync();
+		}
+		base += k;
+		m = nm;
+	}
+	wave_sync();
+	if (un) {
+		unsigned long long at = 0;
+		if (lane == 0)
+			at = atomicAdd(&d.ctr[CTR_UNFINISHED], (unsigned long long)un);
+		at = __shfl(at, 0);
+		for (uint32_t t = 0; t < un; t += 64)
+			if (t + lane < un)
+				d.ev_slot[at + t + lane] = lds.unf[(uh + t + lane) & (kUnfRing - 1)];
+	}
 }
 
 // ---------------------------------------------------------------------------------
@@ -3877,11 +4102,19 @@ static uint32_t agg_grid(uint32_t n, int cus) {
 } // k_pub_scan: <= 2048
 uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n, agg_grid(n, cus)) * kAggThreads; }
 
-hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
+hipError_t launch_fresh_dfa(const Dev& d, hipStream_t st, int cus) {
 	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
 	const uint64_t groups = ((uint64_t)d.n + kFreshThreads * 4 - 1) / (kFreshThreads * 4);
 	const int grid = (int)(groups < (uint64_t)cus * EBD_FRESH_WGS ? groups : (uint64_t)cus * EBD_FRESH_WGS);
-	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
+	hipLaunchKernelGGL(k_fresh_dfa, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
+	return hipGetLastError();
+}
+hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
+	// one-wave workgroups, EBD_SCAN_WGS per CU (LDS-bound), each a contiguous range of at
+	// least 256 events
+	const uint64_t groups = ((uint64_t)d.n + 255) / 256;
+	const int grid = (int)(groups < (uint64_t)cus * EBD_SCAN_WGS ? groups : (uint64_t)cus * EBD_SCAN_WGS);
+	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(64), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus) {

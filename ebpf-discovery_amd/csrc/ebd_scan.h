@@ -1,0 +1,374 @@
+// ebd_scan.h — the fast path as a structural scan: HttpRequestParser::parse of one buffer by
+// a fresh parser (Discovery.cpp:141-159 handleNewSession), computed from delimiter positions
+// instead of a byte-at-a-time state machine.  Written once for the GPU kernel (k_fresh: the
+// buffer sits in an LDS tile, ebd_kernels.hip) and its host twin (ebd_host_scan).
+//
+// A fresh parse of a buffer is a short sequence of spans, each with one byte class
+// (P = libhttpparser/src/HttpRequestParser.cpp):
+//   "GET /" | "POST /"                        P:162-199  (any other byte: INVALID there)
+//   URL bytes, then ' '                        P:201-213  class U (C_URL)
+//   "HTTP/1.0" | "HTTP/1.1", CR, LF            P:215-262
+//   per header line:  key ':' SP* value CR LF  P:264-352  key class K, value V / H / C
+//   CR LF                                      P:264-267, P:354-364
+// so the result is fixed by the first byte of each span that leaves the span's class.  The
+// scan finds those bytes span by span:
+//   * header values of other keys (the bulk of a request: User-Agent, Accept ...) need only
+//     the first byte outside [0x20, 0x7e] (class V is exactly the printable bytes, P:33).
+//     Those bytes are located once per 16-byte piece for the whole tile, by every lane of the
+//     wave over consecutive pieces (nv4 + __ballot: one bit per piece, `nvword`), so a value
+//     of any length costs one bitmap word and one piece;
+//   * the short spans (URL, keys, Host and client-IP values) are tested byte by byte against
+//     the class table, 16 bytes at a time.
+// The spans are taken in stream order and each search ends at the first byte outside its
+// class, so the first such byte of the whole request is the one the reference stops at: the
+// result is exact.  One shape is left to the generic parser (scan_slow): a header key that
+// holds a space (P:268-270 skips it, which changes the key the Host / client-IP tests see).
+#pragma once
+
+#include "../../include/ebpf_discovery_amd.h"
+#include "ebd_spec.h"
+
+namespace ebd {
+
+// SWAR over 4 bytes: bit 7 of every byte outside [0x20, 0x7e], the bytes that are not C_VAL
+// (P:33, P:47-65 in the C locale; bytes >= 0x80 are in no class).  Exact per byte: the low 7
+// bits plus 0x60 (0x01) carry into bit 7 exactly when they are >= 0x20 (== 0x7f).
+EBD_HD uint32_t nv4(uint32_t w) {
+	const uint32_t y = w & 0x7f7f7f7fu;
+	return (w | ~(y + 0x60606060u) | (y + 0x01010101u)) & 0x80808080u;
+}
+
+// First flagged byte at or after byte lo of a 16-byte piece given as four nv4 words; 16 if none.
+EBD_HD uint32_t first_flag16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3, uint32_t lo) {
+	unsigned long long a = f0 | ((unsigned long long)f1 << 32), b = f2 | ((unsigned long long)f3 << 32);
+	a &= lo >= 8 ? 0ull : (~0ull << (8 * lo));
+	b &= lo <= 8 ? ~0ull : (~0ull << (8 * (lo - 8)));
+	return a ? ((uint32_t)__builtin_ctzll(a) >> 3) : b ? 8u + ((uint32_t)__builtin_ctzll(b) >> 3) : 16u;
+}
+
+// Bit numbers of the classes in the inverted class table (ncls[b] = ~byte_class(b)).
+enum : uint32_t { NB_URL = 0, NB_KEY = 1, NB_VAL = 2, NB_HOST = 3, NB_CIP = 4 };
+static_assert(C_URL == 1u << NB_URL && C_KEY == 1u << NB_KEY && C_VAL == 1u << NB_VAL && C_HOST == 1u << NB_HOST &&
+				C_CIP == 1u << NB_CIP,
+		"class bits");
+
+// The source of a scan (tile coordinates: the buffer is bytes [B, B + L)):
+//   byte(p), dw(p) (4 bytes at any p), ld8(p), piece(pc, w) (bytes [16 pc, 16 pc + 16)),
+//   nvword(j) (bit i: piece 64 j + i holds a byte outside [0x20, 0x7e]), ncls(b).
+// Bytes past the buffer are whatever the tile holds there; every search is bounded by E.
+
+// First position in [p, e) whose byte is not in class `bit`; e if none (P:47-65).
+template <typename Src>
+EBD_HD uint32_t first_not(const Src& s, uint32_t p, uint32_t e, uint32_t bit) {
+	for (uint32_t pc = p >> 4; 16 * pc < e; pc++) {
+		uint32_t w[4];
+		s.piece(pc, w);
+		uint32_t m = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < 16; k++)
+			m |= ((s.ncls((w[k >> 2] >> (8 * (k & 3))) & 0xffu) >> bit) & 1u) << k;
+		if (16 * pc < p)
+			m &= 0xffffu << (p & 15u);
+		if (m) {
+			const uint32_t r = 16 * pc + (uint32_t)__builtin_ctz(m);
+			return r < e ? r : e;
+		}
+	}
+	return e;
+}
+
+// First position in [p, e) whose byte is outside [0x20, 0x7e]; e if none.  Pieces without
+// such a byte are skipped 64 at a time through the tile's piece bitmap.
+template <typename Src>
+EBD_HD uint32_t first_nv(const Src& s, uint32_t p, uint32_t e) {
+	uint32_t pc = p >> 4;
+	while (16 * pc < e) {
+		const uint32_t j = pc >> 6;
+		const unsigned long long wd = s.nvword(j) & (~0ull << (pc & 63u));
+		if (!wd) {
+			pc = (j + 1) << 6;
+			continue;
+		}
+		pc = (j << 6) + (uint32_t)__builtin_ctzll(wd);
+		if (16 * pc >= e)
+			break;
+		uint32_t w[4];
+		s.piece(pc, w);
+		const uint32_t f = first_flag16(nv4(w[0]), nv4(w[1]), nv4(w[2]), nv4(w[3]), 16 * pc < p ? (p & 15u) : 0u);
+		if (f < 16) {
+			const uint32_t r = 16 * pc + f;
+			return r < e ? r : e;
+		}
+		pc++;
+	}
+	return e;
+}
+
+// 4 bytes of a literal (little-endian), and its letter bytes (0x20 each): a key byte b
+// matches a lower-case letter c iff (b | 0x20) == c (P:280 lower-cases with tolower, which
+// only changes 'A'..'Z'), and any other literal byte only by itself.
+constexpr uint32_t lit_word(const char* s, uint32_t n, uint32_t i) {
+	uint32_t w = 0;
+	for (uint32_t k = 0; k < 4; k++)
+		if (4 * i + k < n)
+			w |= (uint32_t)(uint8_t)s[4 * i + k] << (8 * k);
+	return w;
+}
+constexpr uint32_t lit_letters(const char* s, uint32_t n, uint32_t i) {
+	uint32_t m = 0;
+	for (uint32_t k = 0; k < 4; k++)
+		if (4 * i + k < n && s[4 * i + k] >= 'a' && s[4 * i + k] <= 'z')
+			m |= 0x20u << (8 * k);
+	return m;
+}
+constexpr uint32_t lit_valid(uint32_t n, uint32_t i) {
+	return 4 * i + 4 <= n ? 0xffffffffu : 4 * i >= n ? 0u : (0xffffffffu >> (8 * (4 * i + 4 - n)));
+}
+
+// The first n bytes of the key (kd: its first 24 bytes) equal the lower-case literal s.
+template <uint32_t N>
+EBD_HD bool key_is(const uint32_t (&kd)[6], const char (&s)[N]) {
+	constexpr uint32_t n = N - 1;
+	uint32_t x = 0;
+#pragma unroll
+	for (uint32_t i = 0; i < (n + 3) / 4; i++)
+		x |= ((kd[i] | lit_letters(s, n, i)) ^ lit_word(s, n, i)) & lit_valid(n, i);
+	return x == 0;
+}
+
+enum : uint32_t { SK_OTHER = 0, SK_HOST = 1, SK_CLIENT = 2 };
+
+// currentHeader.key lower-cased and cut at 21 bytes (P:276-281, kMaxHeaderKeyLength P:44)
+// against "host" (P:366-368) and the client-IP keys (P:43, P:370-372).  The key has no space
+// here (scan_event leaves such keys to scan_slow), so it is bytes [q, q + n).
+EBD_HD uint32_t key_type(const uint32_t (&kd)[6], uint32_t n) {
+	if (n == 4)
+		return key_is(kd, "host") ? SK_HOST : SK_OTHER;
+	bool c = false;
+	if (n == 11)
+		c = key_is(kd, "x-client-ip");
+	else if (n == 14)
+		c = key_is(kd, "true-client-ip");
+	else if (n == 15)
+		c = key_is(kd, "x-forwarded-for");
+	else if (n == 16)
+		c = key_is(kd, "x-http-client-ip");
+	else if (n >= kMaxHeaderKeyLength) // truncated to 21: only the 21-byte key can match
+		c = key_is(kd, "rproxy_remote_address");
+	return c ? SK_CLIENT : SK_OTHER;
+}
+
+// The outcome of a fresh parse of one buffer (positions relative to the buffer).
+struct ScanOut {
+	uint32_t status;   // EBD_STATUS_UNFINISHED / FINISHED / INVALID
+	uint32_t consumed; // HttpRequestParser::parse's return (P:85-106)
+	uint32_t url_off, url_len, host_off, host_len, cip_off;
+	uint32_t info; // EBD_INFO_POST | EBD_INFO_CIP of a FINISHED request
+	uint32_t slow; // a header key holds a space: scan_slow decides
+};
+
+EBD_HD void scan_init(ScanOut& o, uint32_t L) {
+	o.status = EBD_STATUS_UNFINISHED;
+	o.consumed = L;
+	o.url_off = o.url_len = o.host_off = o.host_len = o.cip_off = 0;
+	o.info = 0;
+	o.slow = 0;
+}
+
+// P:85-106 for a fresh parser over bytes [B, B + L) (L <= 8192, so the 8193-byte cap at
+// P:88-91 cannot trigger).  INVALID consumes the byte that failed, FINISHED the final LF,
+// an unfinished parse the whole buffer.  The request line and Host/URL spans of a FINISHED
+// request are filled in; a request with a client-IP header gets the raw value start of the
+// first one (P:309-316: for a fresh parser the first client-IP key sets clientIPKey, so its
+// header is the one parsed into clientIp; the token is k_agg_fast's, as on the DFA path).
+template <typename Src>
+EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
+	scan_init(o, L);
+	if (L == 0)
+		return;
+	const uint32_t E = B + L;
+	// P:162-199: the method must stay a prefix of GET / POST until its space, then '/'
+	const bool post = s.byte(B) == 'P';
+	const uint32_t nm = post ? 6u : 5u; // "POST /" | "GET /"
+	{
+		const unsigned long long x = (unsigned long long)s.dw(B) | ((unsigned long long)s.dw(B + 4) << 32);
+		const unsigned long long lit = post ? 0x2f2054534f50ull : 0x2f20544547ull;
+		const unsigned long long d = (x ^ lit) & (nm == 6 ? 0xffffffffffffull : 0xffffffffffull);
+		const uint32_t k = d ? ((uint32_t)__builtin_ctzll(d) >> 3) : nm;
+		if (k < nm && k < L) {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = k + 1;
+			return;
+		}
+		if (L < nm)
+			return;
+	}
+	// P:201-213: URL bytes until the space
+	const uint32_t u0 = B + nm - 1; // the '/'
+	const uint32_t ue = first_not(s, u0 + 1, E, NB_URL);
+	if (ue >= E)
+		return;
+	if (s.byte(ue) != ' ') {
+		o.status = EBD_STATUS_INVALID;
+		o.consumed = ue - B + 1;
+		return;
+	}
+	// P:215-262: "HTTP/1.0" | "HTTP/1.1", CR, LF
+	uint32_t q = ue + 1;
+	{
+		const unsigned long long x = (unsigned long long)s.dw(q) | ((unsigned long long)s.dw(q + 4) << 32);
+		const unsigned long long dx = (x ^ 0x302e312f50545448ull) & ~(1ull << 56); // '0' / '1' differ in bit 0
+		const uint32_t dy = (s.dw(q + 8) ^ 0x0a0du) & 0xffffu;
+		const uint32_t k = dx ? ((uint32_t)__builtin_ctzll(dx) >> 3) : dy ? 8u + ((uint32_t)__builtin_ctz(dy) >> 3) : 10u;
+		const uint32_t avail = E - q;
+		if (k < 10 && k < avail) {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = q + k - B + 1;
+			return;
+		}
+		if (avail < 10)
+			return;
+	}
+	q += 10;
+	bool host_seen = false, cip_seen = false;
+	uint32_t host_off = 0, host_len = 0, cip_off = 0;
+	for (;;) {
+		if (q >= E)
+			return;
+		// P:264-297 HEADER_KEY: key bytes up to ':' (a CR first ends the headers, P:265-267)
+		const uint32_t ke = s.byte(q) == '\r' ? q : first_not(s, q, E, NB_KEY);
+		if (ke >= E)
+			return;
+		const uint32_t ck = s.byte(ke);
+		if (ck == '\r') { // P:354-364 HEADERS_END: LF finishes the request
+			if (ke + 1 >= E)
+				return;
+			if (s.byte(ke + 1) != '\n') {
+				o.status = EBD_STATUS_INVALID;
+				o.consumed = ke + 1 - B + 1;
+				return;
+			}
+			o.status = EBD_STATUS_FINISHED;
+			o.consumed = ke + 1 - B + 1;
+			o.url_off = nm - 1;
+			o.url_len = ue - u0;
+			o.host_off = host_off;
+			o.host_len = host_len;
+			o.cip_off = cip_off;
+			o.info = (post ? EBD_INFO_POST : 0u) | (cip_seen ? EBD_INFO_CIP : 0u);
+			return;
+		}
+		if (ck == ' ') { // P:268-270 skips it: the key is not its bytes
+			o.slow = 1;
+			return;
+		}
+		if (ck != ':') {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = ke - B + 1;
+			return;
+		}
+		const uint32_t kn = ke - q;
+		uint32_t kt = SK_OTHER;
+		if (kn == 4 || kn == 11 || (kn >= 14 && kn <= 16) || kn >= kMaxHeaderKeyLength) {
+			uint32_t kd[6];
+#pragma unroll
+			for (uint32_t i = 0; i < 6; i++)
+				kd[i] = s.dw(q + 4 * i);
+			kt = key_type(kd, kn);
+		}
+		if (kt == SK_HOST && host_seen) { // P:282-287: a second Host
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = ke - B + 1;
+			return;
+		}
+		// P:299-319 SP_BEFORE_VALUE: spaces skipped, then a C_VAL byte (a CR fails: empty value)
+		uint32_t v = ke + 1;
+		while (v < E && s.byte(v) == ' ')
+			v++;
+		if (v >= E)
+			return;
+		if ((s.ncls(s.byte(v)) >> NB_VAL) & 1u) {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = v - B + 1;
+			return;
+		}
+		// P:321-352 HEADER_VALUE up to CR: Host C_HOST, client-IP C_CIP, other keys C_VAL
+		const uint32_t w = kt == SK_HOST ? first_not(s, v + 1, E, NB_HOST)
+				: kt == SK_CLIENT        ? first_not(s, v + 1, E, NB_CIP)
+										 : first_nv(s, v + 1, E);
+		if (w >= E)
+			return;
+		if (s.byte(w) != '\r') {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = w - B + 1;
+			return;
+		}
+		if (w + 1 >= E) // P:248-262 HEADER_NEWLINE
+			return;
+		if (s.byte(w + 1) != '\n') {
+			o.status = EBD_STATUS_INVALID;
+			o.consumed = w + 1 - B + 1;
+			return;
+		}
+		if (kt == SK_HOST) {
+			host_seen = true;
+			host_off = v - B;
+			host_len = w - v;
+		} else if (kt == SK_CLIENT && !cip_seen) {
+			cip_seen = true;
+			cip_off = v - B;
+		}
+		q = w + 2;
+	}
+}
+
+// The generic parser (gp_step, the reference handlers restated) over the same bytes, for the
+// buffers scan_event leaves (a header key with a space).
+template <typename Src>
+EBD_HD void scan_slow(const Src& s, const KeyTrie* trie, uint32_t B, uint32_t L, ScanOut& o) {
+	scan_init(o, L);
+	GenParser g;
+	gp_init(g);
+	uint32_t i = 0;
+	while (i < L) {
+		gp_step(g, trie, s.byte(B + i), i);
+		i++;
+		if (gp_done(g))
+			break;
+	}
+	if (!gp_done(g))
+		return;
+	o.consumed = i;
+	if (g.state != ST_FINISHED) {
+		o.status = EBD_STATUS_INVALID;
+		return;
+	}
+	o.status = EBD_STATUS_FINISHED;
+	o.url_off = g.url_start;
+	o.url_len = g.url_len;
+	if (g.f & GPF_HOST) {
+		o.host_off = g.host_start;
+		o.host_len = g.host_len;
+	}
+	const bool cip = (g.f & (GPF_CIP_FOUND | GPF_IN_CIP)) != 0;
+	o.cip_off = cip ? g.cip_start : 0u;
+	o.info = (s.byte(B) == 'P' ? EBD_INFO_POST : 0u) | (cip ? EBD_INFO_CIP : 0u);
+}
+
+// The per-event result of a scan (status, consumed, spans; POST, HTTPS, CIP bits).
+EBD_HD ebd_event_result scan_result(const ScanOut& o, uint8_t flags) {
+	ebd_event_result r;
+	r.consumed = (uint16_t)o.consumed;
+	r.status = (uint8_t)o.status;
+	const bool fin = o.status == EBD_STATUS_FINISHED;
+	r.info = fin ? (uint8_t)(o.info | ((flags & 16) ? EBD_INFO_HTTPS : 0u)) : (uint8_t)0;
+	r.u.span.url_off = (uint16_t)(fin ? o.url_off : 0u);
+	r.u.span.url_len = (uint16_t)(fin ? o.url_len : 0u);
+	r.u.span.host_off = (uint16_t)(fin ? o.host_off : 0u);
+	r.u.span.host_len = (uint16_t)(fin ? o.host_len : 0u);
+	r.u.span.cip_off = (uint16_t)(fin ? o.cip_off : 0u);
+	r.u.span.cip_len = 0;
+	return r;
+}
+
+} // namespace ebd

@@ -162,6 +162,8 @@ _SIGS = {
     "ebd_host_dfa_next": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_host_fresh": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p, C.c_uint32,
                                  C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "ebd_host_scan": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint8, C.c_void_p, C.c_void_p,
+                                C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ebd_host_gp_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
     "ebd_host_dfa_parse": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint8, C.c_int, C.c_void_p, C.c_void_p]),
     "ebd_host_classify": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_uint8, C.c_void_p, C.c_uint32, C.c_void_p,
@@ -744,6 +746,22 @@ def host_fresh(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_
     _check(lib().ebd_host_fresh(_p(b), len(buf), pid, flags, _p(s), _nets4(v4), len(v4), _nets6(v6), len(v6),
                                 _p(hk), _p(out), _p(key)), "ebd_host_fresh")
     return out[0], (int(key[0]), int(key[1]))
+
+
+def host_scan(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_DATA, src16=bytes(16), v4=(), v6=(),
+              hash_key=None, shift=0, want_slow=False):
+    """The structural fast path (k_fresh, ebd_scan.h) for one buffer at byte `shift` of its tile."""
+    out = np.zeros(1, RESULT_DTYPE)
+    hk = _hkey(hash_key)
+    key = np.zeros(2, np.uint64)
+    b = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+    s = np.frombuffer(src16, np.uint8)
+    v4, v6 = list(v4), list(v6)
+    rc = lib().ebd_host_scan(_p(b), len(buf), shift, pid, flags, _p(s), _nets4(v4), len(v4), _nets6(v6), len(v6),
+                             _p(hk), _p(out), _p(key))
+    _check(min(rc, 0), "ebd_host_scan")
+    res = (out[0], (int(key[0]), int(key[1])))
+    return res + (bool(rc),) if want_slow else res
 
 
 def host_gp_parse(chunks, flags=FLAG_UNENCRYPTED, reset_between=False, walker="gp"):

@@ -38,8 +38,19 @@ def oracle_single(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=(), v6=()):
     return out[0], blob, o.services()
 
 
-def check_fresh_against_oracle(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=(), v6=()):
-    r, key = ebd.host_fresh(buf, pid, flags, src.ljust(16, b"\0"), v4, v6)
+def scan_shifted(shift):
+    """The structural fast path (k_fresh) with the buffer at byte `shift` of its tile."""
+    def f(buf, pid=0, flags=NEW4, src16=bytes(16), v4=(), v6=()):
+        return ebd.host_scan(buf, pid, flags, src16, v4, v6, shift=shift)
+    return f
+
+
+# the DFA fast path (k_fresh_dfa) and the structural scan (k_fresh) at three tile alignments
+FAST_PATHS = {"dfa": ebd.host_fresh, "scan0": scan_shifted(0), "scan7": scan_shifted(7), "scan15": scan_shifted(15)}
+
+
+def check_fresh_against_oracle(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=(), v6=(), fn=ebd.host_fresh):
+    r, key = fn(buf, pid, flags, src.ljust(16, b"\0"), v4, v6)
     o, blob, svcs = oracle_single(buf, flags, src, pid, v4, v6)
     if o["status"] == O_STATUS_UNF:
         assert r["status"] == ebd.STATUS_UNFINISHED, buf
@@ -64,13 +75,15 @@ def check_fresh_against_oracle(buf, flags=NEW4, src=b"\x7f\0\0\1", pid=77, v4=()
 O_STATUS_UNF = 1
 
 
-def test_fresh_reference_vectors(vectors):
+@pytest.mark.parametrize("path", sorted(FAST_PATHS))
+def test_fresh_reference_vectors(vectors, path):
+    fn = FAST_PATHS[path]
     for case in vectors["parser_valid"] + vectors["parser_invalid"]:
         if len(case["chunks"]) == 1:
-            check_fresh_against_oracle(b(case["chunks"][0]), flags=NEW4 | (SSL if case.get("is_https") else 0))
+            check_fresh_against_oracle(b(case["chunks"][0]), flags=NEW4 | (SSL if case.get("is_https") else 0), fn=fn)
     for case in vectors["probe_parser"]:
         if "chunks" in case and len(case["chunks"]) == 1:
-            check_fresh_against_oracle(b(case["chunks"][0]))
+            check_fresh_against_oracle(b(case["chunks"][0]), fn=fn)
 
 
 QUIRKS = [
@@ -113,20 +126,24 @@ QUIRKS = [
 ]
 
 
-def test_fresh_quirks():
+@pytest.mark.parametrize("path", sorted(FAST_PATHS))
+def test_fresh_quirks(path):
+    fn = FAST_PATHS[path]
     for buf in QUIRKS:
-        check_fresh_against_oracle(buf)
-        check_fresh_against_oracle(buf, flags=ebd.FLAG_IPV6 | SSL | ebd.FLAG_NEW_DATA, src=bytes(15) + b"\x01")
+        check_fresh_against_oracle(buf, fn=fn)
+        check_fresh_against_oracle(buf, flags=ebd.FLAG_IPV6 | SSL | ebd.FLAG_NEW_DATA, src=bytes(15) + b"\x01", fn=fn)
 
 
-def test_fresh_generated_config3_sample():
+@pytest.mark.parametrize("path", sorted(FAST_PATHS))
+def test_fresh_generated_config3_sample(path):
+    fn = FAST_PATHS[path]
     ev, lens, offs, payload = ebd.generate_host(3, 3, 0, 4000)
     o = O.Oracle()
     out, blob = o.process(ev, lens, offs, payload)
     pay = payload.tobytes()
     for i in range(len(ev)):
         buf = pay[int(offs[i]):int(offs[i]) + int(lens[i])]
-        r, _ = ebd.host_fresh(buf, int(ev["pid"][i]), int(ev["flags"][i]), ev["sourceIP"][i].tobytes())
+        r, _ = fn(buf, int(ev["pid"][i]), int(ev["flags"][i]), ev["sourceIP"][i].tobytes())
         assert r["consumed"] == out["consumed"][i], i
         assert r["status"] == {1: 1, 2: 2, 3: 3}[int(out["status"][i])], i
         if r["status"] == ebd.STATUS_FINISHED:
