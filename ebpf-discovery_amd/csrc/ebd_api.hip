@@ -187,6 +187,7 @@ struct ebd_ctx {
 	LruRound lr{};              // the exact-LRU rounds' scratch (allocated on first need)
 	void* lr_mem = nullptr;
 	unsigned long long* h_lr = nullptr; // pinned: a round's counters
+	unsigned long long* h_small = nullptr; // pinned: the counts and totals a C-ABI call waits for (kSmall words)
 	uint8_t* h_ps = nullptr;            // pinned: ebd_parse_streams' calls and bytes, both ways
 	size_t h_ps_cap = 0;
 	uint8_t* d_ps = nullptr;            // their device copy (grown as needed, kept)
@@ -259,6 +260,8 @@ struct ebd_ctx {
 	double kt_ms[16] = {0};
 	uint64_t kt_n[16] = {0};
 };
+
+constexpr size_t kSmall = 256; // ebd_ctx::h_small words
 
 static const char* kKernelNames[] = {"k_fresh", "k_sset_build", "k_slow_collect", "sort", "k_walk", "k_carry_pass",
 		"k_agg_fast", "k_publish", "k_sset_clear", "k_verify", "k_clear_used", "k_emit"};
@@ -393,6 +396,8 @@ static void ctx_free(ebd_ctx* c) {
 		(void)hipFree(c->lr.stat);
 	if (c->h_lr)
 		(void)hipHostFree(c->h_lr);
+	if (c->h_small)
+		(void)hipHostFree(c->h_small);
 	if (c->h_ps)
 		(void)hipHostFree(c->h_ps);
 	if (c->d_ps)
@@ -577,6 +582,7 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMemsetAsync(c->d_ctr, 0, (CTR_COUNT + 1) * sizeof(unsigned long long), c->stream));
 	CTX_TRY(hipMalloc(&c->d_cnt, sizeof(unsigned long long)));
 	CTX_TRY(hipHostMalloc(&c->h_ctr, (CTR_COUNT + 1) * sizeof(unsigned long long), hipHostMallocDefault));
+	CTX_TRY(hipHostMalloc(&c->h_small, kSmall * sizeof(unsigned long long), hipHostMallocDefault));
 	CTX_TRY(hipHostMalloc(&c->h_end, CTR_COUNT * sizeof(unsigned long long), hipHostMallocDefault));
 	if (cfg->flags & EBD_CFG_NETWORK_COUNTERS) {
 		c->net_on = 1;
@@ -1512,8 +1518,9 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
 	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, own, own + 64, c->stream, c->cus));
 	unsigned long long h[3 * 64];
-	HIP_TRY(hipMemcpyAsync(h, own, 2 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_small, own, 2 * 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	std::memcpy(h, c->h_small, 2 * 64 * sizeof(unsigned long long));
 	uint64_t total = 0, stotal = 0;
 	for (uint32_t w = 0; w < world; w++) {
 		counts[w] = (uint32_t)h[w];
@@ -1604,7 +1611,7 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(launch_wire_bytes_needed(recs, n, need, nullptr, tmp + 2 * (size_t)n, c->stream, c->cus));
 	HIP_TRY(excl_scan(c, tmp + 2 * (size_t)n, tmp + 3 * (size_t)n, n));
-	unsigned long long last[2] = {0, 0}; // the last record's needed bytes and offset: the total
+	unsigned long long* last = c->h_small; // the last record's needed bytes and offset: the total
 	HIP_TRY(hipMemcpyAsync(&last[0], tmp + 3 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipMemcpyAsync(&last[1], tmp + 4 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1884,25 +1891,26 @@ static int trace_device4(ebd_ctx* c, const ebd_trace_config* t, const GenOut* ou
 	const uint64_t n = t->n;
 	const uint32_t a = t->align ? t->align : 1, J = gen4_J(n);
 	const uint64_t tasks = (uint64_t)kSlots4 * J;
+	ScratchScope scope(c);
 	uint32_t *cnt = nullptr, *st = nullptr;
 	unsigned long long *alen = nullptr, *boff = nullptr;
-	HIP_TRY(hipMallocAsync((void**)&cnt, tasks * 4 + 4, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&st, tasks * 4 + 4, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&alen, n * 8 + 8, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&boff, n * 8 + 8, c->stream));
+	HIP_TRY(scratch_get(c, tasks * 4 + 4, (void**)&cnt));
+	HIP_TRY(scratch_get(c, tasks * 4 + 4, (void**)&st));
+	HIP_TRY(scratch_get(c, n * 8 + 8, (void**)&alen));
+	HIP_TRY(scratch_get(c, n * 8 + 8, (void**)&boff));
 	HIP_TRY(launch_gen4_count(t->seed, J, cnt, c->stream));
 	size_t b1 = 0, b2 = 0;
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, cnt, st, (int)tasks, c->stream)); // wraps mod 2^32: differences stay exact
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, alen, boff, (int)(n + 1), c->stream));
 	void* tmp = nullptr;
-	HIP_TRY(hipMallocAsync(&tmp, (b1 > b2 ? b1 : b2) + 16, c->stream));
+	HIP_TRY(scratch_get(c, (b1 > b2 ? b1 : b2) + 16, &tmp));
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, cnt, st, (int)tasks, c->stream));
 	HIP_TRY(hipMemsetAsync(alen, 0, n * 8 + 8, c->stream));
 	HIP_TRY(launch_gen4_len(c->d_gen, t->seed, J, n, a, st, alen, c->stream));
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, alen, boff, (int)(n + 1), c->stream));
-	unsigned long long total = 0;
-	HIP_TRY(hipMemcpyAsync(&total, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_small, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	const unsigned long long total = c->h_small[0];
 	int rc = 0;
 	if (out) {
 		if (total > out->cap)
@@ -1911,12 +1919,7 @@ static int trace_device4(ebd_ctx* c, const ebd_trace_config* t, const GenOut* ou
 			HIP_TRY(launch_gen4_write(c->d_gen, t->seed, J, n, st, boff, out->ev, out->len, (unsigned long long*)out->off,
 					out->payload, (unsigned long long*)out->gidx, c->stream));
 	}
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
-	HIP_TRY(hipFreeAsync(cnt, c->stream));
-	HIP_TRY(hipFreeAsync(st, c->stream));
-	HIP_TRY(hipFreeAsync(alen, c->stream));
-	HIP_TRY(hipFreeAsync(boff, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream)); // the scratch is the next call's
 	if (n_events)
 		*n_events = (uint32_t)n;
 	if (bytes)
@@ -1932,12 +1935,13 @@ static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out
 	if (t->config == 4)
 		return trace_device4(c, t, out, n_events, bytes);
 	const uint32_t n = t->n, a = t->align ? t->align : 1, cfg = gen_config(t->config);
+	ScratchScope scope(c);
 	unsigned long long *alen = nullptr, *boff = nullptr;
 	uint32_t *keep = nullptr, *pos = nullptr;
-	HIP_TRY(hipMallocAsync((void**)&alen, (size_t)n * 8 + 8, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&boff, (size_t)n * 8 + 8, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&keep, (size_t)n * 4 + 4, c->stream));
-	HIP_TRY(hipMallocAsync((void**)&pos, (size_t)n * 4 + 4, c->stream));
+	HIP_TRY(scratch_get(c, (size_t)n * 8 + 8, (void**)&alen));
+	HIP_TRY(scratch_get(c, (size_t)n * 8 + 8, (void**)&boff));
+	HIP_TRY(scratch_get(c, (size_t)n * 4 + 4, (void**)&keep));
+	HIP_TRY(scratch_get(c, (size_t)n * 4 + 4, (void**)&pos));
 	HIP_TRY(launch_gen_len(c->d_gen, cfg, t->seed, t->first, n, a, t->shard_count, t->shard_index, alen, keep, c->stream));
 	if (t->shard_count <= 1) // every candidate is kept (a kept event may be empty only here)
 		HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)keep, 1, n, c->stream));
@@ -1945,17 +1949,17 @@ static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, alen, boff, (int)n + 1, c->stream));
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, keep, pos, (int)n + 1, c->stream));
 	void* tmp = nullptr;
-	HIP_TRY(hipMallocAsync(&tmp, (b1 > b2 ? b1 : b2) + 16, c->stream));
+	HIP_TRY(scratch_get(c, (b1 > b2 ? b1 : b2) + 16, &tmp));
 	// the (n+1)-th entries become the totals
 	HIP_TRY(hipMemsetAsync(alen + n, 0, 8, c->stream));
 	HIP_TRY(hipMemsetAsync(keep + n, 0, 4, c->stream));
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, alen, boff, (int)n + 1, c->stream));
 	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, keep, pos, (int)n + 1, c->stream));
-	unsigned long long total = 0;
-	uint32_t kept = 0;
-	HIP_TRY(hipMemcpyAsync(&total, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipMemcpyAsync(&kept, pos + n, 4, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_small, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
+	HIP_TRY(hipMemcpyAsync(c->h_small + 1, pos + n, 4, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
+	const unsigned long long total = c->h_small[0];
+	const uint32_t kept = (uint32_t)c->h_small[1];
 	rc = 0;
 	if (out) {
 		if (total > out->cap)
@@ -1964,12 +1968,7 @@ static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out
 			HIP_TRY(launch_gen_write(c->d_gen, cfg, t->seed, t->first, n, keep, pos, boff, out->ev, out->len,
 					(unsigned long long*)out->off, out->payload, (unsigned long long*)out->gidx, c->stream));
 	}
-	HIP_TRY(hipFreeAsync(tmp, c->stream));
-	HIP_TRY(hipFreeAsync(alen, c->stream));
-	HIP_TRY(hipFreeAsync(boff, c->stream));
-	HIP_TRY(hipFreeAsync(keep, c->stream));
-	HIP_TRY(hipFreeAsync(pos, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(hipStreamSynchronize(c->stream)); // the scratch is the next call's
 	if (n_events)
 		*n_events = kept;
 	if (bytes)
@@ -2127,6 +2126,7 @@ int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags
 struct HostTile {
 	std::vector<uint8_t> t;
 	std::vector<unsigned long long> nv;
+	std::vector<uint16_t> cm[CB_N];
 	uint8_t nc[256];
 	uint32_t byte(uint32_t p) const { return t[p]; }
 	uint32_t dw(uint32_t p) const {
@@ -2142,6 +2142,12 @@ struct HostTile {
 	}
 	unsigned long long nvword(uint32_t j) const { return nv[j]; }
 	uint32_t ncls(uint32_t b) const { return nc[b & 0xffu]; }
+	unsigned long long clsword(uint32_t c, uint32_t a) const {
+		unsigned long long v = 0;
+		for (uint32_t k = 0; k < 4; k++)
+			v |= (unsigned long long)(4 * a + k < cm[c].size() ? cm[c][4 * a + k] : 0xffffu) << (16 * k);
+		return v;
+	}
 };
 
 int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid, uint8_t flags, const uint8_t* src16,
@@ -2159,20 +2165,30 @@ int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid
 		s.t[k] = (k & 1) ? '\n' : '\r';
 	if (len)
 		std::memcpy(s.t.data() + shift, buf, len);
+	for (uint32_t b = 0; b < 256; b++)
+		s.nc[b] = (uint8_t)(~trie->cls[b] & 0x1fu);
 	s.nv.assign((pieces + 63) / 64, 0ull);
+	for (uint32_t c = 0; c < CB_N; c++)
+		s.cm[c].assign(pieces, 0);
 	for (uint32_t pc = 0; pc < pieces; pc++) {
-		uint32_t w[4];
+		uint32_t w[4], m[CB_N];
 		s.piece(pc, w);
 		if (nv4(w[0]) | nv4(w[1]) | nv4(w[2]) | nv4(w[3]))
 			s.nv[pc >> 6] |= 1ull << (pc & 63);
+		piece_classes(s, w, m);
+		for (uint32_t c = 0; c < CB_N; c++)
+			s.cm[c][pc] = (uint16_t)m[c];
 	}
-	for (uint32_t b = 0; b < 256; b++)
-		s.nc[b] = (uint8_t)(~trie->cls[b] & 0x1fu);
 	ScanOut o;
-	scan_event(s, shift, len, o);
-	const bool slow = o.slow != 0;
-	if (slow)
-		scan_slow(s, trie, shift, len, o);
+	int path = 0; // 0: scan_fast, 2: scan_event, 1: the generic parser (as k_fresh runs them)
+	if (!scan_fast(s, shift, len, o)) {
+		path = 2;
+		scan_event(s, shift, len, o);
+		if (o.slow) {
+			path = 1;
+			scan_slow(s, trie, shift, len, o);
+		}
+	}
 	ebd_event_result r = scan_result(o, flags);
 	Hash128 h{0, 0};
 	if (r.status == EBD_STATUS_FINISHED) {
@@ -2196,7 +2212,7 @@ int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid
 		key[0] = h.lo;
 		key[1] = h.hi;
 	}
-	return slow ? 1 : 0;
+	return path;
 }
 
 int ebd_host_gp_parse(const uint8_t* data, const uint32_t* chunk_len, uint32_t nchunks, uint8_t flags, int reset_between,
@@ -2281,6 +2297,14 @@ int ebd_parser_init(ebd_parser_state* st) {
 	return 0;
 }
 
+int ebd_parser_state_check(const ebd_parser_state* st, uint64_t stream_len) {
+	if (!st)
+		return -EINVAL;
+	StreamParser sp;
+	std::memcpy(&sp, st, sizeof(sp));
+	return stream_state_ok(sp, stream_len) ? 0 : -EINVAL;
+}
+
 int ebd_parser_reset(ebd_parser_state* st) {
 	if (!st)
 		return -EINVAL;
@@ -2300,11 +2324,11 @@ const char* ebd_client_ip_key_name(uint32_t id) {
 int ebd_parse_streams(ebd_ctx* c, ebd_parse_call* calls, uint32_t n, const uint8_t* data, uint64_t data_len) {
 	if (!c || (n && (!calls || (!data && data_len))))
 		return -EINVAL;
-	for (uint32_t k = 0; k < n; k++) { // every stream inside data, every state from this ABI
+	for (uint32_t k = 0; k < n; k++) { // every stream inside data, every state one this ABI wrote
 		const ebd_parse_call& q = calls[k];
-		GenParser g;
-		std::memcpy(&g, &q.state, sizeof(g));
-		if (q.data_off > data_len || q.data_len > data_len - q.data_off || g.length > q.data_len || g.state > ST_INVALID)
+		StreamParser sp;
+		std::memcpy(&sp, &q.state, sizeof(sp));
+		if (q.data_off > data_len || q.data_len > data_len - q.data_off || !stream_state_ok(sp, q.data_len))
 			return -EINVAL;
 	}
 	if (n == 0)

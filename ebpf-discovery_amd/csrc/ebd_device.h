@@ -168,6 +168,24 @@ struct LruRound {
 	unsigned long long* stat; // EBD_LRU_TRACE only (else null): the walks' statistics, k_walk<true> / k_lru_advance
 };
 
+// ebd_parse_streams' parser (ebd_parser_state's contents): the generic state machine plus
+// HttpRequest::clientIp as positions in the request stream (HttpRequestParser.h:28-39).
+struct StreamParser {
+	GenParser g;
+	uint32_t vstart, vend; // the current client-IP header value (stream positions)
+	uint32_t ntok, dropped;
+	uint32_t tok[EBD_PARSE_MAX_TOKENS][2];
+};
+static_assert(sizeof(StreamParser) <= sizeof(ebd_parser_state), "stream parser fits ebd_parser_state");
+
+// A caller-owned state k_parse_streams may run: every field that indexes something in range
+// (the token list, the key trie, the stream the call sees).  ebd_parse_streams rejects others.
+EBD_HD bool stream_state_ok(const StreamParser& sp, uint64_t stream_len) {
+	const GenParser& g = sp.g;
+	return g.state <= ST_INVALID && g.length <= stream_len && g.key < kTrieNodes && sp.ntok <= EBD_PARSE_MAX_TOKENS &&
+			sp.vstart <= sp.vend && sp.vend <= g.length && g.cipkey <= 5;
+}
+
 struct Dev {
 	// immutable tables
 	const uint8_t* dfa;

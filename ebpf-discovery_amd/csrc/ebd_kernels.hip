@@ -1061,17 +1061,18 @@ void k_fresh_dfa(Dev d) {
 // The payload is read once, from HBM, in lines; everything after the DMA is LDS traffic.
 // ---------------------------------------------------------------------------------
 #ifndef EBD_SCAN_TILE
-#define EBD_SCAN_TILE 16384
+#define EBD_SCAN_TILE 12288
 #endif
 #ifndef EBD_SCAN_WGS
-#define EBD_SCAN_WGS 8 // one-wave workgroups per CU (LDS-bound: 8 x 18.4 KiB)
+#define EBD_SCAN_WGS 8 // one-wave workgroups per CU (LDS-bound: 8 x 19.4 KiB)
 #endif
 constexpr uint32_t kTileBytes = EBD_SCAN_TILE, kTilePieces = kTileBytes / 16, kTileWords = kTilePieces / 64;
 static_assert(kTilePieces % 64 == 0 && kTilePieces >= (EBD_BUFFER_MAX_DATA_SIZE + 30) / 16, "a tile holds any one buffer");
-constexpr uint32_t kUnfRing = 512; // UNFINISHED events waiting to be listed (a flush takes 256)
+constexpr uint32_t kUnfRing = 256; // UNFINISHED events waiting to be listed (a flush takes 128)
 
 struct ScanLds {
 	uint8_t tile[kTileBytes + 64]; // + reads a few bytes past the last buffer (key words, protocol)
+	uint16_t cm[CB_N][kTilePieces]; // class bitmaps: bit i of cm[c][pc] = byte 16 pc + i not in class c
 	unsigned long long nvw[kTileWords];
 	uint8_t ncls[256]; // ~byte_class (ebd_scan.h NB_*)
 	uint32_t unf[kUnfRing];
@@ -1102,6 +1103,8 @@ struct TileSrc {
 	}
 	__device__ __forceinline__ unsigned long long nvword(uint32_t j) const { return nv[j]; }
 	__device__ __forceinline__ uint32_t ncls(uint32_t b) const { return nc[b]; }
+	__device__ __forceinline__ unsigned long long clsword(uint32_t c, uint32_t a) const { return ((const unsigned long long*)cm[c])[a]; }
+	const uint16_t (*cm)[kTilePieces];
 };
 
 // An event's words as a lane of k_fresh holds them (Discovery.cpp:92-110: flags, pid, the
@@ -1131,13 +1134,23 @@ __device__ __forceinline__ ScanMeta scan_meta(const Dev& d, uint32_t i, uint32_t
 	return m;
 }
 
+// scan_event (and the generic parser for a key with a space) for the buffers scan_fast leaves:
+// a call, so that its loops do not take registers from the straight-line path.
+__device__ __attribute__((noinline)) void scan_exact(const uint8_t* t, const unsigned long long* nv, const uint8_t* nc,
+		const uint16_t (*cm)[kTilePieces], const KeyTrie* trie, uint32_t B, uint32_t L, ScanOut& o) {
+	const TileSrc src{t, nv, nc, cm};
+	scan_event(src, B, L, o);
+	if (o.slow)
+		scan_slow(src, trie, B, L, o);
+}
+
 __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 	__shared__ __attribute__((aligned(16))) ScanLds lds;
 	const uint32_t lane = threadIdx.x;
 	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
 	const uint32_t rb = min(d.n, blockIdx.x * per), re = min(d.n, rb + per);
 	((uint32_t*)lds.ncls)[lane] = ~((const uint32_t*)d.trie->cls)[lane] & 0x1f1f1f1fu;
-	const TileSrc src{lds.tile, lds.nvw, lds.ncls};
+	const TileSrc src{lds.tile, lds.nvw, lds.ncls, lds.cm};
 	uint32_t uh = 0, un = 0; // the UNFINISHED ring: head and entries (wave-uniform)
 	uint32_t base = rb;
 	ScanMeta m = scan_meta(d, base + lane, rb, re);
@@ -1188,12 +1201,20 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 		}
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		wave_sync();
-		// the piece bitmap: bit j of word w = piece 64 w + j holds a byte outside [0x20, 0x7e]
+		// the tile's bitmaps, every lane on its own pieces: bit j of nvw[w] = piece 64 w + j holds
+		// a byte outside [0x20, 0x7e]; the class bitmaps cm (ebd_scan.h piece_classes)
 		for (uint32_t j0 = 0; j0 < N; j0 += 64) {
-			const uint4 v = *(const uint4*)(lds.tile + 16 * min(j0 + lane, N - 1));
+			const uint32_t j = min(j0 + lane, N - 1);
+			const uint4 v = *(const uint4*)(lds.tile + 16 * j);
+			const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+			uint32_t cmk[CB_N];
+			piece_classes(src, w, cmk);
 			const unsigned long long b = __ballot((nv4(v.x) | nv4(v.y) | nv4(v.z) | nv4(v.w)) != 0u);
 			if (lane == 0)
 				lds.nvw[j0 >> 6] = b;
+#pragma unroll
+			for (uint32_t c = 0; c < CB_N; c++)
+				lds.cm[c][j] = (uint16_t)cmk[c];
 		}
 		wave_sync();
 		bool unf = false;
@@ -1204,11 +1225,19 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 			if (parse) {
 				const uint32_t B = 16 * P + (uint32_t)(a & 15u);
 				ScanOut o;
-				scan_event(src, B, m.L, o);
-				if (o.slow)
-					scan_slow(src, d.trie, B, m.L, o);
+#ifdef EBD_SX_NOSCAN
+				scan_init(o, m.L);
+				o.status = src.byte(B) == 'Z' ? EBD_STATUS_FINISHED : EBD_STATUS_INVALID;
+#else
+				if (!scan_fast(src, B, m.L, o)) // the shapes scan_fast leaves (ebd_scan.h): rare
+					scan_exact(lds.tile, lds.nvw, lds.ncls, lds.cm, d.trie, B, m.L, o);
+#endif
 				r = scan_result(o, (uint8_t)flags);
+#ifdef EBD_SX_NOKEY
+				if (o.status == EBD_STATUS_FINISHED && src.byte(B) == 'Z') {
+#else
 				if (o.status == EBD_STATUS_FINISHED) {
+#endif
 					key = endpoint_key<2>(d.hkey, m.pid, o.host_off, o.host_len, o.url_off, o.url_len,
 							[&](uint32_t x) { return src.ld8(B + x); });
 					if (!(o.info & EBD_INFO_CIP)) { // the client is the session's source address (Aggregator.cpp:57-63)
@@ -1238,7 +1267,7 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 			lds.unf[(uh + un + __builtin_amdgcn_mbcnt_hi((uint32_t)(ub >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ub, 0))) &
 					(kUnfRing - 1)] = base + lane;
 		un += (uint32_t)__popcll(ub);
-		if (un >= kUnfRing / 2) {
+		if (un >= kUnfRing / 2) { // (un < kUnfRing / 2 + 64 <= kUnfRing entries)
 			wave_sync();
 			unsigned long long at = 0;
 			if (lane == 0)
@@ -3881,13 +3910,6 @@ __global__ void k_agg_requests(Dev d, const ebd_request* rq, uint32_t n, const u
 // what HttpRequest holds beyond the aggregator's needs: every value of a header whose key is
 // result.clientIPKey, split into result.clientIp's tokens at its newline (P:248-262, 381-409).
 // ---------------------------------------------------------------------------------
-struct StreamParser {
-	GenParser g;
-	uint32_t vstart, vend; // the current client-IP header value (stream positions)
-	uint32_t ntok, dropped;
-	uint32_t tok[EBD_PARSE_MAX_TOKENS][2];
-};
-static_assert(sizeof(StreamParser) <= sizeof(ebd_parser_state), "stream parser fits ebd_parser_state");
 
 // parseClientIPValue (P:392-409): boost::split(token_compress_on) on ',' then each token's trim
 // and IPv4 port / IPv6 bracket handling (front_token); tokens appended in order.
@@ -3928,6 +3950,10 @@ __global__ void k_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint
 		ebd_parse_call& c = calls[k];
 		StreamParser sp;
 		__builtin_memcpy(&sp, &c.state, sizeof(sp));
+		// the host checked the state (ebd_parse_streams -> stream_state_ok); kept in bounds here too,
+		// so that no state indexes past the token list or the key trie
+		sp.ntok = min(sp.ntok, (uint32_t)EBD_PARSE_MAX_TOKENS);
+		sp.g.key = sp.g.key < kTrieNodes ? sp.g.key : kTrieDead;
 		GenParser& g = sp.g;
 		const uint8_t* s = data + c.data_off; // stream position p is s[p]
 		const uint32_t end = c.data_len;

@@ -17,8 +17,9 @@
 //     Those bytes are located once per 16-byte piece for the whole tile, by every lane of the
 //     wave over consecutive pieces (nv4 + __ballot: one bit per piece, `nvword`), so a value
 //     of any length costs one bitmap word and one piece;
-//   * the short spans (URL, keys, Host and client-IP values) are tested byte by byte against
-//     the class table, 16 bytes at a time.
+//   * the short spans (URL, keys, Host and client-IP values) are tested against per-byte class
+//     bitmaps, also built once per tile by the whole wave (a class-table lookup per byte and
+//     v_dot4_u32_u8 to gather the bits), so a span of up to 64 bytes costs one bitmap word.
 // The spans are taken in stream order and each search ends at the first byte outside its
 // class, so the first such byte of the whole request is the one the reference stops at: the
 // result is exact.  One shape is left to the generic parser (scan_slow): a header key that
@@ -54,27 +55,65 @@ static_assert(C_URL == 1u << NB_URL && C_KEY == 1u << NB_KEY && C_VAL == 1u << N
 
 // The source of a scan (tile coordinates: the buffer is bytes [B, B + L)):
 //   byte(p), dw(p) (4 bytes at any p), ld8(p), piece(pc, w) (bytes [16 pc, 16 pc + 16)),
-//   nvword(j) (bit i: piece 64 j + i holds a byte outside [0x20, 0x7e]), ncls(b).
+//   nvword(j) (bit i: piece 64 j + i holds a byte outside [0x20, 0x7e]), ncls(b),
+//   clsword(c, a) (the class bitmaps below).
 // Bytes past the buffer are whatever the tile holds there; every search is bounded by E.
 
-// First position in [p, e) whose byte is not in class `bit`; e if none (P:47-65).
+// Class bitmaps of the tile: bit b of word clsword(c, a) is set where tile byte 64 a + b is
+// NOT in class c (c = CB_URL, CB_KEY, CB_HOST, CB_CIP).  They are built once per tile by every
+// lane over consecutive pieces (class_masks16), so a search costs one word per 64 bytes.
+enum : uint32_t { CB_URL = 0, CB_KEY = 1, CB_HOST = 2, CB_CIP = 3, CB_N = 4 };
+
+// The 16-bit "not in class" masks of one 16-byte piece for the four classes, from the inverted
+// class bytes packed four to a word (f[j] byte i = ncls of piece byte 4 j + i): bit n of the
+// class's byte goes to bit 4 j + i by v_dot4_u32_u8 against the weights 1, 2, 4, 8 (and 16 ..
+// 128 for the next word).
+EBD_HD uint32_t dot4u8(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+	for (int i = 0; i < 4; i++)
+		c += ((a >> (8 * i)) & 0xffu) * ((b >> (8 * i)) & 0xffu);
+	return c;
+#endif
+}
+EBD_HD uint32_t class_mask16(const uint32_t (&f)[4], uint32_t nb) {
+	const uint32_t sel = 0x01010101u << nb;
+	const uint32_t lo = dot4u8(f[0] & sel, 0x08040201u, dot4u8(f[1] & sel, 0x80402010u, 0u));
+	const uint32_t hi = dot4u8(f[2] & sel, 0x08040201u, dot4u8(f[3] & sel, 0x80402010u, 0u));
+	return (lo | (hi << 8)) >> nb;
+}
+
+// A piece's four class masks (mask bit i: piece byte i is not in the class), from its words.
 template <typename Src>
-EBD_HD uint32_t first_not(const Src& s, uint32_t p, uint32_t e, uint32_t bit) {
-	for (uint32_t pc = p >> 4; 16 * pc < e; pc++) {
-		uint32_t w[4];
-		s.piece(pc, w);
-		uint32_t m = 0;
+EBD_HD void piece_classes(const Src& s, const uint32_t (&w)[4], uint32_t (&m)[CB_N]) {
+	uint32_t f[4];
 #pragma unroll
-		for (uint32_t k = 0; k < 16; k++)
-			m |= ((s.ncls((w[k >> 2] >> (8 * (k & 3))) & 0xffu) >> bit) & 1u) << k;
-		if (16 * pc < p)
-			m &= 0xffffu << (p & 15u);
-		if (m) {
-			const uint32_t r = 16 * pc + (uint32_t)__builtin_ctz(m);
-			return r < e ? r : e;
-		}
+	for (uint32_t j = 0; j < 4; j++) {
+		const uint32_t x = w[j];
+		f[j] = s.ncls(x & 0xffu) | (s.ncls((x >> 8) & 0xffu) << 8) | (s.ncls((x >> 16) & 0xffu) << 16) | (s.ncls(x >> 24) << 24);
 	}
-	return e;
+	m[CB_URL] = class_mask16(f, NB_URL);
+	m[CB_KEY] = class_mask16(f, NB_KEY);
+	m[CB_HOST] = class_mask16(f, NB_HOST);
+	m[CB_CIP] = class_mask16(f, NB_CIP);
+}
+
+// First position in [p, e) whose byte is not in class c; e if none (P:47-65).
+template <typename Src>
+EBD_HD uint32_t first_not(const Src& s, uint32_t p, uint32_t e, uint32_t c) {
+	if (p >= e)
+		return e;
+	uint32_t a = p >> 6;
+	unsigned long long w = s.clsword(c, a) & (~0ull << (p & 63u));
+	while (!w) {
+		a++;
+		if (64 * a >= e)
+			return e;
+		w = s.clsword(c, a);
+	}
+	const uint32_t r = 64 * a + (uint32_t)__builtin_ctzll(w);
+	return r < e ? r : e;
 }
 
 // First position in [p, e) whose byte is outside [0x20, 0x7e]; e if none.  Pieces without
@@ -140,21 +179,31 @@ enum : uint32_t { SK_OTHER = 0, SK_HOST = 1, SK_CLIENT = 2 };
 
 // currentHeader.key lower-cased and cut at 21 bytes (P:276-281, kMaxHeaderKeyLength P:44)
 // against "host" (P:366-368) and the client-IP keys (P:43, P:370-372).  The key has no space
-// here (scan_event leaves such keys to scan_slow), so it is bytes [q, q + n).
-EBD_HD uint32_t key_type(const uint32_t (&kd)[6], uint32_t n) {
-	if (n == 4)
+// here (scan_event leaves such keys to scan_slow), so it is bytes [q, q + n); only a key of
+// a matching length reads its words.
+template <typename Src>
+EBD_HD uint32_t key_type(const Src& s, uint32_t q, uint32_t n) {
+	uint32_t kd[6];
+	if (n == 4) {
+		kd[0] = s.dw(q);
 		return key_is(kd, "host") ? SK_HOST : SK_OTHER;
-	bool c = false;
-	if (n == 11)
-		c = key_is(kd, "x-client-ip");
-	else if (n == 14)
-		c = key_is(kd, "true-client-ip");
-	else if (n == 15)
-		c = key_is(kd, "x-forwarded-for");
-	else if (n == 16)
-		c = key_is(kd, "x-http-client-ip");
-	else if (n >= kMaxHeaderKeyLength) // truncated to 21: only the 21-byte key can match
+	}
+	if (n != 11 && (n < 14 || n > 16) && n < kMaxHeaderKeyLength)
+		return SK_OTHER;
+#pragma unroll
+	for (uint32_t i = 0; i < 4; i++)
+		kd[i] = s.dw(q + 4 * i);
+	bool c;
+	if (n < kMaxHeaderKeyLength) {
+		c = n == 11 ? key_is(kd, "x-client-ip")
+				: n == 14 ? key_is(kd, "true-client-ip")
+				: n == 15 ? key_is(kd, "x-forwarded-for")
+						  : key_is(kd, "x-http-client-ip");
+	} else { // truncated to 21: only the 21-byte key can match
+		kd[4] = s.dw(q + 16);
+		kd[5] = s.dw(q + 20);
 		c = key_is(kd, "rproxy_remote_address");
+	}
 	return c ? SK_CLIENT : SK_OTHER;
 }
 
@@ -205,7 +254,7 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 	}
 	// P:201-213: URL bytes until the space
 	const uint32_t u0 = B + nm - 1; // the '/'
-	const uint32_t ue = first_not(s, u0 + 1, E, NB_URL);
+	const uint32_t ue = first_not(s, u0 + 1, E, CB_URL);
 	if (ue >= E)
 		return;
 	if (s.byte(ue) != ' ') {
@@ -236,7 +285,7 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 		if (q >= E)
 			return;
 		// P:264-297 HEADER_KEY: key bytes up to ':' (a CR first ends the headers, P:265-267)
-		const uint32_t ke = s.byte(q) == '\r' ? q : first_not(s, q, E, NB_KEY);
+		const uint32_t ke = s.byte(q) == '\r' ? q : first_not(s, q, E, CB_KEY);
 		if (ke >= E)
 			return;
 		const uint32_t ck = s.byte(ke);
@@ -267,15 +316,7 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 			o.consumed = ke - B + 1;
 			return;
 		}
-		const uint32_t kn = ke - q;
-		uint32_t kt = SK_OTHER;
-		if (kn == 4 || kn == 11 || (kn >= 14 && kn <= 16) || kn >= kMaxHeaderKeyLength) {
-			uint32_t kd[6];
-#pragma unroll
-			for (uint32_t i = 0; i < 6; i++)
-				kd[i] = s.dw(q + 4 * i);
-			kt = key_type(kd, kn);
-		}
+		const uint32_t kt = key_type(s, q, ke - q);
 		if (kt == SK_HOST && host_seen) { // P:282-287: a second Host
 			o.status = EBD_STATUS_INVALID;
 			o.consumed = ke - B + 1;
@@ -283,8 +324,14 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 		}
 		// P:299-319 SP_BEFORE_VALUE: spaces skipped, then a C_VAL byte (a CR fails: empty value)
 		uint32_t v = ke + 1;
-		while (v < E && s.byte(v) == ' ')
-			v++;
+		{
+			const uint32_t x = s.dw(v) ^ 0x20202020u; // the first non-space of the next 4 bytes
+			if (x)
+				v += (uint32_t)__builtin_ctz(x) >> 3;
+			else
+				for (v += 4; v < E && s.byte(v) == ' ';)
+					v++;
+		}
 		if (v >= E)
 			return;
 		if ((s.ncls(s.byte(v)) >> NB_VAL) & 1u) {
@@ -292,10 +339,18 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 			o.consumed = v - B + 1;
 			return;
 		}
-		// P:321-352 HEADER_VALUE up to CR: Host C_HOST, client-IP C_CIP, other keys C_VAL
-		const uint32_t w = kt == SK_HOST ? first_not(s, v + 1, E, NB_HOST)
-				: kt == SK_CLIENT        ? first_not(s, v + 1, E, NB_CIP)
-										 : first_nv(s, v + 1, E);
+		// P:321-352 HEADER_VALUE up to CR: other keys' bytes are C_VAL, i.e. printable, so their
+		// CR is the first byte outside [0x20, 0x7e]; Host (C_HOST) and client-IP (C_CIP) values
+		// also fail at their first byte outside their class before it
+		const uint32_t w = first_nv(s, v + 1, E);
+		if (kt != SK_OTHER) {
+			const uint32_t h = first_not(s, v + 1, w, kt == SK_HOST ? CB_HOST : CB_CIP);
+			if (h < w) {
+				o.status = EBD_STATUS_INVALID;
+				o.consumed = h - B + 1;
+				return;
+			}
+		}
 		if (w >= E)
 			return;
 		if (s.byte(w) != '\r') {
@@ -320,6 +375,180 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 		}
 		q = w + 2;
 	}
+}
+
+// ---------------------------------------------------------------------------------
+// scan_fast: scan_event in straight-line form for the common shapes, so that the lanes of a
+// wave (one buffer each) run the same instructions: every search looks at two 64-byte bitmap
+// words (two flagged pieces for a header value of another key, found through the piece
+// bitmap) and each header line is one pass of the loop.  Returns false where a search is not
+// resolved that way (a URL, key, Host or client-IP value of more than 64-127 bytes, a header
+// value running past the next 1-2 KiB of the tile, three spaces after a ':', a space in a
+// key): the caller then runs scan_event, which takes every shape.  Where it returns true the
+// result is scan_event's.
+// ---------------------------------------------------------------------------------
+// v_alignbyte_b32: bytes [k, k + 4) of hi:lo (k = 0..3)
+EBD_HD uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+	return __builtin_amdgcn_alignbyte(hi, lo, k);
+#else
+	return (uint32_t)((((unsigned long long)hi << 32) | lo) >> (8 * k));
+#endif
+}
+
+EBD_HD uint32_t ctz64_or(unsigned long long w, uint32_t none) { return w ? (uint32_t)__builtin_ctzll(w) : none; }
+
+// First flagged byte of class bitmap c at or after p, within the two words from p's: r (<= e).
+// False: neither word has one and the buffer goes on past them.
+template <typename Src>
+EBD_HD bool search2(const Src& s, uint32_t c, uint32_t p, uint32_t e, uint32_t& r) {
+	const uint32_t a = p >> 6;
+	const unsigned long long w0 = s.clsword(c, a) & (~0ull << (p & 63u)), w1 = s.clsword(c, a + 1);
+	const uint32_t x = w0 ? 64 * a + ctz64_or(w0, 64) : 64 * (a + 1) + ctz64_or(w1, 64);
+	r = x < e ? x : e;
+	return (w0 | w1) != 0 || 64 * (a + 2) >= e;
+}
+
+// First byte outside [0x20, 0x7e] at or after p (<= e): the first flagged piece (piece bitmap)
+// and, if its flags all lie before p, the next one.  False: not within two bitmap words.
+template <typename Src>
+EBD_HD bool nv_search2(const Src& s, uint32_t p, uint32_t e, uint32_t& r) {
+	const uint32_t pc0 = p >> 4, j = pc0 >> 6;
+	unsigned long long wd = s.nvword(j) & (~0ull << (pc0 & 63u));
+	uint32_t jb = j;
+	if (!wd) {
+		jb = j + 1;
+		wd = s.nvword(jb);
+	}
+	if (!wd) {
+		r = e;
+		return 1024 * (j + 2) >= e;
+	}
+	uint32_t pc = 64 * jb + (uint32_t)__builtin_ctzll(wd);
+	uint32_t w[4];
+	s.piece(pc, w);
+	uint32_t f = first_flag16(nv4(w[0]), nv4(w[1]), nv4(w[2]), nv4(w[3]), 16 * pc < p ? (p & 15u) : 0u);
+	if (f == 16) { // the flags of p's own piece lie before p: the next flagged piece of the word
+		const unsigned long long wd2 = wd & (wd - 1);
+		if (!wd2) {
+			r = e;
+			return 16 * (64 * jb + 64) >= e;
+		}
+		pc = 64 * jb + (uint32_t)__builtin_ctzll(wd2);
+		s.piece(pc, w);
+		f = first_flag16(nv4(w[0]), nv4(w[1]), nv4(w[2]), nv4(w[3]), 0u);
+	}
+	const uint32_t x = 16 * pc + f;
+	r = x < e ? x : e;
+	return true;
+}
+
+// Outcomes of one step of scan_fast, first match wins (the order is the reference's byte
+// order along the line).
+enum : uint32_t { SF_GO = 0, SF_UNF = 1, SF_FIN = 2, SF_INV = 3, SF_SLOW = 4 };
+
+template <typename Src>
+EBD_HD bool scan_fast(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
+	scan_init(o, L);
+	const uint32_t E = B + L;
+	uint32_t dec = L == 0 ? SF_UNF : SF_GO, pos = 0;
+	auto decide = [&](bool c, uint32_t d, uint32_t p) {
+		const bool t = dec == SF_GO && c;
+		dec = t ? d : dec;
+		pos = t ? p : pos;
+	};
+	// P:162-199 "GET /" | "POST /"
+	const uint32_t m0 = s.dw(B), m1 = s.dw(B + 4);
+	const bool post = (m0 & 0xffu) == 'P';
+	const uint32_t nm = post ? 6u : 5u;
+	{
+		const unsigned long long d = (((unsigned long long)m1 << 32 | m0) ^ (post ? 0x2f2054534f50ull : 0x2f20544547ull)) &
+				(post ? 0xffffffffffffull : 0xffffffffffull);
+		const uint32_t k = d ? ((uint32_t)__builtin_ctzll(d) >> 3) : nm;
+		decide(k < nm && k < L, SF_INV, B + k);
+		decide(L < nm, SF_UNF, 0);
+	}
+	// P:201-213 URL bytes, then ' '; P:215-262 "HTTP/1.0" | "HTTP/1.1" CR LF
+	const uint32_t u0 = B + nm - 1;
+	uint32_t ue;
+	const bool uok = search2(s, CB_URL, u0 + 1, E, ue);
+	{
+		const uint32_t ur = ue < E ? ue : E;
+		const uint32_t p0 = s.dw(ur), p1 = s.dw(ur + 4), p2 = s.dw(ur + 8);
+		const unsigned long long x = (unsigned long long)align_byte(p1, p0, 1) | ((unsigned long long)align_byte(p2, p1, 1) << 32);
+		const unsigned long long dx = (x ^ 0x302e312f50545448ull) & ~(1ull << 56);
+		const uint32_t dy = ((p2 >> 8) ^ 0x0a0du) & 0xffffu;
+		const uint32_t k = dx ? ((uint32_t)__builtin_ctzll(dx) >> 3) : dy ? 8u + ((uint32_t)__builtin_ctz(dy) >> 3) : 10u;
+		const uint32_t avail = E - ur - 1;
+		decide(!uok, SF_SLOW, 0);
+		decide(ue >= E, SF_UNF, 0);
+		decide((p0 & 0xffu) != ' ', SF_INV, ue);
+		decide(k < 10 && k < avail, SF_INV, ue + 1 + k);
+		decide(avail < 10, SF_UNF, 0);
+	}
+	uint32_t q = ue + 11;
+	bool host_seen = false, cip_seen = false;
+	uint32_t host_off = 0, host_len = 0, cip_off = 0;
+	// one header line per pass (P:264-352), every lane through the same instructions
+	while (dec == SF_GO) {
+		uint32_t ke;
+		const bool kok = search2(s, CB_KEY, q, E, ke);
+		const uint32_t kr = ke < E ? ke : E;
+		const uint32_t c4 = s.dw(kr), ck = c4 & 0xffu, c1 = (c4 >> 8) & 0xffu;
+		const uint32_t kt = key_type(s, q, ke - q);
+		const uint32_t nsp = ctz64_or(((c4 >> 8) ^ 0x202020u) & 0xffffffu, 24) >> 3;
+		const uint32_t v = ke + 1 + nsp, bv = (c4 >> (8 * (nsp + 1))) & 0xffu;
+		const uint32_t vs = (v < E ? v : E) + 1;
+		uint32_t wn, wc;
+		const bool nok = nv_search2(s, vs, E, wn);
+		const bool cok = search2(s, kt == SK_HOST ? CB_HOST : CB_CIP, vs, E, wc);
+		const uint32_t w = kt == SK_OTHER ? wn : wc;
+		const bool vok = kt == SK_OTHER ? nok : cok;
+		const uint32_t w4 = s.dw(w < E ? w : E), cw = w4 & 0xffu, cw1 = (w4 >> 8) & 0xffu;
+		decide(q >= E, SF_UNF, 0);
+		decide(!kok, SF_SLOW, 0);
+		decide(ke >= E, SF_UNF, 0);
+		// P:265-267, P:354-364: a CR in the key ends the headers; LF finishes the request
+		decide(ck == '\r' && ke + 1 >= E, SF_UNF, 0);
+		decide(ck == '\r' && c1 == '\n', SF_FIN, ke + 1);
+		decide(ck == '\r', SF_INV, ke + 1);
+		decide(ck == ' ', SF_SLOW, 0); // P:268-270: the key skips it
+		decide(ck != ':', SF_INV, ke);
+		decide(kt == SK_HOST && host_seen, SF_INV, ke); // P:282-287
+		// P:299-319: spaces, then a C_VAL byte (bytes ke+1..ke+3 are in c4)
+		decide(nsp == 3, SF_SLOW, 0);
+		decide(v >= E, SF_UNF, 0);
+		decide(bv < 0x20u || bv > 0x7eu, SF_INV, v);
+		// P:321-352: the value ends at its first byte outside its class: CR, LF (P:248-262)
+		decide(!vok, SF_SLOW, 0);
+		decide(w >= E, SF_UNF, 0);
+		decide(cw != '\r', SF_INV, w);
+		decide(w + 1 >= E, SF_UNF, 0);
+		decide(cw1 != '\n', SF_INV, w + 1);
+		const bool go = dec == SF_GO;
+		const bool nh = go && kt == SK_HOST, nc = go && kt == SK_CLIENT && !cip_seen;
+		host_off = nh ? v - B : host_off;
+		host_len = nh ? w - v : host_len;
+		host_seen |= nh;
+		cip_off = nc ? v - B : cip_off;
+		cip_seen |= nc;
+		q = w + 2;
+	}
+	if (dec == SF_SLOW)
+		return false;
+	if (dec == SF_INV || dec == SF_FIN) {
+		o.status = dec == SF_FIN ? EBD_STATUS_FINISHED : EBD_STATUS_INVALID;
+		o.consumed = pos - B + 1;
+	}
+	if (dec == SF_FIN) {
+		o.url_off = nm - 1;
+		o.url_len = ue - u0;
+		o.host_off = host_off;
+		o.host_len = host_len;
+		o.cip_off = cip_off;
+		o.info = (post ? EBD_INFO_POST : 0u) | (cip_seen ? EBD_INFO_CIP : 0u);
+	}
+	return true;
 }
 
 // The generic parser (gp_step, the reference handlers restated) over the same bytes, for the

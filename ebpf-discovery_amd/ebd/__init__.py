@@ -172,6 +172,7 @@ _SIGS = {
     "ebd_testing_set_lru_window": (C.c_int, [C.c_void_p, C.c_uint32]),
     "ebd_parser_init": (C.c_int, [C.c_void_p]),
     "ebd_parser_reset": (C.c_int, [C.c_void_p]),
+    "ebd_parser_state_check": (C.c_int, [C.c_void_p, C.c_uint64]),
     "ebd_parse_streams": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "ebd_client_ip_key_name": (C.c_char_p, [C.c_uint32]),
     "ebd_host_endpoint_key": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p]),
@@ -761,7 +762,7 @@ def host_scan(buf: bytes, pid=0, flags=FLAG_IPV4 | FLAG_UNENCRYPTED | FLAG_NEW_D
                              _p(hk), _p(out), _p(key))
     _check(min(rc, 0), "ebd_host_scan")
     res = (out[0], (int(key[0]), int(key[1])))
-    return res + (bool(rc),) if want_slow else res
+    return res + (int(rc),) if want_slow else res
 
 
 def host_gp_parse(chunks, flags=FLAG_UNENCRYPTED, reset_between=False, walker="gp"):

@@ -468,7 +468,12 @@ typedef struct ebd_parse_call {
  * result.clientIPKey).  Host-only: they write the state, nothing runs on the GPU. */
 int ebd_parser_init(ebd_parser_state* st);
 int ebd_parser_reset(ebd_parser_state* st);
-/* n parsers, one chunk each (host arrays; data is the calls' streams).  Blocks until done. */
+/* 0 if st is a state these calls can have written for a stream of stream_len bytes (its
+ * position, client-IP value and token count, key and clientIPKey in range), else -EINVAL.
+ * Host-only; ebd_parse_streams applies it to every call and fails with -EINVAL. */
+int ebd_parser_state_check(const ebd_parser_state* st, uint64_t stream_len);
+/* n parsers, one chunk each (host arrays; data is the calls' streams).  Blocks until done;
+ * -EINVAL (nothing runs) if a stream lies outside data or a state fails ebd_parser_state_check. */
 int ebd_parse_streams(ebd_ctx* ctx, ebd_parse_call* calls, uint32_t n, const uint8_t* data, uint64_t data_len);
 /* HEADER_CLIENT_IP_KEYS[id - 1] (HttpRequestParser.cpp:43) for a client_ip_key id, "" for 0. */
 const char* ebd_client_ip_key_name(uint32_t id);

@@ -79,3 +79,31 @@ def test_parser_state_init_and_reset_keep_the_client_ip_key():
     assert st[0] == init_state and st[6] == 4 and st[12:16].view(np.uint32)[0] == 0
     assert ebd.lib().ebd_client_ip_key_name(4) == b"x-forwarded-for"
     assert ebd.lib().ebd_client_ip_key_name(0) == b""
+
+
+def test_parser_state_check_rejects_corrupted_states():
+    """ebd_parse_streams runs caller-owned states; every field that indexes something (the
+    token list, the key trie, the stream) is checked before anything runs."""
+    import numpy as np
+    import ebd
+    L = ebd.lib()
+    st = np.zeros(320, np.uint8)
+    assert L.ebd_parser_init(ebd._p(st)) == 0
+    assert L.ebd_parser_state_check(ebd._p(st), 0) == 0
+
+    def bad(edit, stream_len=100):
+        s = st.copy()
+        edit(s)
+        return L.ebd_parser_state_check(ebd._p(s), stream_len) == -22
+
+    u32 = lambda s, off, v: s.__setitem__(slice(off, off + 4), np.frombuffer(np.uint32(v).tobytes(), np.uint8))
+    assert bad(lambda s: u32(s, 48, 33))            # ntok > EBD_PARSE_MAX_TOKENS
+    assert bad(lambda s: s.__setitem__(5, 200))     # key past the trie
+    assert bad(lambda s: s.__setitem__(0, 12))      # no such parser state
+    assert bad(lambda s: s.__setitem__(6, 9))       # clientIPKey past the 5 keys
+    assert bad(lambda s: u32(s, 12, 101))           # position past the stream
+    assert bad(lambda s: (u32(s, 12, 10), u32(s, 40, 5), u32(s, 44, 4)))  # value start after its end
+    assert bad(lambda s: (u32(s, 12, 10), u32(s, 40, 5), u32(s, 44, 11)))  # value end past the position
+    s = st.copy()
+    u32(s, 12, 10), u32(s, 40, 5), u32(s, 44, 9), u32(s, 48, 32)
+    assert L.ebd_parser_state_check(ebd._p(s), 10) == 0

@@ -165,3 +165,15 @@ def test_many_streams_in_one_call(ctx):
         assert int(calls[k]["consumed"]) == o.parse(r, UNENC), r
         want = {"UNFINISHED": 0, "FINISHED": 1, "INVALID": 2}.get(o.state, 0)
         assert int(calls[k]["status"]) == want, r
+
+
+def test_corrupted_state_is_rejected(ctx):
+    """A state with a token count past the list is refused before the kernel runs."""
+    calls = np.zeros(2, ebd.PARSE_CALL_DTYPE)
+    for k in range(2):
+        assert ebd.lib().ebd_parser_init(ebd._p(calls["state"][k])) == 0
+        calls[k]["data_off"], calls[k]["data_len"] = 0, 4
+    calls["state"][1].view(np.uint8)[48:52] = np.frombuffer(np.uint32(40).tobytes(), np.uint8)
+    buf = np.frombuffer(b"GET ", np.uint8)
+    assert ebd.lib().ebd_parse_streams(ctx.h, ebd._p(calls), 2, ebd._p(buf), 4) == -22
+    assert int(calls[0]["consumed"]) == 0  # nothing ran
