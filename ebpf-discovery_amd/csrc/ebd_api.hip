@@ -20,7 +20,7 @@
 
 namespace ebd {
 hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus);
-hipError_t launch_fresh_dfa(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_fresh_scan(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus);
 hipError_t launch_slow_collect(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_walk(const Dev& d, uint32_t nslow, hipStream_t st, int cus);
@@ -470,8 +470,8 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 		return -EINVAL;
 	ebd_ctx* c = new ebd_ctx();
 	c->cfg = *cfg;
-	if (const char* f = std::getenv("EBD_FRESH")) // A/B: EBD_FRESH=dfa runs k_fresh_dfa
-		c->cfg.flags = std::strcmp(f, "dfa") == 0 ? (c->cfg.flags | EBD_CFG_FRESH_DFA) : (c->cfg.flags & ~EBD_CFG_FRESH_DFA);
+	if (const char* f = std::getenv("EBD_FRESH")) // A/B: EBD_FRESH=scan runs k_fresh_scan, =dfa k_fresh
+		c->cfg.flags = std::strcmp(f, "scan") == 0 ? (c->cfg.flags | EBD_CFG_FRESH_SCAN) : (c->cfg.flags & ~EBD_CFG_FRESH_SCAN);
 	c->device = cfg->device;
 	c->max_events = cfg->max_events;
 	if (hipSetDevice(c->device) != hipSuccess) {
@@ -791,7 +791,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		return 0;
 	}
 	HIP_TRY(timed(c, KT_FRESH, [&] {
-		return (c->cfg.flags & EBD_CFG_FRESH_DFA) ? launch_fresh_dfa(d, c->stream, c->cus) : launch_fresh(d, c->stream, c->cus);
+		return (c->cfg.flags & EBD_CFG_FRESH_SCAN) ? launch_fresh_scan(d, c->stream, c->cus) : launch_fresh(d, c->stream, c->cus);
 	}));
 	HIP_TRY(timed(c, KT_CARRY_INSERT, [&] { return launch_sset_build(d, c->sset_cap, c->stream, c->cus); }));
 	HIP_TRY(timed(c, KT_SLOW_COLLECT, [&] { return launch_slow_collect(d, c->stream, c->cus); }));
@@ -2180,8 +2180,22 @@ int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid
 			s.cm[c][pc] = (uint16_t)m[c];
 	}
 	ScanOut o;
-	int path = 0; // 0: scan_fast, 2: scan_event, 1: the generic parser (as k_fresh runs them)
-	if (!scan_fast(s, shift, len, o)) {
+	int path = 0; // 0: request line + line records (scan_fold), 2: scan_event, 1: the generic parser
+	// as k_fresh runs them: every LF of the tile starts a line, each line parsed on its own
+	const ReqOut rq = scan_reqline(s, shift, len);
+	std::vector<uint32_t> starts;
+	std::vector<LineRec> recs;
+	for (uint32_t p = 0; p < s.t.size(); p++)
+		if (s.t[p] == '\n' && p + 1 < s.t.size()) {
+			starts.push_back(p + 1);
+			recs.push_back(scan_line(s, p + 1, shift + len));
+		}
+	uint32_t l0 = (uint32_t)starts.size();
+	for (uint32_t l = 0; l < starts.size(); l++)
+		if (starts[l] == rq.q)
+			l0 = l;
+	auto lines = [&](uint32_t l) { return l < recs.size() ? recs[l] : LineRec{LN_SLOW, 0}; };
+	if (!scan_fold(rq, lines, l0, (uint32_t)starts.size(), shift, len, o)) {
 		path = 2;
 		scan_event(s, shift, len, o);
 		if (o.slow) {

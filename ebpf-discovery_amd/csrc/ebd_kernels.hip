@@ -763,7 +763,7 @@ __global__ __launch_bounds__(kFreshThreads)
 #if EBD_FRESH_WGS > 1
 __attribute__((amdgpu_waves_per_eu(EBD_FRESH_WGS * kFreshThreads / 256, 8)))
 #endif
-void k_fresh_dfa(Dev d) {
+void k_fresh(Dev d) {
 	__shared__ __attribute__((aligned(16))) FreshLds lds;
 	uint8_t* T = lds.T;
 	FreshShared& sh = lds.sh;
@@ -1042,7 +1042,8 @@ void k_fresh_dfa(Dev d) {
 }
 
 // ---------------------------------------------------------------------------------
-// k_fresh: the structural scan (ebd_scan.h) over LDS tiles of whole buffers.
+// k_fresh_scan: the structural scan (ebd_scan.h) over LDS tiles of whole buffers (EBD_CFG_FRESH_SCAN;
+// k_fresh, the projected DFA, is the default: section 8 of DESIGN.md has both measured).
 //
 // Every workgroup is one wave with a contiguous range of the batch and no partner: it never
 // waits for another wave.  Per tile:
@@ -1051,29 +1052,40 @@ void k_fresh_dfa(Dev d) {
 //   2. the buffers land in the wave's LDS tile in one LDS-DMA stream (global_load_lds, 16 B
 //      per lane, consecutive: the whole-line read shape) when they lie back to back in the
 //      payload, as a batch from the ring buffer does; other layouts are copied buffer by buffer;
-//   3. the wave marks the pieces that hold a byte outside [0x20, 0x7e] (nv4 + __ballot: one
-//      64-bit word per 1 KiB of tile);
-//   4. each lane scans one buffer from LDS (scan_event): request line, header keys, Host and
-//      client-IP values byte-class-tested 16 bytes at a time, other header values skipped to
-//      their CR through the piece bitmap;
-//   5. result, key and client class go out in event order (16-B rows of consecutive lanes:
-//      whole lines), UNFINISHED events to the session list through an LDS ring, 256 at a time.
+//   3. lanes over pieces: the piece bitmap of bytes outside [0x20, 0x7e] (nv4 + __ballot), the
+//      key / Host / client-IP class bitmaps (class table + v_dot4_u32_u8), and the list of
+//      every LF + 1 in the tile (a wave prefix sum places each lane's LFs);
+//   4. lanes over buffers: the request line (scan_reqline);
+//   5. lanes over lines: each listed line parsed on its own (scan_line) against the buffer it
+//      lies in (a bitmap of buffer-start pieces and its prefix counts);
+//   6. lanes over buffers: the line records folded in order (scan_fold), the key and client
+//      class; result and key go out in event order (16-B rows of consecutive lanes: whole
+//      lines), UNFINISHED events to the session list through an LDS ring, 64 at a time.
 // The payload is read once, from HBM, in lines; everything after the DMA is LDS traffic.
 // ---------------------------------------------------------------------------------
 #ifndef EBD_SCAN_TILE
-#define EBD_SCAN_TILE 12288
+#define EBD_SCAN_TILE 11264
 #endif
 #ifndef EBD_SCAN_WGS
 #define EBD_SCAN_WGS 8 // one-wave workgroups per CU (LDS-bound: 8 x 19.4 KiB)
 #endif
+#ifndef EBD_SCAN_LINES
+#define EBD_SCAN_LINES 320
+#endif
 constexpr uint32_t kTileBytes = EBD_SCAN_TILE, kTilePieces = kTileBytes / 16, kTileWords = kTilePieces / 64;
 static_assert(kTilePieces % 64 == 0 && kTilePieces >= (EBD_BUFFER_MAX_DATA_SIZE + 30) / 16, "a tile holds any one buffer");
-constexpr uint32_t kUnfRing = 256; // UNFINISHED events waiting to be listed (a flush takes 128)
+static_assert(kTileBytes + 64 < 65536, "tile positions fit the 16-bit line records");
+constexpr uint32_t kLines = EBD_SCAN_LINES; // lines a tile lists (a buffer with more goes to scan_event)
+constexpr uint32_t kUnfRing = 128;          // UNFINISHED events waiting to be listed (a flush takes 64)
 
 struct ScanLds {
 	uint8_t tile[kTileBytes + 64]; // + reads a few bytes past the last buffer (key words, protocol)
 	uint16_t cm[CB_N][kTilePieces]; // class bitmaps: bit i of cm[c][pc] = byte 16 pc + i not in class c
 	unsigned long long nvw[kTileWords];
+	unsigned long long evb[kTileWords]; // bit j of word w: piece 64 w + j starts a buffer of the tile
+	uint16_t evpre[kTileWords];         // buffers starting before word w
+	uint16_t evq[64], evend[64], evfirst[64]; // per buffer (by rank): first header line, end, its record
+	LineRec lrec[kLines];
 	uint8_t ncls[256]; // ~byte_class (ebd_scan.h NB_*)
 	uint32_t unf[kUnfRing];
 };
@@ -1083,6 +1095,7 @@ struct TileSrc {
 	const uint8_t* t;
 	const unsigned long long* nv;
 	const uint8_t* nc;
+	const uint16_t (*cm)[kTilePieces];
 	__device__ __forceinline__ uint32_t byte(uint32_t p) const { return t[p]; }
 	__device__ __forceinline__ uint32_t dw(uint32_t p) const {
 		const uint32_t* a = (const uint32_t*)(t + (p & ~3u));
@@ -1104,7 +1117,6 @@ struct TileSrc {
 	__device__ __forceinline__ unsigned long long nvword(uint32_t j) const { return nv[j]; }
 	__device__ __forceinline__ uint32_t ncls(uint32_t b) const { return nc[b]; }
 	__device__ __forceinline__ unsigned long long clsword(uint32_t c, uint32_t a) const { return ((const unsigned long long*)cm[c])[a]; }
-	const uint16_t (*cm)[kTilePieces];
 };
 
 // An event's words as a lane of k_fresh holds them (Discovery.cpp:92-110: flags, pid, the
@@ -1134,8 +1146,8 @@ __device__ __forceinline__ ScanMeta scan_meta(const Dev& d, uint32_t i, uint32_t
 	return m;
 }
 
-// scan_event (and the generic parser for a key with a space) for the buffers scan_fast leaves:
-// a call, so that its loops do not take registers from the straight-line path.
+// scan_event (and the generic parser for a key with a space) for the buffers the line records
+// leave: a call, so that its loops do not take registers from the straight-line path.
 __device__ __attribute__((noinline)) void scan_exact(const uint8_t* t, const unsigned long long* nv, const uint8_t* nc,
 		const uint16_t (*cm)[kTilePieces], const KeyTrie* trie, uint32_t B, uint32_t L, ScanOut& o) {
 	const TileSrc src{t, nv, nc, cm};
@@ -1144,7 +1156,11 @@ __device__ __attribute__((noinline)) void scan_exact(const uint8_t* t, const uns
 		scan_slow(src, trie, B, L, o);
 }
 
-__global__ __launch_bounds__(64) void k_fresh(Dev d) {
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long b) {
+	return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+__global__ __launch_bounds__(64) void k_fresh_scan(Dev d) {
 	__shared__ __attribute__((aligned(16))) ScanLds lds;
 	const uint32_t lane = threadIdx.x;
 	const uint32_t per = (uint32_t)(((unsigned long long)d.n + gridDim.x - 1) / gridDim.x);
@@ -1168,7 +1184,7 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 			S += lane >= (uint32_t)o ? y : 0u;
 		}
 		const uint32_t k = (uint32_t)__popcll(__ballot(m.valid && S <= kTilePieces)); // >= 1: a buffer fits alone
-		const bool mine = lane < k;
+		const bool mine = lane < k, mp = mine && parse;
 		const uint32_t P = S - np; // the buffer's first tile piece
 		const uint32_t N = __shfl(S, (int)k - 1);
 		const ScanMeta nm = scan_meta(d, base + k + lane, rb, re); // the next tile's events
@@ -1199,10 +1215,20 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 				}
 			}
 		}
+		if (lane < kTileWords)
+			lds.evb[lane] = 0ull;
 		asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 		wave_sync();
-		// the tile's bitmaps, every lane on its own pieces: bit j of nvw[w] = piece 64 w + j holds
-		// a byte outside [0x20, 0x7e]; the class bitmaps cm (ebd_scan.h piece_classes)
+		// the buffers of the tile, by rank: where they start and end
+		const uint32_t rank = lane_rank(__ballot(mp));
+		const uint32_t B = 16 * P + (uint32_t)(a & 15u), E = B + (mp ? m.L : 0u);
+		if (mp) {
+			atomicOr(&lds.evb[P >> 6], 1ull << (P & 63u));
+			lds.evend[rank] = (uint16_t)E;
+			lds.evfirst[rank] = 0xffffu;
+		}
+		// lanes over pieces: the bitmaps and the line list (every LF + 1, in tile order)
+		uint32_t nl = 0;
 		for (uint32_t j0 = 0; j0 < N; j0 += 64) {
 			const uint32_t j = min(j0 + lane, N - 1);
 			const uint4 v = *(const uint4*)(lds.tile + 16 * j);
@@ -1215,6 +1241,60 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 #pragma unroll
 			for (uint32_t c = 0; c < CB_N; c++)
 				lds.cm[c][j] = (uint16_t)cmk[c];
+			const bool own = j0 + lane < N;
+			unsigned long long z0 = own ? (lf4(v.x) | ((unsigned long long)lf4(v.y) << 32)) : 0ull;
+			unsigned long long z1 = own ? (lf4(v.z) | ((unsigned long long)lf4(v.w) << 32)) : 0ull;
+			const uint32_t c = (uint32_t)(__popcll(z0) + __popcll(z1));
+			uint32_t x = c; // inclusive prefix over the lanes
+#pragma unroll
+			for (int o = 1; o < 64; o <<= 1) {
+				const uint32_t y = __shfl_up(x, (unsigned)o, 64);
+				x += lane >= (uint32_t)o ? y : 0u;
+			}
+			uint32_t at = nl + x - c;
+			for (; z0; z0 &= z0 - 1, at++)
+				if (at < kLines)
+					lds.lrec[at].a = (16 * j + ((uint32_t)__builtin_ctzll(z0) >> 3) + 1) << 16;
+			for (; z1; z1 &= z1 - 1, at++)
+				if (at < kLines)
+					lds.lrec[at].a = (16 * j + 8 + ((uint32_t)__builtin_ctzll(z1) >> 3) + 1) << 16;
+			nl += __shfl(x, 63);
+		}
+		const uint32_t nlines = min(nl, kLines);
+		wave_sync();
+		if (lane < kTileWords) { // buffers starting before each word of evb
+			const uint32_t c = (uint32_t)__popcll(lds.evb[lane]);
+			uint32_t x = c;
+#pragma unroll
+			for (int o = 1; o < 16; o <<= 1) {
+				const uint32_t y = __shfl_up(x, (unsigned)o, 64);
+				x += lane >= (uint32_t)o ? y : 0u;
+			}
+			lds.evpre[lane] = (uint16_t)(x - c);
+		}
+		static_assert(kTileWords <= 16, "evpre scan covers 16 words");
+		// lanes over buffers: the request lines (P:162-262)
+#ifndef EBD_SX_STAGE
+#define EBD_SX_STAGE 9
+#endif
+		ReqOut rq;
+		rq.dec = SF_UNF;
+		if (mp && EBD_SX_STAGE >= 2) {
+			rq = scan_reqline(src, B, m.L);
+			lds.evq[rank] = (uint16_t)(rq.dec == SF_GO && rq.q < E ? rq.q : 0xffffu);
+		}
+		wave_sync();
+		// lanes over lines: each listed line against the buffer it lies in (P:264-352)
+		for (uint32_t l0 = 0; l0 < (EBD_SX_STAGE >= 3 ? nlines : 0u); l0 += 64) {
+			const uint32_t l = l0 + lane;
+			if (l < nlines) {
+				const uint32_t q = lds.lrec[l].a >> 16, pc = min(q >> 4, N - 1), wi = pc >> 6;
+				const uint32_t e = lds.evpre[wi] + (uint32_t)__popcll(lds.evb[wi] & ((2ull << (pc & 63u)) - 1ull)) - 1u;
+				const LineRec r = scan_line(src, q, lds.evend[e]);
+				lds.lrec[l] = r;
+				if (q == lds.evq[e])
+					lds.evfirst[e] = (uint16_t)l;
+			}
 		}
 		wave_sync();
 		bool unf = false;
@@ -1223,21 +1303,13 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 			ebd_event_result r;
 			Hash128 key{0, 0};
 			if (parse) {
-				const uint32_t B = 16 * P + (uint32_t)(a & 15u);
 				ScanOut o;
-#ifdef EBD_SX_NOSCAN
+				const uint32_t l0 = lds.evfirst[rank];
 				scan_init(o, m.L);
-				o.status = src.byte(B) == 'Z' ? EBD_STATUS_FINISHED : EBD_STATUS_INVALID;
-#else
-				if (!scan_fast(src, B, m.L, o)) // the shapes scan_fast leaves (ebd_scan.h): rare
-					scan_exact(lds.tile, lds.nvw, lds.ncls, lds.cm, d.trie, B, m.L, o);
-#endif
+				if (EBD_SX_STAGE >= 4 && !scan_fold(rq, [&](uint32_t l) { return lds.lrec[l < kLines ? l : 0]; }, l0, nlines, B, m.L, o) && EBD_SX_STAGE >= 5)
+					scan_exact(lds.tile, lds.nvw, lds.ncls, lds.cm, d.trie, B, m.L, o); // rare shapes (ebd_scan.h)
 				r = scan_result(o, (uint8_t)flags);
-#ifdef EBD_SX_NOKEY
-				if (o.status == EBD_STATUS_FINISHED && src.byte(B) == 'Z') {
-#else
-				if (o.status == EBD_STATUS_FINISHED) {
-#endif
+				if (o.status == EBD_STATUS_FINISHED && EBD_SX_STAGE >= 6) {
 					key = endpoint_key<2>(d.hkey, m.pid, o.host_off, o.host_len, o.url_off, o.url_len,
 							[&](uint32_t x) { return src.ld8(B + x); });
 					if (!(o.info & EBD_INFO_CIP)) { // the client is the session's source address (Aggregator.cpp:57-63)
@@ -1261,11 +1333,10 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 			d.res[i] = r;
 			d.keys[i] = key;
 		}
-		// UNFINISHED events to the session-set list (k_sset_build), 256 per counter atomic
+		// UNFINISHED events to the session-set list (k_sset_build), 64 per counter atomic
 		const unsigned long long ub = __ballot(unf);
 		if (unf)
-			lds.unf[(uh + un + __builtin_amdgcn_mbcnt_hi((uint32_t)(ub >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ub, 0))) &
-					(kUnfRing - 1)] = base + lane;
+			lds.unf[(uh + un + lane_rank(ub)) & (kUnfRing - 1)] = base + lane;
 		un += (uint32_t)__popcll(ub);
 		if (un >= kUnfRing / 2) { // (un < kUnfRing / 2 + 64 <= kUnfRing entries)
 			wave_sync();
@@ -1281,6 +1352,7 @@ __global__ __launch_bounds__(64) void k_fresh(Dev d) {
 		}
 		base += k;
 		m = nm;
+		wave_sync(); // the next tile's DMA rewrites what this one's lanes read
 	}
 	wave_sync();
 	if (un) {
@@ -4128,19 +4200,19 @@ static uint32_t agg_grid(uint32_t n, int cus) {
 } // k_pub_scan: <= 2048
 uint32_t agg_stage_per_block(uint32_t n, int cus) { return agg_steps_per_block(n, agg_grid(n, cus)) * kAggThreads; }
 
-hipError_t launch_fresh_dfa(const Dev& d, hipStream_t st, int cus) {
+hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
 	// one workgroup per CU (LDS-bound occupancy), each a contiguous range of the batch
 	const uint64_t groups = ((uint64_t)d.n + kFreshThreads * 4 - 1) / (kFreshThreads * 4);
 	const int grid = (int)(groups < (uint64_t)cus * EBD_FRESH_WGS ? groups : (uint64_t)cus * EBD_FRESH_WGS);
-	hipLaunchKernelGGL(k_fresh_dfa, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
+	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(kFreshThreads), 0, st, d);
 	return hipGetLastError();
 }
-hipError_t launch_fresh(const Dev& d, hipStream_t st, int cus) {
+hipError_t launch_fresh_scan(const Dev& d, hipStream_t st, int cus) {
 	// one-wave workgroups, EBD_SCAN_WGS per CU (LDS-bound), each a contiguous range of at
 	// least 256 events
 	const uint64_t groups = ((uint64_t)d.n + 255) / 256;
 	const int grid = (int)(groups < (uint64_t)cus * EBD_SCAN_WGS ? groups : (uint64_t)cus * EBD_SCAN_WGS);
-	hipLaunchKernelGGL(k_fresh, dim3(grid > 0 ? grid : 1), dim3(64), 0, st, d);
+	hipLaunchKernelGGL(k_fresh_scan, dim3(grid > 0 ? grid : 1), dim3(64), 0, st, d);
 	return hipGetLastError();
 }
 hipError_t launch_sset_build(const Dev& d, uint32_t cap, hipStream_t st, int cus) {

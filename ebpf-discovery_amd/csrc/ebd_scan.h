@@ -60,9 +60,10 @@ static_assert(C_URL == 1u << NB_URL && C_KEY == 1u << NB_KEY && C_VAL == 1u << N
 // Bytes past the buffer are whatever the tile holds there; every search is bounded by E.
 
 // Class bitmaps of the tile: bit b of word clsword(c, a) is set where tile byte 64 a + b is
-// NOT in class c (c = CB_URL, CB_KEY, CB_HOST, CB_CIP).  They are built once per tile by every
+// NOT in class c (c = CB_KEY, CB_HOST, CB_CIP; the URL, one span per buffer, is looked up
+// byte by byte: class_search).  They are built once per tile by every
 // lane over consecutive pieces (class_masks16), so a search costs one word per 64 bytes.
-enum : uint32_t { CB_URL = 0, CB_KEY = 1, CB_HOST = 2, CB_CIP = 3, CB_N = 4 };
+enum : uint32_t { CB_KEY = 0, CB_HOST = 1, CB_CIP = 2, CB_N = 3 };
 
 // The 16-bit "not in class" masks of one 16-byte piece for the four classes, from the inverted
 // class bytes packed four to a word (f[j] byte i = ncls of piece byte 4 j + i): bit n of the
@@ -84,7 +85,7 @@ EBD_HD uint32_t class_mask16(const uint32_t (&f)[4], uint32_t nb) {
 	return (lo | (hi << 8)) >> nb;
 }
 
-// A piece's four class masks (mask bit i: piece byte i is not in the class), from its words.
+// A piece's class masks (mask bit i: piece byte i is not in the class), from its words.
 template <typename Src>
 EBD_HD void piece_classes(const Src& s, const uint32_t (&w)[4], uint32_t (&m)[CB_N]) {
 	uint32_t f[4];
@@ -93,7 +94,6 @@ EBD_HD void piece_classes(const Src& s, const uint32_t (&w)[4], uint32_t (&m)[CB
 		const uint32_t x = w[j];
 		f[j] = s.ncls(x & 0xffu) | (s.ncls((x >> 8) & 0xffu) << 8) | (s.ncls((x >> 16) & 0xffu) << 16) | (s.ncls(x >> 24) << 24);
 	}
-	m[CB_URL] = class_mask16(f, NB_URL);
 	m[CB_KEY] = class_mask16(f, NB_KEY);
 	m[CB_HOST] = class_mask16(f, NB_HOST);
 	m[CB_CIP] = class_mask16(f, NB_CIP);
@@ -141,6 +141,40 @@ EBD_HD uint32_t first_nv(const Src& s, uint32_t p, uint32_t e) {
 		pc++;
 	}
 	return e;
+}
+
+// First byte at or after p not in class nb (ncls bit), from the class table byte by byte over
+// at most NP pieces: r (<= e).  False: none in them and the buffer goes on past them.
+template <uint32_t NP, typename Src>
+EBD_HD bool class_search(const Src& s, uint32_t p, uint32_t e, uint32_t nb, uint32_t& r) {
+	const uint32_t sel = 0x01010101u << nb;
+	uint32_t pc = p >> 4, lo = p & 15u;
+#pragma unroll
+	for (uint32_t i = 0; i < NP; i++) {
+		uint32_t w[4], f[4];
+		s.piece(pc, w);
+#pragma unroll
+		for (uint32_t j = 0; j < 4; j++) {
+			const uint32_t x = w[j];
+			f[j] = (s.ncls(x & 0xffu) | (s.ncls((x >> 8) & 0xffu) << 8) | (s.ncls((x >> 16) & 0xffu) << 16) |
+						   (s.ncls(x >> 24) << 24)) &
+					sel;
+		}
+		const uint32_t k = first_flag16(f[0], f[1], f[2], f[3], lo);
+		if (k < 16) {
+			const uint32_t x = 16 * pc + k;
+			r = x < e ? x : e;
+			return true;
+		}
+		pc++;
+		lo = 0;
+		if (16 * pc >= e) {
+			r = e;
+			return true;
+		}
+	}
+	r = e;
+	return false;
 }
 
 // 4 bytes of a literal (little-endian), and its letter bytes (0x20 each): a key byte b
@@ -254,7 +288,12 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 	}
 	// P:201-213: URL bytes until the space
 	const uint32_t u0 = B + nm - 1; // the '/'
-	const uint32_t ue = first_not(s, u0 + 1, E, CB_URL);
+	uint32_t ue = E;
+	for (uint32_t p = u0 + 1; p < E;) { // the URL: class_search 4 pieces at a time
+		if (class_search<4>(s, p, E, NB_URL, ue))
+			break;
+		p = ((p >> 4) + 4) << 4;
+	}
 	if (ue >= E)
 		return;
 	if (s.byte(ue) != ' ') {
@@ -377,16 +416,6 @@ EBD_HD void scan_event(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 	}
 }
 
-// ---------------------------------------------------------------------------------
-// scan_fast: scan_event in straight-line form for the common shapes, so that the lanes of a
-// wave (one buffer each) run the same instructions: every search looks at two 64-byte bitmap
-// words (two flagged pieces for a header value of another key, found through the piece
-// bitmap) and each header line is one pass of the loop.  Returns false where a search is not
-// resolved that way (a URL, key, Host or client-IP value of more than 64-127 bytes, a header
-// value running past the next 1-2 KiB of the tile, three spaces after a ':', a space in a
-// key): the caller then runs scan_event, which takes every shape.  Where it returns true the
-// result is scan_event's.
-// ---------------------------------------------------------------------------------
 // v_alignbyte_b32: bytes [k, k + 4) of hi:lo (k = 0..3)
 EBD_HD uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t k) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -443,13 +472,89 @@ EBD_HD bool nv_search2(const Src& s, uint32_t p, uint32_t e, uint32_t& r) {
 	return true;
 }
 
-// Outcomes of one step of scan_fast, first match wins (the order is the reference's byte
-// order along the line).
+// Outcomes of a line or a request, first match wins (the order is the reference's byte order).
 enum : uint32_t { SF_GO = 0, SF_UNF = 1, SF_FIN = 2, SF_INV = 3, SF_SLOW = 4 };
 
+// ---------------------------------------------------------------------------------
+// Lanes over header lines.  k_fresh's per-lane walk of a buffer, line after line, runs for the
+// longest buffer of the wave and diverges on every line kind.  Instead the wave enumerates
+// every LF of its tile (each one starts a candidate header line, LF + 1), parses each line in
+// a lane of its own with straight-line code (scan_line: the P:264-352 handlers of one line),
+// and each buffer's lane only parses its request line (scan_reqline) and folds the records
+// of its lines in order (scan_fold): the first line that is not a complete "key: value CRLF"
+// decides the outcome, and the cross-line rules are applied there: a second Host
+// (P:282-287) and the first client-IP header (P:309-316).  Lines that start after a line that
+// decided the outcome, or outside the buffer, are parsed but never folded.  A line the
+// straight-line code cannot settle (SLOW: a space in its key, three spaces after ':', a key
+// or Host / client-IP value longer than its two bitmap words) sends the buffer to scan_event.
+// ---------------------------------------------------------------------------------
+enum : uint32_t { LN_OK = 0, LN_FIN = 1, LN_INV = 2, LN_UNF = 3, LN_SLOW = 4 };
+
+// A line's record: a = code | kt << 4 | start << 16 (the line's first byte; tile positions
+// < 2^16); b = v | w << 16 for LN_OK (the value's first byte and its CR), else pos (the LF of
+// LN_FIN, the failing byte of LN_INV).  An LN_OK line's ':' is start + key length, which for
+// the one key that needs it (a second Host, P:282-287) is start + 4.
+struct LineRec {
+	uint32_t a, b;
+};
+
 template <typename Src>
-EBD_HD bool scan_fast(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
-	scan_init(o, L);
+EBD_HD LineRec scan_line(const Src& s, uint32_t q, uint32_t E) {
+	uint32_t dec = SF_GO, pos = 0;
+	auto decide = [&](bool c, uint32_t d, uint32_t p) {
+		const bool t = dec == SF_GO && c;
+		dec = t ? d : dec;
+		pos = t ? p : pos;
+	};
+	uint32_t ke;
+	const bool kok = search2(s, CB_KEY, q, E, ke); // a CR at q is not K: ke = q
+	const uint32_t kr = ke < E ? ke : E;
+	const uint32_t c4 = s.dw(kr), ck = c4 & 0xffu, c1 = (c4 >> 8) & 0xffu;
+	const uint32_t kt = key_type(s, q, ke - q);
+	const uint32_t nsp = ctz64_or(((c4 >> 8) ^ 0x202020u) & 0xffffffu, 24) >> 3;
+	const uint32_t v = ke + 1 + nsp, bv = (c4 >> (8 * (nsp + 1))) & 0xffu;
+	const uint32_t vs = (v < E ? v : E) + 1;
+	uint32_t w;
+	bool vok;
+	if (kt == SK_OTHER)
+		vok = nv_search2(s, vs, E, w);
+	else
+		vok = search2(s, kt == SK_HOST ? CB_HOST : CB_CIP, vs, E, w);
+	const uint32_t w4 = s.dw(w < E ? w : E), cw = w4 & 0xffu, cw1 = (w4 >> 8) & 0xffu;
+	decide(q >= E, LN_UNF, 0);
+	decide(!kok, LN_SLOW, 0);
+	decide(ke >= E, LN_UNF, 0);
+	// P:265-267, P:354-364: a CR in the key ends the headers; LF finishes the request
+	decide(ck == '\r' && ke + 1 >= E, LN_UNF, 0);
+	decide(ck == '\r' && c1 == '\n', LN_FIN, ke + 1);
+	decide(ck == '\r', LN_INV, ke + 1);
+	decide(ck == ' ', LN_SLOW, 0); // P:268-270: the key skips it
+	decide(ck != ':', LN_INV, ke);
+	// P:299-319: spaces, then a C_VAL byte (bytes ke+1..ke+3 are in c4)
+	decide(nsp == 3, LN_SLOW, 0);
+	decide(v >= E, LN_UNF, 0);
+	decide(bv < 0x20u || bv > 0x7eu, LN_INV, v);
+	// P:321-352: the value ends at its first byte outside its class: CR, then LF (P:248-262)
+	decide(!vok, LN_SLOW, 0);
+	decide(w >= E, LN_UNF, 0);
+	decide(cw != '\r', LN_INV, w);
+	decide(w + 1 >= E, LN_UNF, 0);
+	decide(cw1 != '\n', LN_INV, w + 1);
+	const bool ok = dec == SF_GO;
+	LineRec r;
+	r.a = (ok ? LN_OK : dec) | (kt << 4) | (q << 16);
+	r.b = ok ? (v | (w << 16)) : pos;
+	return r;
+}
+
+// The request line of a buffer (P:162-262): dec SF_GO with the first header line's start q,
+// or the outcome.
+struct ReqOut {
+	uint32_t dec, pos, q, ue, post;
+};
+
+template <typename Src>
+EBD_HD ReqOut scan_reqline(const Src& s, uint32_t B, uint32_t L) {
 	const uint32_t E = B + L;
 	uint32_t dec = L == 0 ? SF_UNF : SF_GO, pos = 0;
 	auto decide = [&](bool c, uint32_t d, uint32_t p) {
@@ -461,78 +566,77 @@ EBD_HD bool scan_fast(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 	const uint32_t m0 = s.dw(B), m1 = s.dw(B + 4);
 	const bool post = (m0 & 0xffu) == 'P';
 	const uint32_t nm = post ? 6u : 5u;
-	{
-		const unsigned long long d = (((unsigned long long)m1 << 32 | m0) ^ (post ? 0x2f2054534f50ull : 0x2f20544547ull)) &
-				(post ? 0xffffffffffffull : 0xffffffffffull);
-		const uint32_t k = d ? ((uint32_t)__builtin_ctzll(d) >> 3) : nm;
-		decide(k < nm && k < L, SF_INV, B + k);
-		decide(L < nm, SF_UNF, 0);
-	}
+	const unsigned long long d = (((unsigned long long)m1 << 32 | m0) ^ (post ? 0x2f2054534f50ull : 0x2f20544547ull)) &
+			(post ? 0xffffffffffffull : 0xffffffffffull);
+	const uint32_t km = d ? ((uint32_t)__builtin_ctzll(d) >> 3) : nm;
+	decide(km < nm && km < L, SF_INV, B + km);
+	decide(L < nm, SF_UNF, 0);
 	// P:201-213 URL bytes, then ' '; P:215-262 "HTTP/1.0" | "HTTP/1.1" CR LF
-	const uint32_t u0 = B + nm - 1;
 	uint32_t ue;
-	const bool uok = search2(s, CB_URL, u0 + 1, E, ue);
-	{
-		const uint32_t ur = ue < E ? ue : E;
-		const uint32_t p0 = s.dw(ur), p1 = s.dw(ur + 4), p2 = s.dw(ur + 8);
-		const unsigned long long x = (unsigned long long)align_byte(p1, p0, 1) | ((unsigned long long)align_byte(p2, p1, 1) << 32);
-		const unsigned long long dx = (x ^ 0x302e312f50545448ull) & ~(1ull << 56);
-		const uint32_t dy = ((p2 >> 8) ^ 0x0a0du) & 0xffffu;
-		const uint32_t k = dx ? ((uint32_t)__builtin_ctzll(dx) >> 3) : dy ? 8u + ((uint32_t)__builtin_ctz(dy) >> 3) : 10u;
-		const uint32_t avail = E - ur - 1;
-		decide(!uok, SF_SLOW, 0);
-		decide(ue >= E, SF_UNF, 0);
-		decide((p0 & 0xffu) != ' ', SF_INV, ue);
-		decide(k < 10 && k < avail, SF_INV, ue + 1 + k);
-		decide(avail < 10, SF_UNF, 0);
-	}
-	uint32_t q = ue + 11;
+	const bool uok = class_search<3>(s, B + nm, E, NB_URL, ue);
+	const uint32_t ur = ue < E ? ue : E;
+	const uint32_t p0 = s.dw(ur), p1 = s.dw(ur + 4), p2 = s.dw(ur + 8);
+	const unsigned long long x = (unsigned long long)align_byte(p1, p0, 1) | ((unsigned long long)align_byte(p2, p1, 1) << 32);
+	const unsigned long long dx = (x ^ 0x302e312f50545448ull) & ~(1ull << 56);
+	const uint32_t dy = ((p2 >> 8) ^ 0x0a0du) & 0xffffu;
+	const uint32_t k = dx ? ((uint32_t)__builtin_ctzll(dx) >> 3) : dy ? 8u + ((uint32_t)__builtin_ctz(dy) >> 3) : 10u;
+	const uint32_t avail = E - ur - 1;
+	decide(!uok, SF_SLOW, 0);
+	decide(ue >= E, SF_UNF, 0);
+	decide((p0 & 0xffu) != ' ', SF_INV, ue);
+	decide(k < 10 && k < avail, SF_INV, ue + 1 + k);
+	decide(avail < 10, SF_UNF, 0);
+	ReqOut r;
+	r.dec = dec;
+	r.pos = pos;
+	r.q = ue + 11;
+	r.ue = ue;
+	r.post = post ? 1u : 0u;
+	return r;
+}
+
+// Folds a buffer's line records in order (lines(l) -> LineRec, l0 = the index of the
+// line that starts at rq.q, n = lines listed).  False: the buffer needs scan_event.
+template <typename Lines>
+EBD_HD bool scan_fold(const ReqOut& rq, const Lines& lines, uint32_t l0, uint32_t n, uint32_t B, uint32_t L, ScanOut& o) {
+	scan_init(o, L);
+	const uint32_t E = B + L;
+	uint32_t dec = rq.dec, pos = rq.pos;
 	bool host_seen = false, cip_seen = false;
 	uint32_t host_off = 0, host_len = 0, cip_off = 0;
-	// one header line per pass (P:264-352), every lane through the same instructions
+	uint32_t q = rq.q, l = l0;
 	while (dec == SF_GO) {
-		uint32_t ke;
-		const bool kok = search2(s, CB_KEY, q, E, ke);
-		const uint32_t kr = ke < E ? ke : E;
-		const uint32_t c4 = s.dw(kr), ck = c4 & 0xffu, c1 = (c4 >> 8) & 0xffu;
-		const uint32_t kt = key_type(s, q, ke - q);
-		const uint32_t nsp = ctz64_or(((c4 >> 8) ^ 0x202020u) & 0xffffffu, 24) >> 3;
-		const uint32_t v = ke + 1 + nsp, bv = (c4 >> (8 * (nsp + 1))) & 0xffu;
-		const uint32_t vs = (v < E ? v : E) + 1;
-		uint32_t wn, wc;
-		const bool nok = nv_search2(s, vs, E, wn);
-		const bool cok = search2(s, kt == SK_HOST ? CB_HOST : CB_CIP, vs, E, wc);
-		const uint32_t w = kt == SK_OTHER ? wn : wc;
-		const bool vok = kt == SK_OTHER ? nok : cok;
-		const uint32_t w4 = s.dw(w < E ? w : E), cw = w4 & 0xffu, cw1 = (w4 >> 8) & 0xffu;
-		decide(q >= E, SF_UNF, 0);
-		decide(!kok, SF_SLOW, 0);
-		decide(ke >= E, SF_UNF, 0);
-		// P:265-267, P:354-364: a CR in the key ends the headers; LF finishes the request
-		decide(ck == '\r' && ke + 1 >= E, SF_UNF, 0);
-		decide(ck == '\r' && c1 == '\n', SF_FIN, ke + 1);
-		decide(ck == '\r', SF_INV, ke + 1);
-		decide(ck == ' ', SF_SLOW, 0); // P:268-270: the key skips it
-		decide(ck != ':', SF_INV, ke);
-		decide(kt == SK_HOST && host_seen, SF_INV, ke); // P:282-287
-		// P:299-319: spaces, then a C_VAL byte (bytes ke+1..ke+3 are in c4)
-		decide(nsp == 3, SF_SLOW, 0);
-		decide(v >= E, SF_UNF, 0);
-		decide(bv < 0x20u || bv > 0x7eu, SF_INV, v);
-		// P:321-352: the value ends at its first byte outside its class: CR, LF (P:248-262)
-		decide(!vok, SF_SLOW, 0);
-		decide(w >= E, SF_UNF, 0);
-		decide(cw != '\r', SF_INV, w);
-		decide(w + 1 >= E, SF_UNF, 0);
-		decide(cw1 != '\n', SF_INV, w + 1);
-		const bool go = dec == SF_GO;
-		const bool nh = go && kt == SK_HOST, nc = go && kt == SK_CLIENT && !cip_seen;
-		host_off = nh ? v - B : host_off;
-		host_len = nh ? w - v : host_len;
-		host_seen |= nh;
-		cip_off = nc ? v - B : cip_off;
-		cip_seen |= nc;
+		if (q >= E) { // the last line ended with the buffer
+			dec = SF_UNF;
+			break;
+		}
+		const LineRec r = lines(l);
+		if (l >= n || (r.a >> 16) != q) { // not listed (more lines than the tile's list holds)
+			dec = SF_SLOW;
+			break;
+		}
+		const uint32_t code = r.a & 15u, kt = (r.a >> 4) & 3u;
+		if (code != LN_OK) {
+			dec = code == LN_FIN ? SF_FIN : code == LN_INV ? SF_INV : code == LN_UNF ? SF_UNF : SF_SLOW;
+			pos = r.b;
+			break;
+		}
+		if (kt == SK_HOST && host_seen) { // P:282-287: a second Host fails at its ':'
+			dec = SF_INV;
+			pos = q + 4;
+			break;
+		}
+		const uint32_t v = r.b & 0xffffu, w = r.b >> 16;
+		if (kt == SK_HOST) {
+			host_seen = true;
+			host_off = v - B;
+			host_len = w - v;
+		} else if (kt == SK_CLIENT && !cip_seen) {
+			cip_seen = true;
+			cip_off = v - B;
+		}
 		q = w + 2;
+		l++;
 	}
 	if (dec == SF_SLOW)
 		return false;
@@ -541,14 +645,20 @@ EBD_HD bool scan_fast(const Src& s, uint32_t B, uint32_t L, ScanOut& o) {
 		o.consumed = pos - B + 1;
 	}
 	if (dec == SF_FIN) {
-		o.url_off = nm - 1;
-		o.url_len = ue - u0;
+		o.url_off = (rq.post ? 6u : 5u) - 1;
+		o.url_len = rq.ue - (B + o.url_off);
 		o.host_off = host_off;
 		o.host_len = host_len;
 		o.cip_off = cip_off;
-		o.info = (post ? EBD_INFO_POST : 0u) | (cip_seen ? EBD_INFO_CIP : 0u);
+		o.info = (rq.post ? EBD_INFO_POST : 0u) | (cip_seen ? EBD_INFO_CIP : 0u);
 	}
 	return true;
+}
+
+// The LFs of 4 words (16 tile bytes): bit 7 of each byte equal to '\n' (exact per byte).
+EBD_HD uint32_t lf4(uint32_t w) {
+	const uint32_t t = w ^ 0x0a0a0a0au;
+	return ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t) & 0x80808080u;
 }
 
 // The generic parser (gp_step, the reference handlers restated) over the same bytes, for the

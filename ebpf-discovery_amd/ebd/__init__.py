@@ -56,6 +56,7 @@ assert EVENT_DTYPE.itemsize == 36 and RESULT_DTYPE.itemsize == 16
 assert SESSION_REQ_DTYPE.itemsize == 32 and SERVICE_DTYPE.itemsize == 80 and SERVICE_NET_DTYPE.itemsize == 32
 CFG_TIMING = 2
 CFG_NETWORK_COUNTERS = 4
+CFG_FRESH_SCAN = 8  # k_fresh_scan (the structural scan) instead of the DFA k_fresh
 # A fixed service-key PRF key for tests that compare keys across contexts or with the host
 # hooks; products leave the key to the library (a fresh random key per context).
 TEST_HASH_KEY = (0x0706050403020100, 0x0F0E0D0C0B0A0908)
@@ -251,10 +252,11 @@ class Context:
     """One GPU context: the Discovery consumer state (session LRU) + the Aggregator."""
 
     def __init__(self, max_events, device=0, max_payload=0, service_capacity=0, string_arena=0, lru_capacity=0,
-                 timing=False, hash_key=None, network_counters=False, net_capacity=0):
+                 timing=False, hash_key=None, network_counters=False, net_capacity=0, fresh_scan=False):
         cfg = Config(device=device, max_events=max_events, max_payload=max_payload,
                      service_capacity=service_capacity, string_arena=string_arena, lru_capacity=lru_capacity,
-                     flags=(CFG_TIMING if timing else 0) | (CFG_NETWORK_COUNTERS if network_counters else 0),
+                     flags=(CFG_TIMING if timing else 0) | (CFG_NETWORK_COUNTERS if network_counters else 0) |
+                     (CFG_FRESH_SCAN if fresh_scan else 0),
                      net_capacity=net_capacity)
         if hash_key is not None:
             cfg.hash_key[0], cfg.hash_key[1] = int(hash_key[0]), int(hash_key[1])

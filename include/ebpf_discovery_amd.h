@@ -214,11 +214,12 @@ typedef struct ebd_config {
  * --enable-network-counters option, main.cpp:78): every external client's /16 and /24 (IPv4)
  * or 48-bit (IPv6) network is kept per service with the time it was last seen. */
 #define EBD_CFG_NETWORK_COUNTERS 4u
-/* Fresh parses (Discovery.cpp:141-159) through the rounds-1..5 projected-DFA kernel
- * (k_fresh_dfa, one lane per buffer) instead of the structural scan (k_fresh, one wave per
- * tile of buffers).  Same results; kept for A/B measurement.  The environment variable
- * EBD_FRESH=dfa sets it for every context. */
-#define EBD_CFG_FRESH_DFA 8u
+/* Fresh parses (Discovery.cpp:141-159) through the structural scan (k_fresh_scan: one wave
+ * per LDS tile of buffers; lanes over pieces, header lines and buffers) instead of the
+ * projected-DFA kernel (k_fresh, one lane per buffer).  Same results; kept for A/B
+ * measurement.  The environment variable EBD_FRESH=scan sets it for
+ * every context (EBD_FRESH=dfa clears it). */
+#define EBD_CFG_FRESH_SCAN 8u
 
 typedef struct ebd_ctx ebd_ctx;
 

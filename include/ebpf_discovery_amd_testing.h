@@ -20,13 +20,13 @@ int ebd_host_dfa_info(uint32_t* info, uint32_t n);
 /* The DFA's transition table next[s * 256 + byte] (cap >= 65536); returns nstates. */
 int ebd_host_dfa_next(uint8_t* out, uint32_t cap);
 
-/* The DFA fast path (k_fresh_dfa's per-event logic) for one buffer; key = its service key under
+/* The DFA fast path (k_fresh's per-event logic) for one buffer; key = its service key under
  * hash_key (ebd_config.hash_key). */
 int ebd_host_fresh(const uint8_t* buf, uint32_t len, uint32_t pid, uint8_t flags, const uint8_t* src16,
 		const ebd_ipv4_network* v4, uint32_t n4, const ebd_ipv6_network* v6, uint32_t n6, const uint64_t hash_key[2],
 		ebd_event_result* out, uint64_t key[2]);
 
-/* The structural fast path (k_fresh's per-event logic, ebd_scan.h) for one buffer placed at
+/* The structural fast path (k_fresh_scan's per-event logic, ebd_scan.h) for one buffer placed at
  * byte `shift` (0..15) of its LDS tile; the rest of the tile is "\r\n" filler.  Returns the
  * path that decided it: 0 scan_fast, 2 scan_event, 1 the generic parser (a key with a space). */
 int ebd_host_scan(const uint8_t* buf, uint32_t len, uint32_t shift, uint32_t pid, uint8_t flags, const uint8_t* src16,

@@ -45,7 +45,7 @@ def scan_shifted(shift):
     return f
 
 
-# the DFA fast path (k_fresh_dfa) and the structural scan (k_fresh) at three tile alignments
+# the DFA fast path (k_fresh) and the structural scan (k_fresh_scan) at three tile alignments
 FAST_PATHS = {"dfa": ebd.host_fresh, "scan0": scan_shifted(0), "scan7": scan_shifted(7), "scan15": scan_shifted(15)}
 
 
