@@ -74,6 +74,9 @@ def parse_args():
                     help="cold: every step is one report interval, the service table cleared before the batch "
                          "(every service of the batch is created inside the timed step); warm: the table keeps "
                          "the services of earlier steps (all hits after the first batch)")
+    ap.add_argument("--pmc4", default=os.path.join(ROOT, "profiles", "pmc_fetch_config4.json"),
+                    help="rocprofv3 FETCH/WRITE_SIZE summary of the config-4 kernels (tools/profile_config4.sh), "
+                         "matched by build id: the config-4 roofline's traffic")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_fetch_config3.json"),
                     help="rocprofv3 FETCH/WRITE_SIZE summary giving HBM traffic per k_fresh launch (matched by build id)")
     ap.add_argument("--dry-run-cpu", action="store_true",
@@ -330,14 +333,17 @@ def run_config(args, cfg, E, steps, warmup, world, rank, dev, key, mode):
     fresh_avg_ms = per_step[top] if cfg == 4 else fresh_ms / max(fresh_launches, 1)
     achieved = alg_bytes / (fresh_avg_ms / 1e3) / 1e9
     traffic = None
-    if world == 1 and os.path.exists(args.pmc):
+    pmc_path = args.pmc4 if cfg == 4 else args.pmc
+    if world == 1 and os.path.exists(pmc_path):
         try:
-            with open(args.pmc) as f:
+            with open(pmc_path) as f:
                 pm = json.load(f)
             if pm.get("events") == n and pm.get("config") == cfg and pm.get("build_id") == ebd.build_id():
-                traffic = pm["hbm_bytes_per_launch"]
+                # config 4: the top kernel's bytes per step (its launches of the step's poll cycles)
+                traffic = pm["kernels"][top]["hbm_bytes_per_step"] if cfg == 4 else pm["hbm_bytes_per_launch"]
             else:
-                log(f"[bench] {args.pmc} is for build {pm.get('build_id')} / {pm.get('events')} events: traffic null")
+                log(f"[bench] config {cfg}: {pmc_path} is for build {pm.get('build_id')}, config {pm.get('config')}, "
+                    f"{pm.get('events')} events; this run is build {ebd.build_id()}, {n} events: traffic null")
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -436,11 +442,12 @@ def main():
               "roofline": {"bound": "hbm", "kernel": m4["top"], "kernel_ms_per_step": m4["kernel_avg_ms"],
                            "achieved": m4["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": m4["achieved"] / HBM_PEAK_GBS, "alg_bytes_per_step": m4["alg_bytes"],
+                           "traffic": m4["traffic"],
                            "step_frac": m4["alg_bytes"] / (m4["ms_per_step"] / 1e3) / 1e9 / HBM_PEAK_GBS},
               "kernel_ms_per_step": m4["kernel_ms_per_step"], "errors": m4["errors"],
               "warm": m4["other"]}
         if not args.no_cpu_baseline:
-            cb = cpu_baseline(4, 4, args.cpu_seconds / 2, threads=False)
+            cb = cpu_baseline(4, m4["seed"], args.cpu_seconds / 2, threads=False)
             c4["cpu_baseline"] = cb
         c4["wall_s"] = time.perf_counter() - t4
     cpu = None

@@ -1274,18 +1274,15 @@ __global__ __launch_bounds__(64) void k_fresh_scan(Dev d) {
 		}
 		static_assert(kTileWords <= 16, "evpre scan covers 16 words");
 		// lanes over buffers: the request lines (P:162-262)
-#ifndef EBD_SX_STAGE
-#define EBD_SX_STAGE 9
-#endif
 		ReqOut rq;
 		rq.dec = SF_UNF;
-		if (mp && EBD_SX_STAGE >= 2) {
+		if (mp) {
 			rq = scan_reqline(src, B, m.L);
 			lds.evq[rank] = (uint16_t)(rq.dec == SF_GO && rq.q < E ? rq.q : 0xffffu);
 		}
 		wave_sync();
 		// lanes over lines: each listed line against the buffer it lies in (P:264-352)
-		for (uint32_t l0 = 0; l0 < (EBD_SX_STAGE >= 3 ? nlines : 0u); l0 += 64) {
+		for (uint32_t l0 = 0; l0 < nlines; l0 += 64) {
 			const uint32_t l = l0 + lane;
 			if (l < nlines) {
 				const uint32_t q = lds.lrec[l].a >> 16, pc = min(q >> 4, N - 1), wi = pc >> 6;
@@ -1306,10 +1303,10 @@ __global__ __launch_bounds__(64) void k_fresh_scan(Dev d) {
 				ScanOut o;
 				const uint32_t l0 = lds.evfirst[rank];
 				scan_init(o, m.L);
-				if (EBD_SX_STAGE >= 4 && !scan_fold(rq, [&](uint32_t l) { return lds.lrec[l < kLines ? l : 0]; }, l0, nlines, B, m.L, o) && EBD_SX_STAGE >= 5)
+				if (!scan_fold(rq, [&](uint32_t l) { return lds.lrec[l < kLines ? l : 0]; }, l0, nlines, B, m.L, o))
 					scan_exact(lds.tile, lds.nvw, lds.ncls, lds.cm, d.trie, B, m.L, o); // rare shapes (ebd_scan.h)
 				r = scan_result(o, (uint8_t)flags);
-				if (o.status == EBD_STATUS_FINISHED && EBD_SX_STAGE >= 6) {
+				if (o.status == EBD_STATUS_FINISHED) {
 					key = endpoint_key<2>(d.hkey, m.pid, o.host_off, o.host_len, o.url_off, o.url_len,
 							[&](uint32_t x) { return src.ld8(B + x); });
 					if (!(o.info & EBD_INFO_CIP)) { // the client is the session's source address (Aggregator.cpp:57-63)
@@ -2092,8 +2089,10 @@ __device__ __forceinline__ void walk_sessions(const Dev& d, const uint8_t* evf, 
 	const uint32_t hz = DRY ? dw.ctl->tend : 0u;
 	__shared__ __attribute__((aligned(16))) uint8_t tabs[kWalkLdsBytes];
 	uint32_t* s_next = (uint32_t*)(tabs + kWalkAttrOff + 256); // the workgroup's next ticket
-	uint32_t* s_base = s_next + 4;                            // chunk c's first session, at c % kWalkSlots
-	uint32_t* s_tag = s_base + kWalkSlots;                    // the chunk s_base holds
+	// chunk c's first session, at c % kWalkSlots: c << 32 | base in one 64-bit word, so that a
+	// reader sees the chunk and its base together (a tag seen, then a base already rewritten by
+	// chunk c + kWalkSlots, cannot happen)
+	unsigned long long* s_cb = (unsigned long long*)(s_next + 4);
 	// the sessions to walk: every one (k_walk_heads), or the exact-LRU round's list
 	const uint32_t* heads = hlist ? hlist : d.heads;
 	const uint32_t nh = hlist ? *hcount : (uint32_t)d.ctr[CTR_HEADS], nslow = (uint32_t)d.ctr[CTR_SLOW];
@@ -2109,7 +2108,7 @@ __device__ __forceinline__ void walk_sessions(const Dev& d, const uint8_t* evf, 
 	if (threadIdx.x < 256 / 16)
 		*(uint4*)(tabs + kWalkAttrOff + 16u * threadIdx.x) = *(const uint4*)(d.dfa + kLdsTableBytes + 16u * threadIdx.x);
 	if (threadIdx.x < kWalkSlots)
-		s_tag[threadIdx.x] = 0; // chunk 0 is never looked up
+		s_cb[threadIdx.x] = 0ull; // chunk 0 is never looked up
 	if (threadIdx.x == 0)
 		*s_next = kWalkThreads; // the lanes' first sessions are chunk 0
 	__syncthreads();
@@ -2134,17 +2133,21 @@ __device__ __forceinline__ void walk_sessions(const Dev& d, const uint8_t* evf, 
 		const uint32_t t = atomicAdd(s_next, 1u);
 		const uint32_t c = t / kWalkChunk, o = t % kWalkChunk, k = c % kWalkSlots;
 		if (o == 0) {
-			s_base[k] = gridDim.x * kWalkChunk + (uint32_t)atomicAdd(d.ctr + CTR_COUNT, (unsigned long long)kWalkChunk);
-			lds_store_rel(&s_tag[k], c);
+			const uint32_t b = gridDim.x * kWalkChunk + (uint32_t)atomicAdd(d.ctr + CTR_COUNT, (unsigned long long)kWalkChunk);
+			__hip_atomic_store(&s_cb[k], ((unsigned long long)c << 32) | b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 		}
-		for (uint32_t spins = 0; lds_load_acq(&s_tag[k]) != c; spins++) {
-			if (spins > (1u << 22)) { // cannot happen (the claimer runs unconditionally): reported, never hung on
+		unsigned long long cb;
+		for (uint32_t spins = 0; ((cb = __hip_atomic_load(&s_cb[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 32) != c;
+				spins++) {
+			// a later chunk in the slot (kWalkSlots chunks claimed while this lane waited), or the
+			// claimer never storing: neither can happen; reported, never followed or hung on
+			if ((cb >> 32) > c || spins > (1u << 22)) {
 				set_error(d, EBD_ERR_INTERNAL);
 				return kNone;
 			}
 			__builtin_amdgcn_s_sleep(1);
 		}
-		const uint32_t hh = s_base[k] + o;
+		const uint32_t hh = (uint32_t)cb + o;
 		return hh < nh ? hh : kNone;
 	};
 	const uint32_t h0 = blockIdx.x * kWalkThreads + threadIdx.x;

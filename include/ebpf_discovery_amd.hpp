@@ -94,6 +94,10 @@ struct HttpRequest {
 	std::string clientIPKey;
 	std::vector<std::string> clientIp;
 	bool isHttps = false;
+	/* not in the reference: the client-IP header had more than EBD_PARSE_MAX_TOKENS entries, so
+	 * clientIp lists only the first ones (the reference's vector has them all; the aggregator only
+	 * reads clientIp[0], Aggregator.cpp:57-63, so discovery results are unaffected) */
+	bool clientIpTruncated = false;
 
 	/* HttpRequest::clear (HttpRequestParser.cpp:67-80) */
 	void clear() {
@@ -103,6 +107,7 @@ struct HttpRequest {
 		host.clear();
 		clientIp.clear();
 		isHttps = false;
+		clientIpTruncated = false;
 	}
 };
 
@@ -185,6 +190,7 @@ private:
 		for (uint32_t k = 0; k < c.ntokens && k < EBD_PARSE_MAX_TOKENS; k++)
 			result.clientIp.push_back(span(c.tokens[k][0], c.tokens[k][1] - c.tokens[k][0]));
 		result.isHttps = c.is_https != 0;
+		result.clientIpTruncated = c.tokens_dropped != 0;
 	}
 
 	ebd_ctx* ctx_;

@@ -337,6 +337,19 @@ void parser_test_cases() {
 	CHECK(parser.isFinished() && !parser.isInvalidState());
 	CHECK(parser.result.clientIp == std::vector<std::string>{"9.9.9.9"});
 	CHECK(parser.result.clientIPKey == "x-forwarded-for");
+	CHECK(!parser.result.clientIpTruncated);
+	// more client tokens than EBD_PARSE_MAX_TOKENS: the first ones are listed and the result says so
+	{
+		std::string many;
+		for (int k = 0; k < EBD_PARSE_MAX_TOKENS + 3; k++)
+			many += (k ? "," : "") + std::to_string(k + 1) + ".0.0.1";
+		ebdamd::HttpRequestParser p;
+		p.parse("GET / HTTP/1.1\r\nX-Forwarded-For: " + many + "\r\n\r\n", EBD_FLAG_SESSION_UNENCRYPTED_HTTP);
+		CHECK(p.isFinished() && !p.isInvalidState());
+		CHECK(p.result.clientIp.size() == EBD_PARSE_MAX_TOKENS);
+		CHECK(p.result.clientIp.front() == "1.0.0.1");
+		CHECK(p.result.clientIpTruncated);
+	}
 }
 
 int run_gpu() {

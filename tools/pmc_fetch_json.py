@@ -35,22 +35,33 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--events", type=int, required=True)
     ap.add_argument("--config", type=int, required=True)
-    ap.add_argument("--kernel", default="k_fresh")
+    ap.add_argument("--kernel", default="k_fresh", help="kernel(s), comma-separated; the first is the summary's")
+    ap.add_argument("--launches-per-step", type=float, default=0,
+                    help="launches of each kernel per bench step (config 4: one per poll cycle): adds per-step bytes")
     ap.add_argument("--out", required=True)
     ap.add_argument("--fetch-scale", type=float, default=1.25)
     ap.add_argument("--build-id", required=True, help="ebd.build_id() of the library the passes measured")
     a = ap.parse_args()
-    fkib, nf = per_launch(a.fetch, "FETCH_SIZE", a.kernel)
-    out = {"kernel": a.kernel, "events": a.events, "config": a.config, "build_id": a.build_id, "dispatches": nf,
-           "fetch_size_kib_per_launch": fkib, "fetch_scale": a.fetch_scale,
-           "hbm_read_bytes_per_launch": fkib * 1024 * a.fetch_scale}
-    total = out["hbm_read_bytes_per_launch"]
-    if a.write:
-        wkib, _ = per_launch(a.write, "WRITE_SIZE", a.kernel)
-        out["write_size_kib_per_launch"] = wkib
-        out["hbm_write_bytes_per_launch"] = wkib * 1024
-        total += wkib * 1024
-    out["hbm_bytes_per_launch"] = total
+    kernels = a.kernel.split(",")
+    per = {}
+    for k in kernels:
+        fkib, nf = per_launch(a.fetch, "FETCH_SIZE", k)
+        e = {"dispatches": nf, "fetch_size_kib_per_launch": fkib, "hbm_read_bytes_per_launch": fkib * 1024 * a.fetch_scale}
+        total = e["hbm_read_bytes_per_launch"]
+        if a.write:
+            wkib, _ = per_launch(a.write, "WRITE_SIZE", k)
+            e["write_size_kib_per_launch"] = wkib
+            e["hbm_write_bytes_per_launch"] = wkib * 1024
+            total += wkib * 1024
+        e["hbm_bytes_per_launch"] = total
+        if a.launches_per_step:
+            e["hbm_bytes_per_step"] = total * a.launches_per_step
+        per[k] = e
+    out = {"kernel": kernels[0], "events": a.events, "config": a.config, "build_id": a.build_id,
+           "fetch_scale": a.fetch_scale, **per[kernels[0]]}
+    if len(kernels) > 1 or a.launches_per_step:
+        out["kernels"] = per
+        out["launches_per_step"] = a.launches_per_step
     out["note"] = ("FETCH_SIZE x 1024 x fetch_scale + WRITE_SIZE x 1024, averaged over the launches; fetch_scale is "
                    "measured on a stream of k_fresh's load shape with known bytes (profiles/r04_fetch_calibration.json: "
                    "x1.25; x2 for plain 16-B-per-lane streams, the guide's rule)")
