@@ -724,9 +724,6 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 		set_error(d, EBD_ERR_INTERNAL); // a record that cannot be real: reported, never followed
 		return false;
 	}
-	// the session's source address (Aggregator.cpp:60-66, 85-88), loaded first so that its latency
-	// overlaps the rescans: it classifies the client when the request has no client-IP header
-	const v4u sv = *(const __attribute__((address_space(1))) v4u*)((const uint8_t*)(d.ev + i) + 16);
 	ScanRec sr;
 	sr.url = Trk{q[R_C01] & 0xffffu, q[R_QS + 0]};
 	sr.host = Trk{q[R_C01] >> 16, q[R_QS + 1]};
@@ -741,14 +738,10 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 	const uint32_t two = 16 * sr.term.c + 4 * flip_quarter<RS_TERM>(d.di, sr.term, 0);
 	fresh_finalize(LdsTable{T}, d.di, sr, q[R_SF] & 0xffu, ((q[R_SF] >> 17) & 1u) != 0, StagedMem{p, fs, q[R_LIM], two, q[R_TW]}, L,
 			d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
-	if (fr.r.status == EBD_STATUS_FINISHED) {
+	// the client's class (source address or client-IP token) is k_agg_fast's: it reads the
+	// event records in event order, whole lines, where a read here came back from HBM
+	if (fr.r.status == EBD_STATUS_FINISHED)
 		d.keys[i] = fr.key;
-		if (!fr.cip) { // the client is the session's source address; a client-IP token is k_agg_fast's
-			uint8_t src[16];
-			__builtin_memcpy(src, &sv, 16);
-			fr.r.info = (uint8_t)(fr.r.info | (classify_source(*d.ifs, (uint8_t)(q[R_SF] >> 8), src) << EBD_INFO_CLASS_SHIFT));
-		}
-	}
 	d.res[i] = fr.r;
 	return fr.r.status == EBD_STATUS_UNFINISHED;
 }
@@ -1119,12 +1112,11 @@ struct TileSrc {
 	__device__ __forceinline__ unsigned long long clsword(uint32_t c, uint32_t a) const { return ((const unsigned long long*)cm[c])[a]; }
 };
 
-// An event's words as a lane of k_fresh holds them (Discovery.cpp:92-110: flags, pid, the
-// saved buffer; the source address classifies a client without a client-IP header).
+// An event's words as a lane of k_fresh_scan holds them (Discovery.cpp:92-110: flags, pid, the
+// saved buffer).
 struct ScanMeta {
 	uint32_t L, pid, fw, valid; // fw: the event's word at byte 32 (flags in its low byte)
 	unsigned long long off;
-	uint32_t src[4];
 };
 
 // Branch-free: a position past the range loads event rb's words (marked invalid), so every
@@ -1135,11 +1127,6 @@ __device__ __forceinline__ ScanMeta scan_meta(const Dev& d, uint32_t i, uint32_t
 	const uint32_t j = i < re ? i : rb;
 	const uint8_t* e = (const uint8_t*)(d.ev + j);
 	m.pid = *(const uint32_t*)e;
-	const v4u s = *(const __attribute__((address_space(1))) v4u_a1*)(e + 16);
-	m.src[0] = s.x;
-	m.src[1] = s.y;
-	m.src[2] = s.z;
-	m.src[3] = s.w;
 	m.fw = *(const uint32_t*)(e + 32);
 	m.L = d.len[j];
 	m.off = d.off[j];
@@ -1308,12 +1295,7 @@ __global__ __launch_bounds__(64) void k_fresh_scan(Dev d) {
 				r = scan_result(o, (uint8_t)flags);
 				if (o.status == EBD_STATUS_FINISHED) {
 					key = endpoint_key<2>(d.hkey, m.pid, o.host_off, o.host_len, o.url_off, o.url_len,
-							[&](uint32_t x) { return src.ld8(B + x); });
-					if (!(o.info & EBD_INFO_CIP)) { // the client is the session's source address (Aggregator.cpp:57-63)
-						uint8_t s16[16];
-						__builtin_memcpy(s16, m.src, 16);
-						r.info = (uint8_t)(r.info | (classify_source(*d.ifs, (uint8_t)flags, s16) << EBD_INFO_CLASS_SHIFT));
-					}
+							[&](uint32_t x) { return src.ld8(B + x); }); // the client's class is k_agg_fast's
 				}
 				unf = o.status == EBD_STATUS_UNFINISHED;
 			} else {
@@ -3266,15 +3248,16 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(EBD
 				cnt++;
 				if (r.info & EBD_INFO_CIP) {
 					queue = true;
-				} else if (!d.net_on) { // k_fresh classified the source address
-					agg_request(d, i, r, (r.info >> EBD_INFO_CLASS_SHIFT) & 3u, sh, 0);
-				} else { // the network maps need the address itself
+				} else { // the client is the session's source address (Aggregator.cpp:57-63)
 					const uint8_t* evb = (const uint8_t*)(d.ev + i);
 					const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16); // sourceIP (4-B aligned)
 					uint8_t src[16];
 					__builtin_memcpy(src, &sv, 16);
 					unsigned long long net = 0;
 					const uint32_t cls = classify_source(*d.ifs, evb[32], src, &net);
+					r.info = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT));
+					if (cls) // the class k_fresh leaves out, into the result's info byte (byte 3)
+						((uint8_t*)(d.res + i))[3] = r.info;
 					agg_request(d, i, r, cls, sh, net);
 				}
 			}
