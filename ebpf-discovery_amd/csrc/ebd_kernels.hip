@@ -421,7 +421,11 @@ struct Chunk {
 
 // 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
 __device__ __forceinline__ Chunk gload16(uintptr_t a) {
+#ifdef EBD_EXP_NTLOAD
+	const v4u v = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4u_a1*)a);
+#else
 	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
+#endif
 	Chunk c;
 	c.w[0] = v.x;
 	c.w[1] = v.y;
@@ -740,9 +744,20 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 			d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
 	// the client's class (source address or client-IP token) is k_agg_fast's: it reads the
 	// event records in event order, whole lines, where a read here came back from HBM
+#ifdef EBD_EXP_NTSTORE
+	if (fr.r.status == EBD_STATUS_FINISHED) {
+		v4u kv;
+		__builtin_memcpy(&kv, &fr.key, 16);
+		__builtin_nontemporal_store(kv, (__attribute__((address_space(1))) v4u*)(d.keys + i));
+	}
+	v4u rv;
+	__builtin_memcpy(&rv, &fr.r, 16);
+	__builtin_nontemporal_store(rv, (__attribute__((address_space(1))) v4u*)(d.res + i));
+#else
 	if (fr.r.status == EBD_STATUS_FINISHED)
 		d.keys[i] = fr.key;
 	d.res[i] = fr.r;
+#endif
 	return fr.r.status == EBD_STATUS_UNFINISHED;
 }
 

@@ -16,13 +16,16 @@ import collections
 import csv
 import glob
 import json
+import re
 
 
 def per_launch(d, counter, kernel):
+    # the kernel's own name, not a longer one that starts with it (k_walk, not k_walk_heads)
+    own = re.compile(r"(^|::|\s)" + re.escape(kernel) + r"\(")
     vals = collections.defaultdict(float)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if own.search(r["Kernel_Name"]) and r["Counter_Name"] == counter:
                 vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for {kernel} under {d}")
