@@ -59,8 +59,13 @@ hipError_t launch_owner_count(const ebd_service* rec, const unsigned long long* 
 		unsigned long long* bytes, hipStream_t st, int cus);
 hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long* ctr, uint32_t world, unsigned long long* cur,
 		ebd_wire_service* out, unsigned long long* srcoff, hipStream_t st, int cus);
-hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb, hipStream_t st, int cus);
-hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
+hipError_t launch_owner_prefix(const unsigned long long* cnt, uint32_t world, unsigned long long* cur, hipStream_t st);
+hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, unsigned long long* nb, hipStream_t st,
+		int cus);
+hipError_t launch_wire_seg_bytes(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		const unsigned long long* seg, uint32_t world, unsigned long long* out, hipStream_t st, int cus);
+hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, const unsigned long long* offs,
+		const unsigned long long* srcoff,
 		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus);
 hipError_t launch_merge(const Dev& d, const ebd_wire_service* rec, uint32_t n, const uint8_t* strings, unsigned long long strlen,
 		const unsigned long long* offs, hipStream_t st, int cus);
@@ -1171,6 +1176,18 @@ int ebd_fetch_results_async(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uin
 	return 0;
 }
 
+// A read into memory the caller owns (pageable as a rule): the stream is drained first, then one
+// blocking hipMemcpy, which returns only once the bytes are in the caller's buffer.  An async copy
+// into pageable memory followed by hipStreamSynchronize is the pattern that returned a stale parser
+// state from ebd_parse_streams: the runtime stages pageable copies itself,
+// and the stream's completion does not cover the host-side end of that staging.
+static hipError_t read_out(ebd_ctx* c, void* dst, const void* src, size_t bytes) {
+	hipError_t e = hipStreamSynchronize(c->stream);
+	if (e != hipSuccess || bytes == 0)
+		return e;
+	return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
 int ebd_fetch_results(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t* n) {
 	if (!c || !n || (cap && !out))
 		return -EINVAL;
@@ -1181,9 +1198,7 @@ int ebd_fetch_results(ebd_ctx* c, ebd_event_result* out, uint32_t cap, uint32_t*
 	if (cap < c->last_n)
 		return -ENOSPC;
 	HIP_TRY(hipSetDevice(c->device));
-	if (c->last_n)
-		HIP_TRY(hipMemcpyAsync(out, c->d_res, (size_t)c->last_n * sizeof(ebd_event_result), hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(read_out(c, out, c->d_res, (size_t)c->last_n * sizeof(ebd_event_result)));
 	return 0;
 }
 
@@ -1203,11 +1218,9 @@ int ebd_fetch_session_requests(ebd_ctx* c, ebd_session_request* out, uint32_t ca
 	if (cap < *n || strcap < *strlen)
 		return -ENOSPC;
 	HIP_TRY(hipSetDevice(c->device));
-	if (*n)
-		HIP_TRY(hipMemcpyAsync(out, c->d_sreq, (size_t)*n * sizeof(SessReq), hipMemcpyDeviceToHost, c->stream));
-	if (*strlen && strings)
-		HIP_TRY(hipMemcpyAsync(strings, c->d_sstr, *strlen, hipMemcpyDeviceToHost, c->stream));
-	HIP_TRY(hipStreamSynchronize(c->stream));
+	HIP_TRY(read_out(c, out, c->d_sreq, (size_t)*n * sizeof(SessReq)));
+	if (strings)
+		HIP_TRY(read_out(c, strings, c->d_sstr, *strlen));
 	return 0;
 }
 
@@ -1233,10 +1246,10 @@ int ebd_collect_services(ebd_ctx* c, ebd_service* out, uint32_t cap, uint32_t* n
 		if (!c->d_collect)
 			HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
 		HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
-		HIP_TRY(hipMemcpyAsync(out, c->d_collect, cnt * sizeof(ebd_service), hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(read_out(c, out, c->d_collect, cnt * sizeof(ebd_service)));
 	}
 	if (used)
-		HIP_TRY(hipMemcpyAsync(strings, c->d_sarena, used, hipMemcpyDeviceToHost, c->stream));
+		HIP_TRY(read_out(c, strings, c->d_sarena, used));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return 0;
 }
@@ -1490,7 +1503,7 @@ static hipError_t excl_scan(ebd_ctx* c, const unsigned long long* nb, unsigned l
 // The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
 // are n entries.
 static hipError_t wire_offsets(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, unsigned long long* nb, unsigned long long* offs) {
-	hipError_t e = launch_wire_bytes(recs, n, nb, c->stream, c->cus);
+	hipError_t e = launch_wire_bytes(recs, n, nullptr, nb, c->stream, c->cus);
 	return e != hipSuccess ? e : excl_scan(c, nb, offs, n);
 }
 
@@ -1542,13 +1555,64 @@ int ebd_export_services_device(ebd_ctx* c, uint32_t world, ebd_wire_service* rec
 			HIP_TRY(hipMemcpyAsync(own + 128, h + 128, 64 * sizeof(unsigned long long), hipMemcpyHostToDevice, c->stream));
 			HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, own + 128, recs, tmp, c->stream, c->cus));
 			HIP_TRY(wire_offsets(c, recs, (uint32_t)total, tmp + total, tmp + 2 * total));
-			HIP_TRY(launch_wire_copy(recs, (uint32_t)total, tmp + 2 * total, tmp, c->d_sarena, strings, c->stream, c->cus));
+			HIP_TRY(launch_wire_copy(recs, (uint32_t)total, nullptr, tmp + 2 * total, tmp, c->d_sarena, strings, c->stream, c->cus));
 			HIP_TRY(tmp_b.release());
 		}
 	}
 	HIP_TRY(own_b.release());
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	return rc;
+}
+
+int ebd_export_capacity(ebd_ctx* c, uint32_t* records, uint64_t* string_bytes) {
+	if (!c || !records || !string_bytes)
+		return -EINVAL;
+	*records = c->slot_cap;
+	*string_bytes = c->sarena_cap + 8;
+	return 0;
+}
+
+int ebd_export_services_device_sized(ebd_ctx* c, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings, uint64_t strcap,
+		uint64_t* sizes) {
+	if (!c || world == 0 || world > 64 || !recs || !strings || !sizes)
+		return -EINVAL;
+	if (cap < c->slot_cap || strcap < c->sarena_cap + 8)
+		return -ENOSPC; // the buffers must hold every service the table can have (ebd_export_capacity)
+	std::lock_guard<std::mutex> lk(c->mu);
+	ScratchScope scope(c);
+	HIP_TRY(hipSetDevice(c->device));
+	if (!c->d_collect)
+		HIP_TRY(hipMalloc(&c->d_collect, (size_t)c->slot_cap * sizeof(ebd_service)));
+	AsyncBuf tmp_b{c}; // cur (64), then srcoff, nb, offs (cap each)
+	HIP_TRY(tmp_b.alloc((64 + 3 * (size_t)cap) * sizeof(unsigned long long)));
+	unsigned long long* cur = (unsigned long long*)tmp_b.p;
+	unsigned long long* tmp = cur + 64;
+	unsigned long long* sz = (unsigned long long*)sizes;
+	const unsigned long long* nsvc = c->d_ctr + CTR_SERVICES; // the record count stays on the device
+	HIP_TRY(hipMemsetAsync(sz, 0, 2 * 64 * sizeof(unsigned long long), c->stream));
+	HIP_TRY(launch_collect(make_dev(c), c->d_collect, c->stream, c->cus));
+	HIP_TRY(launch_owner_count(c->d_collect, c->d_ctr, world, sz, sz + 64, c->stream, c->cus));
+	HIP_TRY(launch_owner_prefix(sz, world, cur, c->stream));
+	HIP_TRY(launch_owner_scatter(c->d_collect, c->d_ctr, world, cur, recs, tmp, c->stream, c->cus));
+	HIP_TRY(launch_wire_bytes(recs, cap, nsvc, tmp + cap, c->stream, c->cus));
+	HIP_TRY(excl_scan(c, tmp + cap, tmp + 2 * (size_t)cap, cap));
+	HIP_TRY(launch_wire_copy(recs, cap, nsvc, tmp + 2 * (size_t)cap, tmp, c->d_sarena, strings, c->stream, c->cus));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int ebd_wire_segment_bytes_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* need, const uint64_t* dst,
+		const uint64_t* seg_counts, uint32_t world, uint64_t* out) {
+	if (!c || world == 0 || world > 64 || !seg_counts || !out || (n && (!recs || (!need == !dst))))
+		return -EINVAL;
+	std::lock_guard<std::mutex> lk(c->mu);
+	HIP_TRY(hipSetDevice(c->device));
+	HIP_TRY(hipMemsetAsync(out, 0, (size_t)world * sizeof(uint64_t), c->stream));
+	if (n)
+		HIP_TRY(launch_wire_seg_bytes(recs, n, need, (const unsigned long long*)dst, (const unsigned long long*)seg_counts, world,
+				(unsigned long long*)out, c->stream, c->cus));
+	HIP_TRY(hipStreamSynchronize(c->stream));
+	return 0;
 }
 
 int ebd_merge_services_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen) {
@@ -1597,12 +1661,13 @@ int ebd_merge_service_keys_device(ebd_ctx* c, const ebd_wire_service* recs, uint
 
 int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n, const uint8_t* strings, uint64_t strlen,
 		const uint8_t* need, uint8_t* out, uint64_t outcap, uint64_t* out_len) {
-	if (!c || !out_len || (n && (!recs || !need || (!strings && strlen))))
+	if (!c || (!out_len && (!out || outcap < strlen)) || (n && (!recs || !need || (!strings && strlen))))
 		return -EINVAL;
 	std::lock_guard<std::mutex> lk(c->mu);
 	ScratchScope scope(c);
 	HIP_TRY(hipSetDevice(c->device));
-	*out_len = 0;
+	if (out_len)
+		*out_len = 0;
 	if (n == 0)
 		return 0;
 	AsyncBuf tmp_b{c}; // nb, soff, nbn, doff
@@ -1611,6 +1676,11 @@ int ebd_wire_compact_device(ebd_ctx* c, const ebd_wire_service* recs, uint32_t n
 	HIP_TRY(wire_offsets(c, recs, n, tmp, tmp + n));
 	HIP_TRY(launch_wire_bytes_needed(recs, n, need, nullptr, tmp + 2 * (size_t)n, c->stream, c->cus));
 	HIP_TRY(excl_scan(c, tmp + 2 * (size_t)n, tmp + 3 * (size_t)n, n));
+	if (!out_len) { // no size query: out holds all the strings, so it holds the needed ones
+		HIP_TRY(launch_wire_compact(recs, n, need, tmp + n, tmp + 3 * (size_t)n, strings, strlen, out, outcap, c->d_ctr, c->stream, c->cus));
+		HIP_TRY(hipStreamSynchronize(c->stream));
+		return 0;
+	}
 	unsigned long long* last = c->h_small; // the last record's needed bytes and offset: the total
 	HIP_TRY(hipMemcpyAsync(&last[0], tmp + 3 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipMemcpyAsync(&last[1], tmp + 4 * (size_t)n - 1, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));

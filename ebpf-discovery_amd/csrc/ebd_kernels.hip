@@ -3814,15 +3814,68 @@ __global__ void k_owner_scatter(const ebd_service* rec, const unsigned long long
 	}
 }
 
+// The segment starts of the owner-grouped export (an exclusive scan of the per-owner record counts,
+// world <= kOwnerMax): one thread, so that the export needs no host read of the counts.
+__global__ void k_owner_prefix(const unsigned long long* cnt, uint32_t world, unsigned long long* cur) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		unsigned long long s = 0;
+		for (uint32_t w = 0; w < world; w++) {
+			cur[w] = s;
+			s += cnt[w];
+		}
+	}
+}
+
 // Bytes each wire record's endpoint takes in the strings (the exclusive scan of this is its offset).
-__global__ void k_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb) {
+// nptr (device, optional): the records that exist; entries from there to n get 0.
+__global__ void k_wire_bytes(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, unsigned long long* nb) {
+	const unsigned long long m = nptr ? *nptr : n;
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x)
-		nb[k] = EBD_WIRE_BYTES(rec[k].endpoint_len);
+		nb[k] = k < m ? EBD_WIRE_BYTES(rec[k].endpoint_len) : 0ull;
+}
+
+// Per segment of records (segment s: seg[s] consecutive records, in order), the bytes of the
+// records that are on (need[k] != 0, or dst[k] != ~0 when need is null): the exchange's byte
+// counts per owner (source side) or per source (owner side), with no host read.
+__global__ void k_wire_seg_bytes(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		const unsigned long long* seg, uint32_t world, unsigned long long* out) {
+	__shared__ unsigned long long pre[kOwnerMax + 1], acc[kOwnerMax];
+	if (threadIdx.x == 0) {
+		unsigned long long s = 0;
+		for (uint32_t w = 0; w < world; w++) {
+			pre[w] = s;
+			s += seg[w];
+		}
+		pre[world] = s;
+	}
+	for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
+		acc[w] = 0;
+	__syncthreads();
+	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+		const bool on = need ? need[k] != 0 : dst[k] != ~0ull;
+		if (!on || k >= pre[world])
+			continue;
+		uint32_t lo = 0, hi = world - 1; // the last segment that starts at or before k
+		while (lo < hi) {
+			const uint32_t mid = (lo + hi + 1) >> 1;
+			if (pre[mid] <= k)
+				lo = mid;
+			else
+				hi = mid - 1;
+		}
+		atomicAdd(&acc[lo], (unsigned long long)EBD_WIRE_BYTES(rec[k].endpoint_len));
+	}
+	__syncthreads();
+	for (uint32_t w = threadIdx.x; w < world; w += blockDim.x)
+		if (acc[w])
+			atomicAdd(&out[w], acc[w]);
 }
 
 // Export: each record's endpoint bytes from the arena to its scanned place in the strings.
-__global__ void k_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
-		const uint8_t* arena, uint8_t* strings) {
+__global__ void k_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, const unsigned long long* offs,
+		const unsigned long long* srcoff, const uint8_t* arena, uint8_t* strings) {
+	if (nptr && *nptr < n)
+		n = (uint32_t)*nptr;
 	for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
 		const uint32_t nb = EBD_WIRE_BYTES(rec[k].endpoint_len);
 		const unsigned long long* src = (const unsigned long long*)(arena + srcoff[k]);
@@ -4496,13 +4549,23 @@ hipError_t launch_owner_scatter(const ebd_service* rec, const unsigned long long
 	hipLaunchKernelGGL(k_owner_scatter, dim3(cus * 8), dim3(256), 0, st, rec, ctr, world, cur, out, srcoff);
 	return hipGetLastError();
 }
-hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, unsigned long long* nb, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_wire_bytes, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, nb);
+hipError_t launch_owner_prefix(const unsigned long long* cnt, uint32_t world, unsigned long long* cur, hipStream_t st) {
+	hipLaunchKernelGGL(k_owner_prefix, dim3(1), dim3(64), 0, st, cnt, world, cur);
 	return hipGetLastError();
 }
-hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* offs, const unsigned long long* srcoff,
-		const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus) {
-	hipLaunchKernelGGL(k_wire_copy, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, offs, srcoff, arena, strings);
+hipError_t launch_wire_bytes(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, unsigned long long* nb, hipStream_t st,
+		int cus) {
+	hipLaunchKernelGGL(k_wire_bytes, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, nptr, nb);
+	return hipGetLastError();
+}
+hipError_t launch_wire_seg_bytes(const ebd_wire_service* rec, uint32_t n, const uint8_t* need, const unsigned long long* dst,
+		const unsigned long long* seg, uint32_t world, unsigned long long* out, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_seg_bytes, dim3(grid_for(n, 256, cus * 4)), dim3(256), 0, st, rec, n, need, dst, seg, world, out);
+	return hipGetLastError();
+}
+hipError_t launch_wire_copy(const ebd_wire_service* rec, uint32_t n, const unsigned long long* nptr, const unsigned long long* offs,
+		const unsigned long long* srcoff, const uint8_t* arena, uint8_t* strings, hipStream_t st, int cus) {
+	hipLaunchKernelGGL(k_wire_copy, dim3(grid_for(n, 256, cus * 8)), dim3(256), 0, st, rec, n, nptr, offs, srcoff, arena, strings);
 	return hipGetLastError();
 }
 hipError_t launch_agg_requests(const Dev& d, const ebd_request* rq, uint32_t n, const uint8_t* strings, hipStream_t st, int cus) {

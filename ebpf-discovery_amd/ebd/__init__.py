@@ -140,6 +140,11 @@ _SIGS = {
     "ebd_report_json": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ebd_export_services_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
                                              C.c_void_p, C.c_void_p]),
+    "ebd_export_capacity": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "ebd_export_services_device_sized": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64,
+                                                   C.c_void_p]),
+    "ebd_wire_segment_bytes_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                C.c_uint32, C.c_void_p]),
     "ebd_merge_services_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "ebd_merge_service_keys_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
     "ebd_wire_compact_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
@@ -512,6 +517,46 @@ class Context:
                "ebd_export_services_device")
         return recs[:n * WIRE_DTYPE.itemsize], strs[:sb], counts, scounts
 
+    def export_services_device_sized(self, world, device):
+        """ebd_export_services_device_sized: the services grouped by owner into buffers the context
+        keeps (capacity: the whole table), with nothing read back.  Returns (records uint8, strings
+        uint8, sizes): sizes is a device int64 [2, world] view, row 0 the records and row 1 the
+        string bytes per owner; records and strings are the capacity-sized buffers (their first
+        sum(sizes[0]) records and sum(sizes[1]) bytes are the export)."""
+        import torch
+        key = (str(device), world)
+        if getattr(self, "_exp_key", None) is None or self._exp_key[0] != key[0]:
+            r, sb = C.c_uint32(), C.c_uint64()
+            _check(lib().ebd_export_capacity(self.h, C.byref(r), C.byref(sb)), "ebd_export_capacity")
+            self._exp_bufs = (torch.empty(r.value * WIRE_DTYPE.itemsize, dtype=torch.uint8, device=device),
+                              torch.empty(max(sb.value, 8), dtype=torch.uint8, device=device),
+                              torch.empty(128, dtype=torch.int64, device=device))
+            self._exp_cap = r.value
+        self._exp_key = key
+        recs, strs, sizes = self._exp_bufs
+        self._fence(recs, strs, sizes, hold=False)
+        _check(lib().ebd_export_services_device_sized(self.h, world, C.c_void_p(recs.data_ptr()), self._exp_cap,
+                                                      C.c_void_p(strs.data_ptr()), strs.numel(), C.c_void_p(sizes.data_ptr())),
+               "ebd_export_services_device_sized")
+        return recs, strs, sizes.view(2, 64)[:, :world]
+
+    def wire_segment_bytes_device(self, recs, seg_counts, need=None, dst=None):
+        """ebd_wire_segment_bytes_device: per segment (seg_counts: device int64 [world], the
+        records of each segment in order) the endpoint bytes of the records whose need byte is set
+        (or whose dst is not -1): a device int64 [world] tensor, nothing read back."""
+        import torch
+        world = seg_counts.numel()
+        n = recs.numel() // WIRE_DTYPE.itemsize
+        out = torch.empty(world, dtype=torch.int64, device=seg_counts.device)
+        seg = seg_counts.to(torch.int64).contiguous()
+        self._fence(recs, seg, out, *(t for t in (need, dst) if t is not None), hold=False)
+        _check(lib().ebd_wire_segment_bytes_device(self.h, C.c_void_p(recs.data_ptr()) if n else None, n,
+                                                   C.c_void_p(need.data_ptr()) if need is not None else None,
+                                                   C.c_void_p(dst.data_ptr()) if dst is not None else None,
+                                                   C.c_void_p(seg.data_ptr()), world, C.c_void_p(out.data_ptr())),
+               "ebd_wire_segment_bytes_device")
+        return out
+
     def merge_services_device(self, recs, strings):
         """Inserts wire records (device uint8 tensors; strings readable 8 bytes past their
         bytes) into this table."""
@@ -533,9 +578,10 @@ class Context:
         _check(lib().ebd_merge_service_keys_device(self.h, C.c_void_p(recs.data_ptr()), n, C.c_void_p(dst.data_ptr())),
                "ebd_merge_service_keys_device")
 
-    def wire_compact_device(self, recs, strings, need):
+    def wire_compact_device(self, recs, strings, need, sized=True):
         """Source side of the bytes round: the endpoint bytes of the exported records whose
-        need byte is set, packed in record order (a device uint8 tensor)."""
+        need byte is set, packed in record order (a device uint8 tensor).  sized=False: no size
+        read; the whole strings-sized buffer comes back, the packed bytes at its start."""
         import torch
         n = recs.numel() // WIRE_DTYPE.itemsize
         assert need.dtype == torch.uint8 and need.numel() == n
@@ -544,6 +590,13 @@ class Context:
         self._fence(recs, strings, need, hold=False)
         ln = C.c_uint64(0)
         sp = C.c_void_p(strings.data_ptr()) if strings.numel() else None
+        if not sized:
+            out = torch.empty(max(strings.numel(), 8), dtype=torch.uint8, device=recs.device)
+            self._fence(out, hold=False)
+            _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
+                                                 C.c_void_p(need.data_ptr()), C.c_void_p(out.data_ptr()), out.numel(), None),
+                   "ebd_wire_compact_device")
+            return out
         _check(lib().ebd_wire_compact_device(self.h, C.c_void_p(recs.data_ptr()), n, sp, strings.numel(),
                                              C.c_void_p(need.data_ptr()), None, 0, C.byref(ln)), "ebd_wire_compact_device")
         out = torch.empty(max(int(ln.value), 8), dtype=torch.uint8, device=recs.device)

@@ -376,66 +376,89 @@ def device_exchange_merge(ctx, device, group=None, map_first=None, two_round=Tru
     records and every record's bytes.  With network counters the services' network-map
     entries follow their services to the owner (one more all_to_all of 32-byte records) and
     merge into its maps (union, later last-seen time).  map_first(first_seq int64 tensor) ->
-    trace positions, applied before the exchange.  Returns {sent, received, record_bytes,
-    string_bytes, need_bytes, string_bytes_one_round, net_sent, net_received}: this rank's
-    records out and in, and the bytes it sent."""
+    trace positions, applied before the exchange.
+
+    Host reads (D2H) per interval: the export leaves its per-owner counts on the device, they go
+    through the size all-to-all as they are, and ONE read takes both what this rank sends and what
+    it receives (records and string bytes).  That is the whole interval for one round.  The two-round
+    protocol reads once more: the bytes round's counts exist only after the owner's key merge has
+    decided which records it needs, so they are read (one D2H of both sides' counts, made by a
+    kernel of the library, ebd_wire_segment_bytes_device) between the two rounds.  Network maps,
+    when on, add the read of their record counts.
+
+    Returns {sent, received, record_bytes, string_bytes, need_bytes, string_bytes_one_round,
+    net_sent, net_received, export_ms, merge_ms, exchange_ms, host_reads}."""
     import time
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     t0 = time.perf_counter()
     check_same_hash_key(ctx, device, group)  # once per context and group
-    recs, strs, counts, scounts = ctx.export_services_device(world, device)  # counts: the export's one sync
-    if map_first is not None:
-        map_wire_first(recs, map_first)
+    recs_all, strs_all, sizes = ctx.export_services_device_sized(world, device)  # sizes: device [2, world]
     nets = ncounts = None
+    d2h = 0
     if getattr(ctx, "network_counters", False):
         nets, ncounts = group_by_owner(ctx.networks_device(device), NET_REC_BYTES, world)
+        d2h += 2  # the map dump's count and the grouping's counts
+    # per destination (records, string bytes); the size all-to-all takes them from the device
+    send = sizes.t().contiguous()  # [world, 2]
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    both = torch.cat([send.reshape(-1), recv.reshape(-1)]).cpu().numpy().astype(np.int64)  # the interval's read
+    d2h += 1
+    counts, scounts = both[0:2 * world:2], both[1:2 * world:2]
+    rc, rsc = both[2 * world::2], both[2 * world + 1::2]
+    n_out, s_out = int(counts.sum()), int(scounts.sum())
+    rb = REC.itemsize
+    recs, strs = recs_all[:n_out * rb], strs_all[:s_out]
+    if map_first is not None:
+        map_wire_first(recs, map_first)
     t_export = time.perf_counter()
     t_merge = 0.0  # the device merges' share (each C call returns when its work is done)
-    d2h = 1        # host reads of exchange sizes (the export's counts included)
+    n_in = int(rc.sum())
+    out_r = torch.empty(n_in * rb, dtype=torch.uint8, device=device)
+    dist.all_to_all_single(out_r, recs, output_split_sizes=[int(c) * rb for c in rc],
+                           input_split_sizes=[int(c) * rb for c in counts], group=group)
     if not two_round:
-        out_r, out_s = exchange(recs, strs, counts, scounts, group)
-        d2h += 2
+        ns = int(rsc.sum())
+        out_s = torch.zeros(ns + STR_SLACK, dtype=torch.uint8, device=device)
+        dist.all_to_all_single(out_s[:ns], strs, output_split_sizes=[int(c) for c in rsc],
+                               input_split_sizes=[int(c) for c in scounts], group=group)
         tm = time.perf_counter()
         ctx.reset_services()
         ctx.merge_services_device(out_r, out_s)
         t_merge += time.perf_counter() - tm
-        sent_bytes, need_bytes = strs.numel(), 0
+        sent_bytes, need_bytes = s_out, 0
     else:
-        out_r, rc = exchange_counts(recs, counts, REC.itemsize, group)
-        d2h += 1
         tm = time.perf_counter()
         ctx.reset_services()
-        n_in = out_r.numel() // REC.itemsize
         dst = torch.empty(n_in, dtype=torch.int64, device=device)
         a = int(np.sum(rc[:rank]))
         b = a + int(rc[rank])
-        rb = REC.itemsize
         # the owner's own records first: they create its services, and their bytes stay local
         ctx.merge_service_keys_device(out_r[a * rb:b * rb], dst[a:b])
         ctx.merge_service_keys_device(out_r[:a * rb], dst[:a])
         ctx.merge_service_keys_device(out_r[b * rb:], dst[b:])
         t_merge += time.perf_counter() - tm
         need_in = (dst >= 0).to(torch.uint8)
-        # one flag per record back to its source: both sides already know the sizes (the records'
-        # counts), so no size exchange and no host read
+        # one flag per record back to its source: both sides know the sizes (the records' counts)
         need = return_to_sources(need_in, rc, counts, group)
-        sbytes = ctx.wire_compact_device(recs, strs, need)
-        # the byte counts per owner and per source from the device in one read
-        bc = owner_byte_counts_device(recs, need, counts, world)
-        rbc = torch.empty_like(bc)
-        dist.all_to_all_single(rbc, bc, group=group)
-        both = torch.cat([bc, rbc]).cpu().numpy()
+        packed = ctx.wire_compact_device(recs, strs, need, sized=False)
+        # the bytes round's counts: per owner here, per source on the owner side, from the device
+        # in one read (both made by k_wire_seg_bytes; no count exchange: each side has both records)
+        bc = ctx.wire_segment_bytes_device(recs, send[:, 0], need=need)
+        rbc = ctx.wire_segment_bytes_device(out_r, recv[:, 0], dst=dst)
+        hb = torch.cat([bc, rbc]).cpu().numpy().astype(np.int64)
         d2h += 1
-        out_s = torch.zeros(int(both[world:].sum()) + STR_SLACK, dtype=torch.uint8, device=device)
-        dist.all_to_all_single(out_s[:int(both[world:].sum())], sbytes,
-                               output_split_sizes=[int(c) for c in both[world:]],
-                               input_split_sizes=[int(c) for c in both[:world]], group=group)
+        ns = int(hb[world:].sum())
+        out_s = torch.zeros(ns + STR_SLACK, dtype=torch.uint8, device=device)
+        dist.all_to_all_single(out_s[:ns], packed[:int(hb[:world].sum())],
+                               output_split_sizes=[int(c) for c in hb[world:]],
+                               input_split_sizes=[int(c) for c in hb[:world]], group=group)
         tm = time.perf_counter()
         ctx.merge_service_bytes_device(out_r, dst, out_s)
         t_merge += time.perf_counter() - tm
-        sent_bytes, need_bytes = sbytes.numel(), need_in.numel()
+        sent_bytes, need_bytes = int(hb[:world].sum()), need_in.numel()
     out_n = None
     if nets is not None:
         out_n = exchange_fixed(nets, ncounts, NET_REC_BYTES, group)
@@ -444,41 +467,13 @@ def device_exchange_merge(ctx, device, group=None, map_first=None, two_round=Tru
         ctx.merge_networks_device(out_n)
         t_merge += time.perf_counter() - tm
     t_end = time.perf_counter()
-    return {"sent": int(counts.sum()), "received": out_r.numel() // REC.itemsize,
+    return {"sent": n_out, "received": n_in,
             "record_bytes": recs.numel(), "string_bytes": sent_bytes, "need_bytes": need_bytes,
-            "string_bytes_one_round": strs.numel(),
+            "string_bytes_one_round": s_out,
             "net_sent": int(ncounts.sum()) if ncounts is not None else 0,
             "net_received": out_n.numel() // NET_REC_BYTES if out_n is not None else 0,
             "export_ms": (t_export - t0) * 1e3, "merge_ms": t_merge * 1e3,
             "exchange_ms": (t_end - t_export - t_merge) * 1e3, "host_reads": d2h}
-
-
-def owner_byte_counts_device(recs, need, counts, world):
-    """owner_byte_counts left on the device (int64 tensor of world entries)."""
-    import torch
-    n = recs.numel() // REC.itemsize
-    if n == 0:
-        return torch.zeros(world, dtype=torch.int64, device=recs.device)
-    ln = recs.view(torch.int32).view(n, REC.itemsize // 4)[:, 9].to(torch.int64) & 0xFFFFFFFF  # endpoint_len
-    nb = torch.where((ln & WIRE_NO_BYTES) != 0, torch.zeros_like(ln), (ln + 7) & ~7) * need.to(torch.int64)
-    own = torch.repeat_interleave(torch.arange(world, device=recs.device),
-                                  torch.tensor(np.asarray(counts, np.int64), device=recs.device))
-    return torch.zeros(world, dtype=torch.int64, device=recs.device).index_add_(0, own, nb)
-
-
-def owner_byte_counts(recs, need, counts, world):
-    """Per owner, the endpoint bytes of the needed records (device wire records grouped by
-    owner, counts[w] each; need: one uint8 flag per record) as a numpy int64 array."""
-    import torch
-    n = recs.numel() // REC.itemsize
-    if n == 0:
-        return np.zeros(world, np.int64)
-    ln = recs.view(torch.int32).view(n, REC.itemsize // 4)[:, 9].to(torch.int64) & 0xFFFFFFFF  # endpoint_len
-    nb = torch.where((ln & WIRE_NO_BYTES) != 0, torch.zeros_like(ln), (ln + 7) & ~7) * need.to(torch.int64)
-    own = torch.repeat_interleave(torch.arange(world, device=recs.device),
-                                  torch.tensor(np.asarray(counts, np.int64), device=recs.device))
-    bc = torch.zeros(world, dtype=torch.int64, device=recs.device).index_add_(0, own, nb)
-    return bc.cpu().numpy()
 
 
 NET_REC_BYTES = 32  # ebd_service_net

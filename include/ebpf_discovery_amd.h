@@ -382,6 +382,24 @@ typedef struct ebd_wire_service {
  * `world` entries.  recs == NULL: sizes only. */
 int ebd_export_services_device(ebd_ctx* ctx, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings,
 		uint64_t strcap, uint32_t* counts, uint64_t* str_counts);
+/* The interval merge with its sizes left on the device (one host read per
+ * interval in ebd/shard.py device_exchange_merge):
+ *  - ebd_export_capacity: the record and string-byte capacity that always holds the whole table
+ *    (every slot, the whole string arena + 8);
+ *  - ebd_export_services_device_sized: ebd_export_services_device into buffers of at least those
+ *    capacities, with sizes (DEVICE, 128 words) = [64 per-owner record counts][64 per-owner string
+ *    bytes] instead of host counts: nothing is read back, so the counts can go straight into the
+ *    size all-to-all;
+ *  - ebd_wire_segment_bytes_device: out[s] (DEVICE, world words) = the 8-padded endpoint bytes of
+ *    the records of segment s (seg_counts: DEVICE, world consecutive segments) whose need byte is
+ *    set, or (need NULL) whose dst is not ~0: the bytes round's counts per owner on the source side
+ *    and per source on the owner side;
+ *  - ebd_wire_compact_device with out_len NULL packs without the size read (outcap >= strlen). */
+int ebd_export_capacity(ebd_ctx* ctx, uint32_t* records, uint64_t* string_bytes);
+int ebd_export_services_device_sized(ebd_ctx* ctx, uint32_t world, ebd_wire_service* recs, uint32_t cap, uint8_t* strings,
+		uint64_t strcap, uint64_t* sizes);
+int ebd_wire_segment_bytes_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, const uint8_t* need, const uint64_t* dst,
+		const uint64_t* seg_counts, uint32_t world, uint64_t* out);
 /* Merges n wire records (DEVICE arrays; strings hold their bytes in record order, readable
  * 8 bytes past strlen) into the context's table: counters add (uint32), the record with the
  * smallest first word fixes scheme and host/url split (Aggregator.cpp:155-168 across GPUs),
@@ -397,7 +415,8 @@ int ebd_merge_services_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32
  *     the source had none).  Merge the owner's own records first and theirs are the creators.
  *  2. the owner returns need[k] = (dst[k] != ~0) to each record's source;
  *     ebd_wire_compact_device packs the bytes of the needed records (need: DEVICE, one byte per
- *     exported record) in record order; out == NULL: *out_len only;
+ *     exported record) in record order; out == NULL: *out_len only; out_len == NULL: no size
+ *     read (outcap >= strlen);
  *  3. ebd_merge_service_bytes_device copies the received bytes (in the order of the records
  *     with dst != ~0, readable 8 bytes past strlen) to the reserved places. */
 int ebd_merge_service_keys_device(ebd_ctx* ctx, const ebd_wire_service* recs, uint32_t n, uint64_t* dst);

@@ -281,15 +281,30 @@ def test_device_two_round_merge_ships_bytes_once_per_new_key():
     dev = torch.device("cuda:0")
     W = 3
     ev, lens, offs, payload = ebd.generate_host(3, 21, 0, 30000)
-    src = []  # per shard: (ctx, recs, strs, counts)
+    src = []  # per shard: (ctx, recs, strs, counts, device sizes)
+    RB = shard.REC.itemsize
     for idx in shard.shard_indices(ev, W):
         ctx = ebd.Context(max_events=max(len(idx), 1), max_payload=payload.size, hash_key=ebd.TEST_HASH_KEY)
         ctx.submit(ev[idx], lens[idx], offs[idx], payload)
-        recs, strs, counts, scounts = ctx.export_services_device(W, dev)
+        # the export whose counts stay on the device, checked against the host-counted one
+        h_recs, h_strs, h_counts, h_scounts = ctx.export_services_device(W, dev)
+        recs_all, strs_all, sz = ctx.export_services_device_sized(W, dev)
+        counts, scounts = sz.cpu().numpy()
+        assert counts.tolist() == h_counts.tolist() and scounts.tolist() == h_scounts.tolist()
+        recs, strs = recs_all[:int(counts.sum()) * RB], strs_all[:int(scounts.sum())]
+        for w, ((ra, sa), (rb_, sb)) in enumerate(zip(_owner_segments(recs, strs, counts, scounts),
+                                                      _owner_segments(h_recs, h_strs, h_counts, h_scounts))):
+            # same records per owner (order inside a segment is free), each with the same bytes
+            def rows(r, st):
+                recs_np = r.cpu().numpy().view(shard.REC)
+                nb = shard.wire_bytes(recs_np["endpoint_len"]).astype(np.int64)
+                so = np.concatenate([[0], np.cumsum(nb)])
+                b = st.cpu().numpy()
+                return sorted((bytes(recs_np[k].tobytes()), bytes(b[so[k]:so[k + 1]])) for k in range(recs_np.size))
+            assert rows(ra, sa) == rows(rb_, sb)
         gpos = torch.tensor(idx.astype(np.int64), device=dev)
         shard.map_wire_first(recs, lambda f: gpos[f])
-        src.append((ctx, recs, strs, counts))
-    RB = shard.REC.itemsize
+        src.append((ctx, recs, strs, counts, sz))
 
     def seg(s, w):  # source s's records for owner w
         c = src[s][3].astype(np.int64)
@@ -300,6 +315,7 @@ def test_device_two_round_merge_ships_bytes_once_per_new_key():
     for w in range(W):
         m = ebd.Context(max_events=1024, max_payload=64, hash_key=ebd.TEST_HASH_KEY)
         parts = [seg(s, w) for s in range(W)]
+        pcounts = torch.tensor([p.numel() // RB for p in parts], dtype=torch.int64, device=dev)
         dsts = [torch.empty(p.numel() // RB, dtype=torch.int64, device=dev) for p in parts]
         for s in [w] + [s for s in range(W) if s != w]:  # the owner's own records first
             m.merge_service_keys_device(parts[s], dsts[s])
@@ -310,22 +326,28 @@ def test_device_two_round_merge_ships_bytes_once_per_new_key():
                 keys = parts[s].view(torch.int64).view(-1, 5)[:, :2].cpu().numpy().tolist()
                 asked = need_for[s][w].cpu().numpy()
                 assert not any(a and tuple(k) in own_keys for a, k in zip(asked, keys))
-        owners.append((m, parts, dsts))
+        owners.append((m, parts, dsts, pcounts))
     sent = 0
     got = [[] for _ in range(W)]
+    bcs = []
     for s in range(W):
-        ctx, recs, strs, counts = src[s]
+        ctx, recs, strs, counts, sz = src[s]
         need = torch.cat([need_for[s][w] for w in range(W)])
-        packed = ctx.wire_compact_device(recs, strs, need)
-        bc = shard.owner_byte_counts(recs, need, counts, W)
-        assert int(bc.sum()) == packed.numel()
+        packed = ctx.wire_compact_device(recs, strs, need)  # with the size read
+        packed2 = ctx.wire_compact_device(recs, strs, need, sized=False)  # without it
+        bc = ctx.wire_segment_bytes_device(recs, sz[0], need=need).cpu().numpy()  # per owner, by the kernel
+        assert int(bc.sum()) == packed.numel() and torch.equal(packed2[:packed.numel()], packed)
+        bcs.append(bc)
         sent += packed.numel()
         a = 0
         for w in range(W):
             got[w].append(packed[a:a + int(bc[w])])
             a += int(bc[w])
+    for w, (m, parts, dsts, pcounts) in enumerate(owners):  # the owner's per-source counts, by the kernel
+        rbc = m.wire_segment_bytes_device(torch.cat(parts), pcounts, dst=torch.cat(dsts)).cpu().numpy()
+        assert rbc.tolist() == [int(bcs[s][w]) for s in range(W)]
     rows = []
-    for w, (m, parts, dsts) in enumerate(owners):
+    for w, (m, parts, dsts, _) in enumerate(owners):
         strs = torch.cat(got[w] + [torch.zeros(shard.STR_SLACK, dtype=torch.uint8, device=dev)])
         m.merge_service_bytes_device(torch.cat(parts), torch.cat(dsts), strs)
         assert m.stats()["errors"] == 0
@@ -356,6 +378,15 @@ def test_device_exchange_merge_over_rccl_world1():
         dist.destroy_process_group()
     assert x["sent"] == x["received"] == len(before)
     assert x["record_bytes"] == 40 * len(before)
+    assert x["host_reads"] == 2  # the sizes, then the bytes round's counts (two rounds)
+    assert ctx.services() == before
+    os.environ["MASTER_PORT"] = "29518"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        x = shard.device_exchange_merge(ctx, torch.device("cuda", 0), map_first=lambda f: f, two_round=False)
+    finally:
+        dist.destroy_process_group()
+    assert x["host_reads"] == 1  # one round: the sizes only
     assert ctx.services() == before
 
 
