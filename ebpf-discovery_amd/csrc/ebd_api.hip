@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <thread>
 #include <sys/random.h>
@@ -43,7 +44,9 @@ hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_sset_clear(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint32_t n, const uint8_t* data, hipStream_t st);
-hipError_t launch_publish(const Dev& d, hipStream_t st, int cus);
+hipError_t launch_publish(const Dev& d, uint32_t nblk, hipStream_t st, int cus);
+hipError_t launch_own(const Dev& d, hipStream_t st, int cus);
+uint32_t own_range_lg();
 uint32_t agg_stage_per_block(uint32_t n, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
 hipError_t launch_collect(const Dev& d, ebd_service* out, hipStream_t st, int cus);
@@ -140,7 +143,20 @@ struct ebd_ctx {
 	uint32_t* d_new_slots = nullptr;
 	ClaimRec* d_cstage = nullptr; // claim stage: max_events + blocks of slack
 	uint64_t cstage_cap = 0;
-	uint32_t* d_blk = nullptr;    // blk_cnt, blk_bytes (u32) then blk_lbase, blk_abase (u64)
+	uint32_t* d_blk = nullptr;    // blk_cnt, blk_bytes (u32) then blk_lbase, blk_abase (u64), blk_cap each
+	uint32_t blk_cap = 0;
+	// owned aggregation (k_own_*, ebd_kernels.hip): the table in 2048-slot ranges, one workgroup each
+	int own_on = 0;
+	uint32_t own_abits = 0, own_bbits = 0;
+	uint64_t own_n = 0;          // the batch size the entry buffers hold
+	OwnCtl* d_own_ctl = nullptr;
+	uint16_t* d_own_rid = nullptr;
+	uint8_t* d_own_sub = nullptr;
+	OwnEnt* d_ownA = nullptr;
+	OwnEnt* d_ownB = nullptr;
+	uint32_t* d_own_bcnt = nullptr;
+	unsigned long long* d_own_boff = nullptr;
+	unsigned long long* d_own_bcur = nullptr;
 	unsigned long long* d_list_ep = nullptr;
 	unsigned long long* d_list_pl = nullptr;
 	uint32_t new_cap = 0;
@@ -323,13 +339,24 @@ static Dev make_dev(ebd_ctx* c) {
 	d.keys = c->d_keys;
 	d.slots = c->d_slots;
 	d.slot_mask = c->slot_cap - 1;
+	d.probe_mask = c->own_on ? (1u << own_range_lg()) - 1u : d.slot_mask;
+	d.own_abits = c->own_abits;
+	d.own_bbits = c->own_bbits;
+	d.own_ctl = c->d_own_ctl;
+	d.own_rid = c->d_own_rid;
+	d.own_sub = c->d_own_sub;
+	d.ownA = c->d_ownA;
+	d.ownB = c->d_ownB;
+	d.own_bcnt = c->d_own_bcnt;
+	d.own_boff = c->d_own_boff;
+	d.own_bcur = c->d_own_bcur;
 	d.new_slots = c->d_new_slots;
 	d.cstage = c->d_cstage;
 	d.cstage_per = 0;
 	d.blk_cnt = c->d_blk;
-	d.blk_bytes = c->d_blk + kMaxAggBlocks;
-	d.blk_lbase = (unsigned long long*)(c->d_blk + 2 * kMaxAggBlocks);
-	d.blk_abase = d.blk_lbase + kMaxAggBlocks;
+	d.blk_bytes = c->d_blk + c->blk_cap;
+	d.blk_lbase = (unsigned long long*)(c->d_blk + 2 * (size_t)c->blk_cap);
+	d.blk_abase = d.blk_lbase + c->blk_cap;
 	d.list_ep = c->d_list_ep;
 	d.list_pl = c->d_list_pl;
 	d.new_cap = c->new_cap;
@@ -383,7 +410,8 @@ struct SlowKey {
 };
 
 static void ctx_free(ebd_ctx* c) {
-	void* ptrs[] = {c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots, c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
+	void* ptrs[] = {c->d_ownA, c->d_ownB, c->d_own_ctl, c->d_own_rid, c->d_own_sub, c->d_own_bcnt, c->d_own_boff, c->d_own_bcur, c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots,
+			c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
 			c->d_sset, c->d_dirty, c->d_evslot, c->d_smask, c->d_slow[0], c->d_slow[1], c->d_pieces, c->d_hrec, c->d_sort_tmp, c->d_sel_tmp, c->d_sel_cnt, c->d_carry[0], c->d_carry[1], c->d_sreq,
 			c->d_sstr, c->d_ctr, c->d_cnt, c->d_collect, c->d_lru_delta, c->d_lru_minus,
 			c->d_lru_scan, c->d_lru_tmp, c->d_lru_jpos, c->d_lru_head, c->d_lru_sess, c->d_lru_live, c->d_nets[0], c->d_nets[1],
@@ -543,8 +571,31 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	// one stretch of per-block capacity per k_agg_fast block: grid * ceil(steps / grid) steps of
 	// kAggThreads events, below (steps + grid) * kAggThreads for any batch up to max_events
 	c->cstage_cap = (((uint64_t)c->max_events + 255) / 256 + kMaxAggBlocks) * 256;
+	c->blk_cap = kMaxAggBlocks;
+	{
+		// the owned aggregation (opt-in) takes tables of 2^18 to 2^26 slots in ranges of
+		// 2^own_range_lg(): 2^own_abits buckets (<= 128) of 2^own_bbits ranges (<= 256); network
+		// counters keep k_agg_fast
+		uint32_t lg = 0;
+		while ((1ull << lg) < c->slot_cap)
+			lg++;
+		const uint32_t rbits = lg > own_range_lg() ? lg - own_range_lg() : 0;
+		const char* agg = getenv("EBD_AGG"); // "own": the owned aggregation (measured slower than k_agg_fast)
+		if (agg && !strcmp(agg, "own") && rbits >= 7 && rbits <= 15 && !(cfg->flags & EBD_CFG_NETWORK_COUNTERS)) {
+			c->own_on = 1;
+			c->own_bbits = rbits < 8 ? rbits : 8;
+			c->own_abits = rbits - c->own_bbits;
+			const uint64_t nr = 1ull << rbits;
+			c->blk_cap = (uint32_t)std::max<uint64_t>(kMaxAggBlocks, nr);
+			c->cstage_cap = std::max<uint64_t>(c->cstage_cap, nr << own_range_lg());
+			CTX_TRY(hipMalloc(&c->d_own_ctl, sizeof(OwnCtl)));
+			CTX_TRY(hipMalloc(&c->d_own_bcnt, nr * sizeof(uint32_t)));
+			CTX_TRY(hipMalloc(&c->d_own_boff, (nr + 1) * sizeof(unsigned long long)));
+			CTX_TRY(hipMalloc(&c->d_own_bcur, nr * sizeof(unsigned long long)));
+		}
+	}
 	CTX_TRY(hipMalloc(&c->d_cstage, c->cstage_cap * sizeof(ClaimRec)));
-	CTX_TRY(hipMalloc(&c->d_blk, (size_t)kMaxAggBlocks * (2 * sizeof(uint32_t) + 2 * sizeof(unsigned long long))));
+	CTX_TRY(hipMalloc(&c->d_blk, (size_t)c->blk_cap * (2 * sizeof(uint32_t) + 2 * sizeof(unsigned long long))));
 	CTX_TRY(hipMalloc(&c->d_list_ep, (size_t)c->new_cap * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_list_pl, (size_t)c->new_cap * sizeof(unsigned long long)));
 	c->verify_cap = c->max_events;
@@ -760,6 +811,29 @@ static int run_lru_rounds(ebd_ctx* c, const Dev& d, uint32_t nslow, int* settled
 	return 0;
 }
 
+// The owned aggregation's per-event and entry buffers for a batch of n events (entries are the
+// counted requests, at most one per event), grown when a larger batch comes.
+static hipError_t ensure_own(ebd_ctx* c, uint32_t n) {
+	if (n <= c->own_n && c->d_ownA)
+		return hipSuccess;
+	const uint64_t want = std::max<uint64_t>(n, 1u << 16);
+	hipError_t e = hipStreamSynchronize(c->stream);
+	if (e != hipSuccess)
+		return e;
+	void** bufs[] = {(void**)&c->d_ownA, (void**)&c->d_ownB, (void**)&c->d_own_rid, (void**)&c->d_own_sub};
+	for (void** b : bufs) {
+		if (*b)
+			(void)hipFree(*b);
+		*b = nullptr;
+	}
+	c->own_n = 0;
+	if ((e = hipMalloc(&c->d_ownA, want * sizeof(OwnEnt))) != hipSuccess || (e = hipMalloc(&c->d_ownB, want * sizeof(OwnEnt))) != hipSuccess ||
+			(e = hipMalloc(&c->d_own_rid, want * sizeof(uint16_t))) != hipSuccess || (e = hipMalloc(&c->d_own_sub, want)) != hipSuccess)
+		return e;
+	c->own_n = want;
+	return hipSuccess;
+}
+
 // One poll cycle on the context stream.  The host waits once, for the counters after the
 // fresh pass (is there session work?), while k_agg_fast already runs; a batch without session
 // work returns with its kernels still queued, and a batch with some returns once the session
@@ -804,8 +878,22 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 	HIP_TRY(hipEventRecord(c->ev_mid, c->stream));
 	// Aggregator::newRequest for the fast-path requests: independent of the session path
 	// (k_slow_collect marked the session events, counters and first arrival are order-free)
-	HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
-	HIP_TRY(timed(c, KT_PUBLISH, [&] { return launch_publish(d, c->stream, c->cus); }));
+	uint32_t pub_blocks = 0; // the claim stretches the publication walks (0: k_agg_fast's grid)
+	if (c->own_on) {
+		HIP_TRY(ensure_own(c, n));
+		d.own_rid = c->d_own_rid;
+		d.own_sub = c->d_own_sub;
+		d.ownA = c->d_ownA;
+		d.ownB = c->d_ownB;
+		d.cstage_per = 1u << own_range_lg();
+		pub_blocks = 1u << (c->own_abits + c->own_bbits);
+		HIP_TRY(hipMemsetAsync(c->d_own_ctl, 0, sizeof(OwnCtl), c->stream));
+		HIP_TRY(hipMemsetAsync(c->d_own_bcnt, 0, ((size_t)1 << (c->own_abits + c->own_bbits)) * sizeof(uint32_t), c->stream));
+		HIP_TRY(timed(c, KT_AGG, [&] { return launch_own(d, c->stream, c->cus); }));
+	} else {
+		HIP_TRY(timed(c, KT_AGG, [&] { return launch_agg_fast(d, c->stream, c->cus); }));
+	}
+	HIP_TRY(timed(c, KT_PUBLISH, [&] { return launch_publish(d, pub_blocks, c->stream, c->cus); }));
 	HIP_TRY(hipEventSynchronize(c->ev_mid));
 	const uint64_t nslow = c->h_ctr[CTR_SLOW];
 	const uint64_t dirty = c->h_ctr[CTR_DIRTY];

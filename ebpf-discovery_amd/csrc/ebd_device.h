@@ -186,6 +186,28 @@ EBD_HD bool stream_state_ok(const StreamParser& sp, uint64_t stream_len) {
 			sp.vstart <= sp.vend && sp.vend <= g.length && g.cipkey <= 5;
 }
 
+// A fast-path request on its way to the owned aggregation (k_own_emit -> k_own_part -> k_own):
+// the service key, the event, w = client class | isHttps << 2 | host length << 3, and what a
+// claim publishes (ClaimRec's fields), so that no pass reads the event again.
+struct OwnEnt {
+	unsigned long long lo, hi;
+	uint32_t i, w;
+	uint32_t pid;
+	uint16_t host_off, host_len, url_off, url_len;
+	uint32_t pad;
+	unsigned long long off;
+};
+static_assert(sizeof(OwnEnt) == 48, "owned-aggregation entry is 48 bytes");
+// The buckets of one batch (zeroed before it): entries per bucket, their starts and cursors in
+// ownA, and the 4096-entry tiles before each bucket (k_own_bcount and k_own_part take one tile
+// per block).
+struct OwnCtl {
+	unsigned long long acnt[256];
+	unsigned long long aoff[257];
+	unsigned long long acur[256];
+	uint32_t tcum[257];
+};
+
 struct Dev {
 	// immutable tables
 	const uint8_t* dfa;
@@ -208,6 +230,18 @@ struct Dev {
 	// service table
 	Slot* slots;
 	uint32_t slot_mask;
+	uint32_t probe_mask; // probing wraps inside probe_mask + 1 slots: kOwnSlots when the table is in ranges
+	// owned aggregation (k_own_*): the counted requests bucketed by range in two exact passes
+	// (2^own_abits buckets of 2^own_bbits ranges), each range then one workgroup's
+	uint32_t own_abits, own_bbits;
+	struct OwnCtl* own_ctl;
+	uint16_t* own_rid;   // per event: its range (0xffff: not a counted request)
+	uint8_t* own_sub;    // per bucket-ordered entry: its range within the bucket
+	struct OwnEnt* ownA; // entries by bucket
+	struct OwnEnt* ownB; // entries by range
+	uint32_t* own_bcnt;  // per range: entries
+	unsigned long long* own_boff; // per range: first entry in ownB (+ the total)
+	unsigned long long* own_bcur; // per range: next free entry
 	uint32_t* new_slots;
 	unsigned long long* list_ep; // beside new_slots: the endpoint's arena offset (~0: none)
 	unsigned long long* list_pl; // beside new_slots: pid | endpoint length << 32

@@ -140,6 +140,12 @@ EBD_HD unsigned long long first_word(unsigned long long seq, bool https, uint32_
 	return (seq << 16) | ((unsigned long long)(https ? 1u : 0u) << 15) | (hl & 0x7fffu);
 }
 
+// The next slot of a probe: linear, wrapping inside the key's range of probe_mask + 1 slots (the
+// whole table, or the 2048-slot range one k_own workgroup holds in LDS).
+__device__ __forceinline__ uint32_t probe_next(const Dev& d, uint32_t idx) {
+	return (idx & ~d.probe_mask) | ((idx + 1) & d.probe_mask);
+}
+
 // Returns the slot (kNone when the table is full); *claimed: this call created the service.
 // inc_int / inc_ext: the counter increments (one request: its class; a merged record: its counts).
 __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first, uint32_t inc_int, uint32_t inc_ext,
@@ -148,7 +154,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 	bool found = false;
 	*claimed = false;
 	unsigned long long seen_first = 0;
-	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
+	for (uint32_t probe = 0; probe <= d.probe_mask; probe++) {
 		Slot* s = d.slots + idx;
 		// One plain load pass over the slot's first 32 bytes.  tag and hi are written once
 		// (0 -> value), first only decreases: a stale copy at worst shows 0 (resolved by
@@ -190,7 +196,7 @@ __device__ uint32_t agg_insert(const Dev& d, Hash128 h, unsigned long long first
 			}
 			atomicAdd(&d.ctr[CTR_COLLISIONS], 1ull); // same tag, other key: keep probing
 		}
-		idx = (idx + 1) & d.slot_mask;
+		idx = probe_next(d, idx);
 	}
 	if (!found) {
 		set_error(d, EBD_ERR_TABLE_FULL);
@@ -421,11 +427,7 @@ struct Chunk {
 
 // 16-byte load through a global (not flat) pointer, any alignment: global_load_dwordx4
 __device__ __forceinline__ Chunk gload16(uintptr_t a) {
-#ifdef EBD_EXP_NTLOAD
-	const v4u v = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4u_a1*)a);
-#else
 	const v4u v = *(const __attribute__((address_space(1))) v4u_a1*)a;
-#endif
 	Chunk c;
 	c.w[0] = v.x;
 	c.w[1] = v.y;
@@ -744,20 +746,9 @@ __device__ __forceinline__ bool finalize_rec(const Dev& d, const uint8_t* T, con
 			d.hkey, q[R_PID], (uint8_t)(q[R_SF] >> 8), fr);
 	// the client's class (source address or client-IP token) is k_agg_fast's: it reads the
 	// event records in event order, whole lines, where a read here came back from HBM
-#ifdef EBD_EXP_NTSTORE
-	if (fr.r.status == EBD_STATUS_FINISHED) {
-		v4u kv;
-		__builtin_memcpy(&kv, &fr.key, 16);
-		__builtin_nontemporal_store(kv, (__attribute__((address_space(1))) v4u*)(d.keys + i));
-	}
-	v4u rv;
-	__builtin_memcpy(&rv, &fr.r, 16);
-	__builtin_nontemporal_store(rv, (__attribute__((address_space(1))) v4u*)(d.res + i));
-#else
 	if (fr.r.status == EBD_STATUS_FINISHED)
 		d.keys[i] = fr.key;
 	d.res[i] = fr.r;
-#endif
 	return fr.r.status == EBD_STATUS_UNFINISHED;
 }
 
@@ -3301,6 +3292,388 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(EBD
 	}
 }
 
+// ---------------------------------------------------------------------------------
+// Owned aggregation: Aggregator::newRequest (Aggregator.cpp:44-130, 155-168) for the fast-path
+// requests with the service table taken one range of kOwnSlots slots per workgroup, in LDS.
+//
+// k_agg_fast is bound by memory-side atomics: a probe read, a counter add and a first-arrival
+// max per request, plus a CAS and a store per new service, land on random 64-B lines at about
+// 20 G atomics/s chip-wide whatever the table's size (tools/ubench_regions.hip: the same work
+// one Infinity-Cache-sized region at a time is no faster).  Here the counted requests are
+// bucketed by the range of their first slot instead, in two passes of coalesced tile writes
+// with exact offsets (the requests of a service share its range, so the counts follow the
+// services' popularity and cannot be bounded in advance):
+//   k_own_count  per event its range (own_rid) and per-bucket counts;   k_own_scan_a  offsets;
+//   k_own_emit   the entries (key, class, claim fields) into their buckets (ownA, own_sub);
+//   k_own_bcount per-range counts from own_sub;                         k_own_scan_b  offsets;
+//   k_own_part   the entries into their ranges (ownB);
+//   k_own        one workgroup per range: its slots into LDS, its requests against them with
+//                LDS atomics, the changed slots back to the table.
+// Probing wraps inside the range (probe_next) for every other user of the table too.  Claims go
+// to the range's stretch of the claim stage (kOwnSlots per range: a claim takes a slot), so the
+// publication kernels run unchanged over one stretch per range.
+// ---------------------------------------------------------------------------------
+constexpr uint32_t kOwnLg = 11, kOwnSlots = 1u << kOwnLg;
+constexpr uint32_t kOwnTile = 4096;                  // events or entries per block tile
+constexpr unsigned long long kOwnLocked = 2;         // an LDS tag while its claimer writes hi (tags are odd)
+constexpr uint16_t kOwnNone = 0xffff;
+
+__device__ __forceinline__ uint32_t own_range(const Dev& d, unsigned long long lo) { return ((uint32_t)lo & d.slot_mask) >> kOwnLg; }
+
+__device__ __forceinline__ bool own_counted(const ebd_event_result& r) {
+	return r.status == EBD_STATUS_FINISHED && !(r.info & EBD_INFO_SESSION); // what k_agg_fast aggregates
+}
+
+// Per event: k_agg_fast's selection and client class (the class written into the result), its
+// range, and per tile the bucket counts (one atomic per bucket and tile).  Requests with a client-IP
+// header are queued per wave and their tokens parsed 64 at a time on full waves, as in k_agg_fast.
+__device__ __forceinline__ void own_cip_one(const Dev& d, uint32_t i, uint8_t* row) {
+	ebd_event_result r = d.res[i];
+	unsigned long long net = 0;
+	const uint32_t cls = cip_classify(d, i, r, row, &net);
+	r.info = (uint8_t)((r.info & ~(3u << EBD_INFO_CLASS_SHIFT)) | (cls << EBD_INFO_CLASS_SHIFT));
+	d.res[i] = r;
+}
+
+__global__ __launch_bounds__(256) void k_own_count(Dev d) {
+	__shared__ __attribute__((aligned(8))) uint8_t rows[256 * kCipStride];
+	__shared__ uint32_t cq[4][kCipRing];
+	__shared__ uint32_t hist[256];
+	__shared__ unsigned long long nreq;
+	const uint32_t nb = 1u << d.own_abits, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	uint8_t* row = rows + threadIdx.x * kCipStride;
+	uint32_t* q = cq[wave];
+	uint32_t qh = 0, qn = 0; // wave-uniform: ring head and queued requests
+	if (threadIdx.x == 0)
+		nreq = 0;
+	uint32_t cnt = 0;
+	for (unsigned long long t0 = (unsigned long long)blockIdx.x * kOwnTile; t0 < d.n; t0 += (unsigned long long)gridDim.x * kOwnTile) {
+		for (uint32_t b = threadIdx.x; b < nb; b += 256)
+			hist[b] = 0;
+		__syncthreads();
+#pragma unroll 1
+		for (uint32_t j = 0; j < kOwnTile / 256; j++) {
+			const unsigned long long ii = t0 + j * 256 + threadIdx.x;
+			bool queue = false;
+			if (ii < d.n) {
+				const uint32_t i = (uint32_t)ii;
+				const ebd_event_result r = d.res[i];
+				uint16_t rid = kOwnNone;
+				if (own_counted(r)) {
+					cnt++;
+					rid = (uint16_t)own_range(d, d.keys[i].lo);
+					atomicAdd(&hist[rid >> d.own_bbits], 1u);
+					if (r.info & EBD_INFO_CIP) { // the client is clientIp.front() (Aggregator.cpp:50-56)
+						queue = true;
+					} else { // the session's source address (Aggregator.cpp:57-63)
+						const uint8_t* evb = (const uint8_t*)(d.ev + i);
+						const v4u sv = *(const __attribute__((address_space(1))) v4u*)(evb + 16);
+						uint8_t src[16];
+						__builtin_memcpy(src, &sv, 16);
+						const uint32_t cls = classify_source(*d.ifs, evb[32], src);
+						if (cls)
+							((uint8_t*)(d.res + i))[3] = (uint8_t)(r.info | (cls << EBD_INFO_CLASS_SHIFT));
+					}
+				}
+				d.own_rid[i] = rid;
+			}
+			const unsigned long long bq = __ballot(queue);
+			if (queue)
+				q[(qh + qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0))) & (kCipRing - 1)] =
+						(uint32_t)ii;
+			qn += (uint32_t)__popcll(bq);
+			if (qn >= 64) { // a full wave of client-IP requests
+				wave_sync();
+				own_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row);
+				qh += 64;
+				qn -= 64;
+				wave_sync(); // the ring words just read may be rewritten
+			}
+		}
+		__syncthreads();
+		for (uint32_t b = threadIdx.x; b < nb; b += 256)
+			if (hist[b])
+				atomicAdd(&d.own_ctl->acnt[b], (unsigned long long)hist[b]);
+		__syncthreads();
+	}
+	wave_sync();
+	if (lane < qn) // what is left in the ring
+		own_cip_one(d, q[(qh + lane) & (kCipRing - 1)], row);
+	atomicAdd(&nreq, (unsigned long long)cnt);
+	__syncthreads();
+	if (threadIdx.x == 0 && nreq)
+		atomicAdd(&d.ctr[CTR_REQUESTS], nreq);
+}
+
+// One thread: the buckets' starts, cursors and tile counts.
+__global__ void k_own_scan_a(Dev d) {
+	if (blockIdx.x != 0 || threadIdx.x != 0)
+		return;
+	OwnCtl& c = *d.own_ctl;
+	const uint32_t nb = 1u << d.own_abits;
+	unsigned long long s = 0;
+	uint32_t t = 0;
+	for (uint32_t b = 0; b < nb; b++) {
+		c.aoff[b] = c.acur[b] = s;
+		c.tcum[b] = t;
+		s += c.acnt[b];
+		t += (uint32_t)((c.acnt[b] + kOwnTile - 1) / kOwnTile);
+	}
+	c.aoff[nb] = s;
+	c.tcum[nb] = t;
+}
+
+// The bucket tile a block takes: bucket b and entries [*e0, *e1) of ownA; false past the last tile.
+__device__ __forceinline__ bool own_tile(const Dev& d, uint32_t k, uint32_t* b, unsigned long long* e0, unsigned long long* e1) {
+	const OwnCtl& c = *d.own_ctl;
+	const uint32_t nb = 1u << d.own_abits;
+	if (k >= c.tcum[nb])
+		return false;
+	uint32_t lo = 0, hi = nb - 1; // the last bucket whose tiles start at or before k
+	while (lo < hi) {
+		const uint32_t mid = (lo + hi + 1) >> 1;
+		if (c.tcum[mid] <= k)
+			lo = mid;
+		else
+			hi = mid - 1;
+	}
+	*b = lo;
+	*e0 = c.aoff[lo] + (unsigned long long)(k - c.tcum[lo]) * kOwnTile;
+	*e1 = c.aoff[lo + 1] < *e0 + kOwnTile ? c.aoff[lo + 1] : *e0 + kOwnTile;
+	return true;
+}
+
+// Pass A: each counted request as an OwnEnt at its bucket's next places (the result already holds
+// its class); one reservation per bucket and tile.
+__global__ __launch_bounds__(256) void k_own_emit(Dev d) {
+	__shared__ uint32_t hist[256];
+	__shared__ unsigned long long base[256];
+	const uint32_t nb = 1u << d.own_abits, smask = (1u << d.own_bbits) - 1u;
+	for (unsigned long long t0 = (unsigned long long)blockIdx.x * kOwnTile; t0 < d.n; t0 += (unsigned long long)gridDim.x * kOwnTile) {
+		for (uint32_t b = threadIdx.x; b < nb; b += 256)
+			hist[b] = 0;
+		__syncthreads();
+		uint32_t pk[kOwnTile / 256]; // rank in the bucket << 16 | range
+#pragma unroll
+		for (uint32_t j = 0; j < kOwnTile / 256; j++) {
+			const unsigned long long i = t0 + j * 256 + threadIdx.x;
+			pk[j] = ~0u;
+			const uint32_t rid = i < d.n ? d.own_rid[i] : kOwnNone;
+			if (rid != kOwnNone)
+				pk[j] = (atomicAdd(&hist[rid >> d.own_bbits], 1u) << 16) | rid;
+		}
+		__syncthreads();
+		for (uint32_t b = threadIdx.x; b < nb; b += 256)
+			if (hist[b])
+				base[b] = atomicAdd(&d.own_ctl->acur[b], (unsigned long long)hist[b]);
+		__syncthreads();
+#pragma unroll
+		for (uint32_t j = 0; j < kOwnTile / 256; j++) {
+			if (pk[j] == ~0u)
+				continue;
+			const uint32_t i = (uint32_t)(t0 + j * 256 + threadIdx.x), rid = pk[j] & 0xffffu;
+			const ebd_event_result r = d.res[i];
+			const Hash128 key = d.keys[i];
+			OwnEnt e;
+			e.lo = key.lo;
+			e.hi = key.hi;
+			e.i = i;
+			e.w = ((r.info >> EBD_INFO_CLASS_SHIFT) & 3u) | ((r.info & EBD_INFO_HTTPS) ? 4u : 0u) | ((uint32_t)r.u.span.host_len << 3);
+			e.pid = d.ev[i].pid;
+			e.host_off = r.u.span.host_off;
+			e.host_len = r.u.span.host_len;
+			e.url_off = r.u.span.url_off;
+			e.url_len = r.u.span.url_len;
+			e.pad = 0;
+			e.off = d.off[i];
+			const unsigned long long pos = base[rid >> d.own_bbits] + (pk[j] >> 16);
+			d.ownA[pos] = e;
+			d.own_sub[pos] = (uint8_t)(rid & smask);
+		}
+		__syncthreads(); // hist and base are rewritten by the next tile
+	}
+}
+
+// Per bucket tile: its entries' counts per range (one atomic per range and tile).
+__global__ __launch_bounds__(256) void k_own_bcount(Dev d) {
+	__shared__ uint32_t hist[256];
+	uint32_t bk;
+	unsigned long long e0, e1;
+	if (!own_tile(d, blockIdx.x, &bk, &e0, &e1))
+		return;
+	const uint32_t nsub = 1u << d.own_bbits;
+	for (uint32_t x = threadIdx.x; x < nsub; x += 256)
+		hist[x] = 0;
+	__syncthreads();
+	for (unsigned long long k = e0 + threadIdx.x; k < e1; k += 256)
+		atomicAdd(&hist[d.own_sub[k]], 1u);
+	__syncthreads();
+	for (uint32_t x = threadIdx.x; x < nsub; x += 256)
+		if (hist[x])
+			atomicAdd(&d.own_bcnt[(bk << d.own_bbits) | x], hist[x]);
+}
+
+// One block: the ranges' starts (exclusive scan of own_bcnt) and cursors; every thread scans a
+// run of consecutive ranges, the runs' totals are scanned across the block.
+__global__ __launch_bounds__(1024) void k_own_scan_b(Dev d) {
+	__shared__ unsigned long long part[1024];
+	const uint32_t nr = 1u << (d.own_abits + d.own_bbits), per = (nr + 1023) / 1024;
+	const uint32_t r0 = threadIdx.x * per, r1 = min(nr, r0 + per);
+	unsigned long long s = 0;
+	for (uint32_t r = r0; r < r1; r++)
+		s += d.own_bcnt[r];
+	part[threadIdx.x] = s;
+	__syncthreads();
+	for (uint32_t o = 1; o < 1024; o <<= 1) {
+		const unsigned long long a = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+		__syncthreads();
+		part[threadIdx.x] += a;
+		__syncthreads();
+	}
+	unsigned long long at = part[threadIdx.x] - s;
+	for (uint32_t r = r0; r < r1; r++) {
+		d.own_boff[r] = d.own_bcur[r] = at;
+		at += d.own_bcnt[r];
+	}
+	if (threadIdx.x == 1023)
+		d.own_boff[nr] = part[1023];
+}
+
+// Pass B: one bucket tile's entries to their ranges' next places in ownB.
+__global__ __launch_bounds__(256) void k_own_part(Dev d) {
+	__shared__ uint32_t hist[256];
+	__shared__ unsigned long long base[256];
+	uint32_t bk;
+	unsigned long long e0, e1;
+	if (!own_tile(d, blockIdx.x, &bk, &e0, &e1))
+		return;
+	const uint32_t nsub = 1u << d.own_bbits;
+	for (uint32_t x = threadIdx.x; x < nsub; x += 256)
+		hist[x] = 0;
+	__syncthreads();
+	uint32_t pk[kOwnTile / 256]; // rank in the range << 8 | range within the bucket
+#pragma unroll
+	for (uint32_t j = 0; j < kOwnTile / 256; j++) {
+		const unsigned long long k = e0 + j * 256 + threadIdx.x;
+		pk[j] = ~0u;
+		if (k < e1) {
+			const uint32_t sub = d.own_sub[k];
+			pk[j] = (atomicAdd(&hist[sub], 1u) << 8) | sub;
+		}
+	}
+	__syncthreads();
+	for (uint32_t x = threadIdx.x; x < nsub; x += 256)
+		if (hist[x])
+			base[x] = atomicAdd(&d.own_bcur[(bk << d.own_bbits) | x], (unsigned long long)hist[x]);
+	__syncthreads();
+#pragma unroll
+	for (uint32_t j = 0; j < kOwnTile / 256; j++)
+		if (pk[j] != ~0u)
+			d.ownB[base[pk[j] & 0xffu] + (pk[j] >> 8)] = d.ownA[e0 + j * 256 + threadIdx.x];
+}
+
+// A range's slot as k_own holds it in LDS: the fields newRequest changes (Slot's first 24 bytes
+// and its two client counters).
+struct OwnSlot {
+	unsigned long long tag, hi, nfirst;
+	uint32_t ic, ec;
+};
+
+// Pass C: one workgroup per range.  A claim takes an empty slot in two steps (CAS 0 -> kOwnLocked,
+// hi, then the tag with release), all inside one loop iteration of the claiming lane, so a lane
+// that reads kOwnLocked only re-reads the slot: its claimer is either a lane of the same wave in
+// the same iteration or another wave, and neither waits for it.
+__global__ __launch_bounds__(256) void k_own(Dev d) {
+	__shared__ OwnSlot ls[kOwnSlots];
+	__shared__ uint8_t dirty[kOwnSlots];
+	__shared__ uint32_t nclaim;
+	const uint32_t rg = blockIdx.x;
+	Slot* g = d.slots + ((size_t)rg << kOwnLg);
+	for (uint32_t k = threadIdx.x; k < kOwnSlots; k += 256) {
+		const ulonglong2 th = *(const ulonglong2*)&g[k].tag;
+		ls[k].tag = th.x;
+		ls[k].hi = th.y;
+		ls[k].nfirst = g[k].nfirst;
+		ls[k].ic = g[k].internal_clients;
+		ls[k].ec = g[k].external_clients;
+		dirty[k] = 0;
+	}
+	if (threadIdx.x == 0)
+		nclaim = 0;
+	__syncthreads();
+	const unsigned long long b = d.own_boff[rg], e = d.own_boff[rg + 1];
+	OwnEnt nx;
+	if (b + threadIdx.x < e)
+		nx = d.ownB[b + threadIdx.x];
+	for (unsigned long long j = b + threadIdx.x; j < e; j += 256) {
+		const OwnEnt q = nx;
+		if (j + 256 < e) // the next entry's load goes out before this one's probe
+			nx = d.ownB[j + 256];
+		uint32_t idx = (uint32_t)q.lo & (kOwnSlots - 1u);
+		bool claimed = false, found = false;
+		for (uint32_t p = 0; p < kOwnSlots;) {
+			const unsigned long long t = __hip_atomic_load(&ls[idx].tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+			if (t == 0) {
+				unsigned long long want = 0;
+				if (__hip_atomic_compare_exchange_strong(&ls[idx].tag, &want, kOwnLocked, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+							__HIP_MEMORY_SCOPE_WORKGROUP)) {
+					ls[idx].hi = q.hi;
+					__hip_atomic_store(&ls[idx].tag, q.lo, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+					claimed = found = true;
+					break;
+				}
+				continue; // another lane took it: read it again
+			}
+			if (t == kOwnLocked)
+				continue; // its claimer finishes within its own iteration
+			if (t == q.lo) {
+				if (ls[idx].hi == q.hi) {
+					found = true;
+					break;
+				}
+				atomicAdd(&d.ctr[CTR_COLLISIONS], 1ull); // same tag, other key: keep probing
+			}
+			idx = (idx + 1u) & (kOwnSlots - 1u);
+			p++;
+		}
+		if (!found) {
+			set_error(d, EBD_ERR_TABLE_FULL);
+			continue;
+		}
+		const uint32_t cls = q.w & 3u;
+		if (cls == CLS_INTERNAL)
+			atomicAdd(&ls[idx].ic, 1u);
+		else if (cls == CLS_EXTERNAL)
+			atomicAdd(&ls[idx].ec, 1u);
+		const unsigned long long nf = ~first_word(d.seq_base + q.i, (q.w & 4u) != 0, q.w >> 3); // the slot keeps ~first
+		if (nf > ls[idx].nfirst)
+			atomicMax(&ls[idx].nfirst, nf);
+		dirty[idx] = 1;
+		if (claimed) { // at most one claim per slot: the range's stretch holds them all
+			ClaimRec cr;
+			cr.slot = (rg << kOwnLg) | idx;
+			cr.pid = q.pid;
+			cr.host_off = q.host_off;
+			cr.host_len = q.host_len;
+			cr.url_off = q.url_off;
+			cr.url_len = q.url_len;
+			cr.off = q.off;
+			d.cstage[(unsigned long long)rg * kOwnSlots + atomicAdd(&nclaim, 1u)] = cr;
+		}
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < kOwnSlots; k += 256) {
+		if (!dirty[k])
+			continue;
+		*(ulonglong2*)&g[k].tag = make_ulonglong2(ls[k].tag, ls[k].hi);
+		g[k].nfirst = ls[k].nfirst;
+		g[k].internal_clients = ls[k].ic;
+		g[k].external_clients = ls[k].ec;
+	}
+	if (threadIdx.x == 0)
+		d.blk_cnt[rg] = nclaim;
+}
+
 // ---- publication of the services k_agg_fast created (one block per k_agg_fast block) ----
 constexpr int kPubThreads = 256, kPubClaims = kPubThreads / 4;
 
@@ -3383,37 +3756,41 @@ __global__ __launch_bounds__(kPubThreads) void k_pub_count(Dev d) {
 }
 
 // Pass 2 (one block): each block's first list entry and arena offset; the list and arena grow.
+// 2048 blocks per round (two per thread, a Hillis-Steele scan over the pairs), a carry between.
 __global__ __launch_bounds__(1024) void k_pub_scan(Dev d, uint32_t nblk) {
 	__shared__ unsigned long long cs[1024], bs[1024];
 	const uint32_t t = threadIdx.x;
-	// nblk <= 2 * 1024: each thread sums two blocks, a Hillis-Steele scan over the pairs
-	const uint32_t b0 = 2 * t, b1 = 2 * t + 1;
-	const unsigned long long c0 = b0 < nblk ? d.blk_cnt[b0] : 0, c1 = b1 < nblk ? d.blk_cnt[b1] : 0;
-	const unsigned long long y0 = b0 < nblk ? d.blk_bytes[b0] : 0, y1 = b1 < nblk ? d.blk_bytes[b1] : 0;
-	cs[t] = c0 + c1;
-	bs[t] = y0 + y1;
-	__syncthreads();
-	for (uint32_t o = 1; o < 1024; o <<= 1) {
-		const unsigned long long a = t >= o ? cs[t - o] : 0, z = t >= o ? bs[t - o] : 0;
+	unsigned long long lbase = d.ctr[CTR_SERVICES], abase = d.ctr[CTR_SARENA]; // the same in every thread
+	for (uint32_t r0 = 0; r0 < nblk; r0 += 2048) {
+		const uint32_t b0 = r0 + 2 * t, b1 = b0 + 1;
+		const unsigned long long c0 = b0 < nblk ? d.blk_cnt[b0] : 0, c1 = b1 < nblk ? d.blk_cnt[b1] : 0;
+		const unsigned long long y0 = b0 < nblk ? d.blk_bytes[b0] : 0, y1 = b1 < nblk ? d.blk_bytes[b1] : 0;
+		cs[t] = c0 + c1;
+		bs[t] = y0 + y1;
 		__syncthreads();
-		cs[t] += a;
-		bs[t] += z;
-		__syncthreads();
+		for (uint32_t o = 1; o < 1024; o <<= 1) {
+			const unsigned long long a = t >= o ? cs[t - o] : 0, z = t >= o ? bs[t - o] : 0;
+			__syncthreads();
+			cs[t] += a;
+			bs[t] += z;
+			__syncthreads();
+		}
+		const unsigned long long ce = cs[t] - c0 - c1, be = bs[t] - y0 - y1; // exclusive prefix of the pair
+		if (b0 < nblk) {
+			d.blk_lbase[b0] = lbase + ce;
+			d.blk_abase[b0] = abase + be;
+		}
+		if (b1 < nblk) {
+			d.blk_lbase[b1] = lbase + ce + c0;
+			d.blk_abase[b1] = abase + be + y0;
+		}
+		lbase += cs[1023];
+		abase += bs[1023];
+		__syncthreads(); // cs and bs are rewritten by the next round
 	}
-	const unsigned long long lbase = d.ctr[CTR_SERVICES], abase = d.ctr[CTR_SARENA];
-	const unsigned long long ce = cs[t] - c0 - c1, be = bs[t] - y0 - y1; // exclusive prefix of the pair
-	if (b0 < nblk) {
-		d.blk_lbase[b0] = lbase + ce;
-		d.blk_abase[b0] = abase + be;
-	}
-	if (b1 < nblk) {
-		d.blk_lbase[b1] = lbase + ce + c0;
-		d.blk_abase[b1] = abase + be + y0;
-	}
-	__syncthreads();
 	if (t == 0) {
-		d.ctr[CTR_SERVICES] = lbase + cs[1023];
-		d.ctr[CTR_SARENA] = abase + bs[1023];
+		d.ctr[CTR_SERVICES] = lbase;
+		d.ctr[CTR_SARENA] = abase;
 	}
 }
 
@@ -3712,7 +4089,7 @@ __global__ void k_net_dump(Dev d, ebd_service_net* out, uint32_t cap, unsigned l
 // The slot of the service with key (lo, hi), kNone if the table has none (find only).
 __device__ uint32_t slot_find(const Dev& d, unsigned long long lo, unsigned long long hi) {
 	uint32_t idx = (uint32_t)lo & d.slot_mask;
-	for (uint32_t probe = 0; probe <= d.slot_mask; probe++) {
+	for (uint32_t probe = 0; probe <= d.probe_mask; probe++) {
 		Slot* s = d.slots + idx;
 		unsigned long long t = s->tag;
 		if (t == 0) // a plain load may see a stale line: the memory-side word decides
@@ -3726,7 +4103,7 @@ __device__ uint32_t slot_find(const Dev& d, unsigned long long lo, unsigned long
 			if (h == hi)
 				return idx;
 		}
-		idx = (idx + 1) & d.slot_mask;
+		idx = probe_next(d, idx);
 	}
 	return kNone;
 }
@@ -4448,12 +4825,29 @@ hipError_t launch_carry_pass(const Dev& d, hipStream_t st) {
 	hipLaunchKernelGGL(k_carry_pass, dim3(grid_for(d.n_carry_in, 64, 256)), dim3(64), 0, st, d, (const uint8_t*)nullptr);
 	return hipGetLastError();
 }
+uint32_t own_range_lg() { return kOwnLg; }
+// The owned aggregation for a batch (own_ctl and own_bcnt zeroed by the caller).
+hipError_t launch_own(const Dev& d, hipStream_t st, int cus) {
+	const uint32_t nranges = 1u << (d.own_abits + d.own_bbits);
+	const uint64_t tiles = ((uint64_t)d.n + kOwnTile - 1) / kOwnTile;
+	const int g = grid_for(tiles, 1, cus * 8);
+	const uint32_t btiles = (uint32_t)tiles + (1u << d.own_abits); // bucket tiles: at most one partial per bucket
+	hipLaunchKernelGGL(k_own_count, dim3(g), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_own_scan_a, dim3(1), dim3(64), 0, st, d);
+	hipLaunchKernelGGL(k_own_emit, dim3(g), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_own_bcount, dim3(btiles), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_own_scan_b, dim3(1), dim3(1024), 0, st, d);
+	hipLaunchKernelGGL(k_own_part, dim3(btiles), dim3(256), 0, st, d);
+	hipLaunchKernelGGL(k_own, dim3(nranges), dim3(256), 0, st, d);
+	return hipGetLastError();
+}
 hipError_t launch_agg_fast(const Dev& d, hipStream_t st, int cus) {
 	hipLaunchKernelGGL(k_agg_fast, dim3(agg_grid(d.n, cus)), dim3(kAggThreads), 0, st, d);
 	return hipGetLastError();
 }
-hipError_t launch_publish(const Dev& d, hipStream_t st, int cus) {
-	const uint32_t g = agg_grid(d.n, cus);
+// nblk: the claim stretches (0: k_agg_fast's grid)
+hipError_t launch_publish(const Dev& d, uint32_t nblk, hipStream_t st, int cus) {
+	const uint32_t g = nblk ? nblk : agg_grid(d.n, cus);
 	hipLaunchKernelGGL(k_pub_count, dim3(g), dim3(kPubThreads), 0, st, d);
 	hipLaunchKernelGGL(k_pub_scan, dim3(1), dim3(1024), 0, st, d, g);
 	hipLaunchKernelGGL(k_publish, dim3(g), dim3(kPubThreads), 0, st, d);
