@@ -454,12 +454,14 @@ struct DevMem {
 constexpr int kFreshThreads = EBD_FRESH_THREADS;
 constexpr int kFreshWaves = kFreshThreads / 64;
 #ifndef EBD_SCAN_WAVES
-#define EBD_SCAN_WAVES 11
+#define EBD_SCAN_WAVES 12
 #endif
 // waves [0, kScanWaves) scan; the others finalize.  The split balances the scan against the
 // finalize batches (which wait on the words past the staged bytes that the record does not
-// carry): with the grid windows, 11 + 5 take 2.84 ms per 20 M config-3 events against 3.03 for
-// 10 + 6, 3.20 for 9 + 7 and 3.14 for 12 + 4.
+// carry).  Round 5 (finalize also classified the source address): 11 + 5 took 2.84 ms per 20 M
+// config-3 events against 3.03 for 10 + 6, 3.20 for 9 + 7 and 3.14 for 12 + 4.  Round 6, with
+// the class moved to k_agg_fast: 12 + 4 2.69-2.72 ms against 2.84-2.86 for 11 + 5, 2.96 for
+// 10 + 6 and 3.10-3.16 for 13 + 3 (config 4's poll cycle: 5.13 against 5.04 ms).
 constexpr int kScanWaves = EBD_SCAN_WAVES;
 constexpr int kPfWaves = 0;
 constexpr int kFinWaves = kFreshWaves - kScanWaves - kPfWaves;
