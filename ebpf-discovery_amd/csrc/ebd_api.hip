@@ -1,7 +1,6 @@
 // ebd_api.hip — the C ABI (include/ebpf_discovery_amd.h): context, device buffers and the
 // per-batch pipeline of ebd_kernels.hip.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cerrno>
 #include <cstdio>
@@ -46,6 +45,14 @@ hipError_t launch_verify(const Dev& d, hipStream_t st, int cus);
 hipError_t launch_parse_streams(const KeyTrie* trie, ebd_parse_call* calls, uint32_t n, const uint8_t* data, hipStream_t st);
 hipError_t launch_publish(const Dev& d, uint32_t nblk, hipStream_t st, int cus);
 hipError_t launch_own(const Dev& d, hipStream_t st, int cus);
+// the library's own device-wide primitives (ebd_kernels.hip)
+size_t prim_sort_tmp_bytes(unsigned long long n);
+size_t prim_scan_tmp_bytes(unsigned long long n, size_t elem);
+hipError_t prim_scan_u32(const unsigned int* in, unsigned int* out, unsigned long long n, int incl, void* tmp, hipStream_t st);
+hipError_t prim_scan_u64(const unsigned long long* in, unsigned long long* out, unsigned long long n, int incl, void* tmp, hipStream_t st);
+hipError_t prim_sort_keys(unsigned long long* a, unsigned long long* b, unsigned long long n, uint32_t lo, uint32_t hi, void* tmp,
+		unsigned long long** sorted, hipStream_t st);
+hipError_t prim_select_keys(const unsigned long long* in, unsigned long long* out, unsigned long long n, int* cnt, void* tmp, hipStream_t st);
 uint32_t own_range_lg();
 uint32_t agg_stage_per_block(uint32_t n, int cus);
 hipError_t launch_slots_init(Slot* slots, uint32_t n, hipStream_t st);
@@ -405,10 +412,6 @@ static uint64_t ctx_now(const ebd_ctx* c) {
 #define EBD_SLOW_DENSE 4
 #endif
 // A session-path key of k_slow_collect (other events hold ~0).
-struct SlowKey {
-	__host__ __device__ bool operator()(unsigned long long k) const { return k != ~0ull; }
-};
-
 static void ctx_free(ebd_ctx* c) {
 	void* ptrs[] = {c->d_ownA, c->d_ownB, c->d_own_ctl, c->d_own_rid, c->d_own_sub, c->d_own_bcnt, c->d_own_boff, c->d_own_bcur, c->d_dfa, c->d_trie, c->d_ifs, c->d_gen, c->d_slots,
 			c->d_new_slots, c->d_cstage, c->d_blk, c->d_list_ep, c->d_list_pl, c->d_verify, c->d_sarena, c->d_res, c->d_keys,
@@ -617,11 +620,10 @@ int ebd_ctx_create(const ebd_config* cfg, ebd_ctx** out) {
 	CTX_TRY(hipMalloc(&c->d_slow[0], n * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_slow[1], n * sizeof(unsigned long long)));
 	CTX_TRY(hipMalloc(&c->d_pieces, n * sizeof(unsigned long long)));
-	CTX_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, c->sort_tmp_bytes, c->d_slow[0], c->d_slow[1], (int)n, 0, 64,
-			c->stream));
-	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes ? c->sort_tmp_bytes : 16));
-	CTX_TRY(hipcub::DeviceSelect::If(nullptr, c->sel_tmp_bytes, c->d_slow[0], c->d_slow[1], c->d_sel_cnt, (int)n, SlowKey{}, c->stream));
-	CTX_TRY(hipMalloc(&c->d_sel_tmp, c->sel_tmp_bytes ? c->sel_tmp_bytes : 16));
+	c->sort_tmp_bytes = prim_sort_tmp_bytes(n);
+	CTX_TRY(hipMalloc(&c->d_sort_tmp, c->sort_tmp_bytes));
+	c->sel_tmp_bytes = prim_scan_tmp_bytes(n, sizeof(unsigned int));
+	CTX_TRY(hipMalloc(&c->d_sel_tmp, c->sel_tmp_bytes));
 	CTX_TRY(hipMalloc(&c->d_sel_cnt, sizeof(int)));
 	// + 64: stream_copy3 reads a carried request's bytes up to 8 past their end
 	CTX_TRY(hipMalloc(&c->d_carry[0], (size_t)lru * sizeof(Carry) + 64));
@@ -908,22 +910,18 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 		// order and the (stable) radix sort needs only the group bits: 4 passes instead of 8.  When
 		// few events take the session path they are compacted first (order kept).
 		const bool dense = nslow * EBD_SLOW_DENSE >= n;
-		unsigned long long* sorted = dense ? c->d_slow[1] : c->d_slow[0];
+		unsigned long long* sorted = nullptr;
+		// the library's stable radix sort (prim_sort_keys, 8 bits per pass) and compaction
 		HIP_TRY(timed(c, KT_SORT, [&] {
-			size_t bytes = c->sort_tmp_bytes;
 			if (dense)
-				return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[0], c->d_slow[1], (int)n, 32, end_bit,
-						c->stream);
-			size_t sb = c->sel_tmp_bytes;
-			hipError_t e = hipcub::DeviceSelect::If(c->d_sel_tmp, sb, c->d_slow[0], c->d_slow[1], c->d_sel_cnt, (int)n, SlowKey{},
-					c->stream);
+				return prim_sort_keys(c->d_slow[0], c->d_slow[1], n, 32, (uint32_t)end_bit, c->d_sort_tmp, &sorted, c->stream);
+			hipError_t e = prim_select_keys(c->d_slow[0], c->d_slow[1], n, c->d_sel_cnt, c->d_sel_tmp, c->stream);
 			if (e != hipSuccess)
 				return e;
-			return hipcub::DeviceRadixSort::SortKeys(c->d_sort_tmp, bytes, c->d_slow[1], c->d_slow[0], (int)nslow, 32, end_bit,
-					c->stream);
+			return prim_sort_keys(c->d_slow[1], c->d_slow[0], nslow, 32, (uint32_t)end_bit, c->d_sort_tmp, &sorted, c->stream);
 		}));
 		d.slow_keys = sorted;
-		d.heads = (uint32_t*)(dense ? c->d_slow[0] : c->d_slow[1]); // the sort's input, free after it
+		d.heads = (uint32_t*)(sorted == c->d_slow[0] ? c->d_slow[1] : c->d_slow[0]); // the sort's other buffer, free after it
 		if (!c->d_hrec)
 			HIP_TRY(hipMalloc(&c->d_hrec, (size_t)c->max_events * sizeof(uint4)));
 		d.hrec = c->d_hrec;
@@ -936,8 +934,7 @@ static int run_batch(ebd_ctx* c, const EventRec* ev, const uint32_t* len, const 
 				HIP_TRY(hipMalloc(&c->d_lru_delta, nb * sizeof(int)));
 				HIP_TRY(hipMalloc(&c->d_lru_minus, nb));
 				HIP_TRY(hipMalloc(&c->d_lru_scan, nb * sizeof(int)));
-				HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, c->lru_tmp_bytes, c->d_lru_delta, c->d_lru_scan,
-						(int)c->max_events, c->stream));
+				c->lru_tmp_bytes = prim_scan_tmp_bytes(c->max_events, sizeof(int));
 				HIP_TRY(hipMalloc(&c->d_lru_tmp, c->lru_tmp_bytes + 16));
 			}
 			HIP_TRY(hipMemsetAsync(c->d_lru_delta, 0, (size_t)n * sizeof(int), c->stream));
@@ -1578,14 +1575,9 @@ struct ScratchScope {
 
 // offs = the exclusive scan of nb (n entries), its scratch from the call's scratch.
 static hipError_t excl_scan(ebd_ctx* c, const unsigned long long* nb, unsigned long long* offs, uint32_t n) {
-	hipError_t e;
-	size_t tb = 0;
-	if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, nb, offs, (int)n, c->stream)) != hipSuccess)
-		return e;
 	void* tmp = nullptr;
-	if ((e = scratch_get(c, tb + 16, &tmp)) != hipSuccess)
-		return e;
-	return hipcub::DeviceScan::ExclusiveSum(tmp, tb, nb, offs, (int)n, c->stream);
+	hipError_t e = scratch_get(c, prim_scan_tmp_bytes(n, sizeof(unsigned long long)), &tmp);
+	return e != hipSuccess ? e : prim_scan_u64(nb, offs, n, 0, tmp, c->stream);
 }
 
 // The exclusive scan of each wire record's endpoint bytes (k_wire_bytes) into offs; nb and offs
@@ -2057,15 +2049,13 @@ static int trace_device4(ebd_ctx* c, const ebd_trace_config* t, const GenOut* ou
 	HIP_TRY(scratch_get(c, n * 8 + 8, (void**)&alen));
 	HIP_TRY(scratch_get(c, n * 8 + 8, (void**)&boff));
 	HIP_TRY(launch_gen4_count(t->seed, J, cnt, c->stream));
-	size_t b1 = 0, b2 = 0;
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, cnt, st, (int)tasks, c->stream)); // wraps mod 2^32: differences stay exact
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, alen, boff, (int)(n + 1), c->stream));
+	const size_t b1 = prim_scan_tmp_bytes(tasks, 4), b2 = prim_scan_tmp_bytes(n + 1, 8);
 	void* tmp = nullptr;
 	HIP_TRY(scratch_get(c, (b1 > b2 ? b1 : b2) + 16, &tmp));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, cnt, st, (int)tasks, c->stream));
+	HIP_TRY(prim_scan_u32(cnt, st, tasks, 0, tmp, c->stream)); // wraps mod 2^32: differences stay exact
 	HIP_TRY(hipMemsetAsync(alen, 0, n * 8 + 8, c->stream));
 	HIP_TRY(launch_gen4_len(c->d_gen, t->seed, J, n, a, st, alen, c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, alen, boff, (int)(n + 1), c->stream));
+	HIP_TRY(prim_scan_u64(alen, boff, n + 1, 0, tmp, c->stream));
 	HIP_TRY(hipMemcpyAsync(c->h_small, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
 	const unsigned long long total = c->h_small[0];
@@ -2103,16 +2093,14 @@ static int trace_device(ebd_ctx* c, const ebd_trace_config* t, const GenOut* out
 	HIP_TRY(launch_gen_len(c->d_gen, cfg, t->seed, t->first, n, a, t->shard_count, t->shard_index, alen, keep, c->stream));
 	if (t->shard_count <= 1) // every candidate is kept (a kept event may be empty only here)
 		HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)keep, 1, n, c->stream));
-	size_t b1 = 0, b2 = 0;
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, alen, boff, (int)n + 1, c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, keep, pos, (int)n + 1, c->stream));
+	const size_t b1 = prim_scan_tmp_bytes((unsigned long long)n + 1, 8);
 	void* tmp = nullptr;
-	HIP_TRY(scratch_get(c, (b1 > b2 ? b1 : b2) + 16, &tmp));
+	HIP_TRY(scratch_get(c, b1 + 16, &tmp));
 	// the (n+1)-th entries become the totals
 	HIP_TRY(hipMemsetAsync(alen + n, 0, 8, c->stream));
 	HIP_TRY(hipMemsetAsync(keep + n, 0, 4, c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b1, alen, boff, (int)n + 1, c->stream));
-	HIP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, b2, keep, pos, (int)n + 1, c->stream));
+	HIP_TRY(prim_scan_u64(alen, boff, (unsigned long long)n + 1, 0, tmp, c->stream));
+	HIP_TRY(prim_scan_u32(keep, pos, (unsigned long long)n + 1, 0, tmp, c->stream));
 	HIP_TRY(hipMemcpyAsync(c->h_small, boff + n, 8, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipMemcpyAsync(c->h_small + 1, pos + n, 4, hipMemcpyDeviceToHost, c->stream));
 	HIP_TRY(hipStreamSynchronize(c->stream));
