@@ -3817,37 +3817,41 @@ __global__ __launch_bounds__(kPrimThreads) void k_sel_scatter(const unsigned lon
 		*cnt = (int)(bsum[blockIdx.x] + total);
 }
 
-// Radix sort: per tile of kPrimChunk keys, the counts of each digit, digit-major (cnt[d * ntiles + t]).
-// (Per-wave chunks of 1024 keys, which spare the scatter its count, took 4.79 against 3.51 ms per
-// 80 M-key sort: a scan four times longer.)
-__global__ __launch_bounds__(kPrimThreads) void k_rs_hist(const unsigned long long* in, unsigned long long n, uint32_t sh, uint32_t ntiles,
-		unsigned int* cnt) {
-	__shared__ unsigned int h[256];
-	h[threadIdx.x] = 0;
+// Radix sort: per tile of kPrimChunk keys, the counts of each digit, digit-major
+// (cnt[d * ntiles + t]).  Digits of up to kRsMaxBits bits: the passes split the sorted bits evenly
+// (the session keys' 27 group bits: 3 passes of 9 bits took less than 4 of 8).
+constexpr uint32_t kRsMaxBits = 10, kRsMaxBins = 1u << kRsMaxBits;
+__global__ __launch_bounds__(kPrimThreads) void k_rs_hist(const unsigned long long* in, unsigned long long n, uint32_t sh, uint32_t db,
+		uint32_t ntiles, unsigned int* cnt) {
+	__shared__ unsigned int h[kRsMaxBins];
+	const uint32_t nbin = 1u << db, m = nbin - 1u;
+	for (uint32_t x = threadIdx.x; x < nbin; x += kPrimThreads)
+		h[x] = 0;
 	__syncthreads();
 	const unsigned long long b = (unsigned long long)blockIdx.x * kPrimChunk;
 	for (uint32_t k = threadIdx.x; k < kPrimChunk; k += kPrimThreads)
 		if (b + k < n)
-			atomicAdd(&h[(uint32_t)(in[b + k] >> sh) & 0xffu], 1u);
+			atomicAdd(&h[(uint32_t)(in[b + k] >> sh) & m], 1u);
 	__syncthreads();
-	cnt[(unsigned long long)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
+	for (uint32_t x = threadIdx.x; x < nbin; x += kPrimThreads)
+		cnt[(unsigned long long)x * ntiles + blockIdx.x] = h[x];
 }
 
-// The tile's keys to their places: wave w takes the tile's w-th quarter in order, 64 keys at a time.
+// The tile's keys to their places: wave w takes the tile's w-th quarter in order, 64 keys at a time,
+// and ranks them among the wave's keys of the same digit with one ballot per digit bit.
 __global__ __launch_bounds__(kPrimThreads) void k_rs_scatter(const unsigned long long* in, unsigned long long* out, unsigned long long n,
-		uint32_t sh, uint32_t ntiles, const unsigned int* off) {
-	__shared__ unsigned int wh[kPrimThreads / 64][256];
-	const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+		uint32_t sh, uint32_t db, uint32_t ntiles, const unsigned int* off) {
+	__shared__ unsigned int wh[kPrimThreads / 64][kRsMaxBins];
+	const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, nbin = 1u << db, m = nbin - 1u;
 	const unsigned long long tb = (unsigned long long)blockIdx.x * kPrimChunk, q = kPrimChunk / (kPrimThreads / 64);
 	const unsigned long long b = tb + w * q, e = min(n, b + q);
-	for (uint32_t x = lane; x < 256; x += 64)
+	for (uint32_t x = lane; x < nbin; x += 64)
 		wh[w][x] = 0;
 	__syncthreads();
 	for (unsigned long long j = b + lane; j < e; j += 64)
-		atomicAdd(&wh[w][(uint32_t)(in[j] >> sh) & 0xffu], 1u);
+		atomicAdd(&wh[w][(uint32_t)(in[j] >> sh) & m], 1u);
 	__syncthreads();
-	{ // per digit: the tile's offset, then each wave's quarter after the earlier waves'
-		const uint32_t dg = threadIdx.x;
+	for (uint32_t dg = threadIdx.x; dg < nbin; dg += kPrimThreads) { // the tile's offset, then each wave's quarter after the earlier's
 		unsigned int s = off[(unsigned long long)dg * ntiles + blockIdx.x];
 		for (uint32_t k = 0; k < kPrimThreads / 64; k++) {
 			const unsigned int c = wh[k][dg];
@@ -3861,10 +3865,9 @@ __global__ __launch_bounds__(kPrimThreads) void k_rs_scatter(const unsigned long
 		const unsigned long long j = j0 + lane;
 		const bool valid = j < e;
 		const unsigned long long key = valid ? in[j] : 0ull;
-		const uint32_t dg = (uint32_t)(key >> sh) & 0xffu;
+		const uint32_t dg = (uint32_t)(key >> sh) & m;
 		unsigned long long peers = __ballot(valid);
-#pragma unroll
-		for (uint32_t bit = 0; bit < 8; bit++) {
+		for (uint32_t bit = 0; bit < db; bit++) {
 			const unsigned long long bb = __ballot((dg >> bit) & 1u);
 			peers &= ((dg >> bit) & 1u) ? bb : ~bb;
 		}
@@ -3883,19 +3886,21 @@ __global__ __launch_bounds__(kPrimThreads) void k_rs_scatter(const unsigned long
 static hipError_t prim_sort(unsigned long long* a, unsigned long long* b, unsigned long long n, uint32_t lo, uint32_t hi, void* tmp,
 		unsigned long long** sorted, hipStream_t st) {
 	*sorted = a;
-	if (n == 0)
+	if (n == 0 || hi <= lo)
 		return hipSuccess;
 	const uint32_t ntiles = (uint32_t)((n + kPrimChunk - 1) / kPrimChunk);
-	unsigned int* cnt = (unsigned int*)tmp;                              // 256 * ntiles
-	void* stmp = (void*)(cnt + 256ull * ntiles);                         // the scan's chunk totals
+	const uint32_t bits = hi - lo, passes = (bits + kRsMaxBits - 1) / kRsMaxBits, db = (bits + passes - 1) / passes;
+	unsigned int* cnt = (unsigned int*)tmp;                              // 2^db * ntiles
+	void* stmp = (void*)(cnt + ((unsigned long long)kRsMaxBins) * ntiles); // the scan's chunk totals
 	unsigned long long* src = a;
 	unsigned long long* dst = b;
-	for (uint32_t sh = lo; sh < hi; sh += 8) {
-		hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kPrimThreads), 0, st, src, n, sh, ntiles, cnt);
-		hipError_t e = prim_scan<unsigned int>(cnt, cnt, 256ull * ntiles, 0, stmp, st);
+	for (uint32_t sh = lo; sh < hi; sh += db) {
+		const uint32_t d = min(db, hi - sh);
+		hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(kPrimThreads), 0, st, src, n, sh, d, ntiles, cnt);
+		hipError_t e = prim_scan<unsigned int>(cnt, cnt, (unsigned long long)(1u << d) * ntiles, 0, stmp, st);
 		if (e != hipSuccess)
 			return e;
-		hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(kPrimThreads), 0, st, src, dst, n, sh, ntiles, (const unsigned int*)cnt);
+		hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(kPrimThreads), 0, st, src, dst, n, sh, d, ntiles, (const unsigned int*)cnt);
 		unsigned long long* t = src;
 		src = dst;
 		dst = t;
@@ -3906,7 +3911,7 @@ static hipError_t prim_sort(unsigned long long* a, unsigned long long* b, unsign
 
 // The scratch bytes prim_sort needs for n keys (and prim_scan for 256 * tiles elements).
 size_t prim_sort_tmp_bytes(unsigned long long n) {
-	const unsigned long long ntiles = (n + kPrimChunk - 1) / kPrimChunk, m = 256ull * ntiles;
+	const unsigned long long ntiles = (n + kPrimChunk - 1) / kPrimChunk, m = (unsigned long long)kRsMaxBins * ntiles;
 	return (size_t)(m * 4 + ((m + kPrimChunk - 1) / kPrimChunk) * 4 + 256);
 }
 size_t prim_scan_tmp_bytes(unsigned long long n, size_t elem) { return (size_t)(((n + kPrimChunk - 1) / kPrimChunk) * elem + 256); }
